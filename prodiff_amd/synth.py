@@ -1,0 +1,163 @@
+"""Seeded synthetic parameters and inputs shared by the golden-vector script,
+the parity tests and ``bench.py``.
+
+No pretrained checkpoint exists offline, so every parity
+fixture is produced with weights drawn here.  The draw is keyed by
+``(seed, crc32(parameter name))`` with numpy's PCG64 generator, which is
+bit-stable across machines, so the GPU box regenerates exactly the weights the
+reference saw in this container without any weight file travelling.
+
+Parameter names and shapes follow the reference state dicts:
+  * ``WaveNet``  -- modules/decoder/wavenet.py:74-99
+  * ``FastDiff`` -- modules/FastDiff/module/FastDiff_model.py:13-72 (weight-norm
+    form, ``weight_g``/``weight_v``, as the checkpoints store it:
+    component/vocoder/fastdiff.py:41)
+"""
+from __future__ import annotations
+
+import zlib
+from collections import OrderedDict
+
+import numpy as np
+
+
+# --------------------------------------------------------------------------
+# parameter name/shape tables
+# --------------------------------------------------------------------------
+def wavenet_param_shapes(in_dims=80, hidden_size=256, residual_layers=20,
+                         residual_channels=256):
+    """Ordered ``{state-dict key: shape}`` of reference ``WaveNet``."""
+    C, H, M = residual_channels, hidden_size, in_dims
+    s = OrderedDict()
+    s["input_projection.weight"] = (C, M, 1)
+    s["input_projection.bias"] = (C,)
+    s["mlp.0.weight"] = (4 * C, C)
+    s["mlp.0.bias"] = (4 * C,)
+    s["mlp.2.weight"] = (C, 4 * C)
+    s["mlp.2.bias"] = (C,)
+    for l in range(residual_layers):
+        p = f"residual_layers.{l}."
+        s[p + "dilated_conv.weight"] = (2 * C, C, 3)
+        s[p + "dilated_conv.bias"] = (2 * C,)
+        s[p + "diffusion_projection.weight"] = (C, C)
+        s[p + "diffusion_projection.bias"] = (C,)
+        s[p + "conditioner_projection.weight"] = (2 * C, H, 1)
+        s[p + "conditioner_projection.bias"] = (2 * C,)
+        s[p + "output_projection.weight"] = (2 * C, C, 1)
+        s[p + "output_projection.bias"] = (2 * C,)
+    s["skip_projection.weight"] = (C, C, 1)
+    s["skip_projection.bias"] = (C,)
+    s["output_projection.weight"] = (M, C, 1)
+    s["output_projection.bias"] = (M,)
+    return s
+
+
+KPNET_RES_IDX = (1, 3, 6, 8, 11, 13)   # Conv1d positions inside residual_conv (modules.py:297-313)
+
+
+def _wn(s, name, shape):
+    s[name + ".bias"] = (shape[0],)
+    s[name + ".weight_g"] = (shape[0], 1, 1)
+    s[name + ".weight_v"] = tuple(shape)
+
+
+def fastdiff_param_shapes(audio_channels=1, inner_channels=32, cond_channels=80,
+                          upsample_ratios=(8, 8, 4), lvc_layers_each_block=4,
+                          lvc_kernel_size=3, kpnet_hidden_channels=64,
+                          kpnet_conv_size=3, diffusion_step_embed_dim_in=128,
+                          diffusion_step_embed_dim_mid=512,
+                          diffusion_step_embed_dim_out=512, weight_norm=True):
+    """Ordered ``{state-dict key: shape}`` of reference ``FastDiff``.
+
+    With ``weight_norm`` every ``nn.Conv1d`` carries ``weight_g``/``weight_v``
+    (FastDiff_model.py:115-122); ``ConvTranspose1d`` and ``Linear`` do not.
+    """
+    Ci, Cc, Hk = inner_channels, cond_channels, kpnet_hidden_channels
+    Lyr, ks, kp = lvc_layers_each_block, lvc_kernel_size, kpnet_conv_size
+    s = OrderedDict()
+
+    def conv(name, shape):
+        if weight_norm:
+            _wn(s, name, shape)
+        else:
+            s[name + ".weight"] = tuple(shape)
+            s[name + ".bias"] = (shape[0],)
+
+    conv("first_audio_conv", (Ci, audio_channels, 7))
+    s["fc_t1.weight"] = (diffusion_step_embed_dim_mid, diffusion_step_embed_dim_in)
+    s["fc_t1.bias"] = (diffusion_step_embed_dim_mid,)
+    s["fc_t2.weight"] = (diffusion_step_embed_dim_out, diffusion_step_embed_dim_mid)
+    s["fc_t2.bias"] = (diffusion_step_embed_dim_out,)
+    nb = len(upsample_ratios)
+    for n in range(nb):
+        r = upsample_ratios[n]
+        p = f"lvc_blocks.{n}."
+        s[p + "upsample.weight"] = (Ci, Ci, 2 * r)
+        s[p + "upsample.bias"] = (Ci,)
+        conv(p + "kernel_predictor.input_conv.0", (Hk, Cc, 5))
+        for j in KPNET_RES_IDX:
+            conv(p + f"kernel_predictor.residual_conv.{j}", (Hk, Hk, kp))
+        conv(p + "kernel_predictor.kernel_conv", (Ci * 2 * Ci * ks * Lyr, Hk, kp))
+        conv(p + "kernel_predictor.bias_conv", (2 * Ci * Lyr, Hk, kp))
+        s[p + "fc_t.weight"] = (Cc, diffusion_step_embed_dim_out)
+        s[p + "fc_t.bias"] = (Cc,)
+        for i in range(Lyr):
+            conv(p + f"convs.{i}", (Ci, Ci, ks))
+    for n in range(nb):
+        p = f"downsample.{n}."
+        conv(p + "residual_dense", (Ci, Ci, 1))
+        for j in range(3):
+            conv(p + f"conv.{j}", (Ci, Ci, 3))
+    conv("final_conv.0", (audio_channels, Ci, 7))
+    return s
+
+
+# --------------------------------------------------------------------------
+# draws
+# --------------------------------------------------------------------------
+def _rng(seed, name):
+    return np.random.default_rng([int(seed), zlib.crc32(name.encode())])
+
+
+def _gain(name):
+    # the LVC kernels multiply 96 taps each; keep them from saturating the gate
+    if "kernel_conv" in name or "bias_conv" in name:
+        return 0.3
+    # a trained eps-network predicts ~N(0,1); keep the synthetic one there too
+    if "final_conv" in name:
+        return 0.2
+    return 1.0
+
+
+def synth_tensor(name, shape, seed):
+    """Deterministic float32 draw for one parameter."""
+    rng = _rng(seed, name)
+    z = rng.standard_normal(size=shape, dtype=np.float32)
+    if name.endswith(".bias"):
+        return (0.02 * z).astype(np.float32)
+    if name.endswith(".weight_g"):
+        return (_gain(name) * (1.0 + 0.1 * z)).astype(np.float32)
+    if name.endswith(".weight_v"):
+        return z
+    if "upsample" in name:            # ConvTranspose1d [Cin, Cout, k]: 2 taps hit each output
+        fan_in = shape[0] * 2
+    else:
+        fan_in = int(np.prod(shape[1:]))
+    return (z * (_gain(name) / np.sqrt(fan_in))).astype(np.float32)
+
+
+def synth_params(shapes, seed):
+    return OrderedDict((k, synth_tensor(k, v, seed)) for k, v in shapes.items())
+
+
+def fold_weight_norm_np(g, v):
+    """w = g * v / ||v|| with the norm over every dim but 0 (torch.nn.utils.weight_norm, dim=0)."""
+    n = np.sqrt(np.sum(v.astype(np.float64) ** 2, axis=tuple(range(1, v.ndim)), keepdims=True))
+    return (g.astype(np.float64) * v / n).astype(np.float32)
+
+
+def synth_inputs(seed, shape, kind="normal", loc=0.0, scale=1.0):
+    rng = np.random.default_rng([int(seed), 0xC0FFEE])
+    if kind == "uniform":
+        return rng.random(size=shape, dtype=np.float32)
+    return (loc + scale * rng.standard_normal(size=shape, dtype=np.float32)).astype(np.float32)

@@ -1,0 +1,277 @@
+"""Generate the golden parity vectors from the REFERENCE PyTorch code.
+
+Runs only in the survey container, where ``/root/reference`` exists:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+The reference is imported read-only with the shims SURVEY.md §8(c) lists
+(lower-case ``modules.fastdiff`` alias for FastDiff_model.py:4-5, and
+``Tensor.cuda`` as identity for the hard-coded ``.cuda()`` in util.py:68,214,424).
+Weights are drawn by ``prodiff_amd.synth`` (keyed by parameter name), so only
+inputs/outputs are stored; the GPU box regenerates the same weights.
+Every random draw the reference makes (``torch.rand``/``torch.randn`` in
+prodiff.py:118,147, ``std_normal`` in util.py:208,226) is replaced by a seeded
+draw and recorded (cloned: util.py:223-224 mutates x in place).
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+sys.path.insert(0, REF)
+
+from prodiff_amd import synth  # noqa: E402
+
+torch.Tensor.cuda = lambda self, *a, **k: self          # shim (util.py:68,214,424)
+torch.set_num_threads(8)
+
+from modules.decoder.wavenet import WaveNet            # noqa: E402
+from modules.diffusion.prodiff import GaussianDiffusion  # noqa: E402
+import modules.FastDiff                                # noqa: E402
+import modules.FastDiff.module                         # noqa: E402
+import modules.FastDiff.module.modules as fd_modules   # noqa: E402
+import modules.FastDiff.module.util as fd_util         # noqa: E402
+sys.modules["modules.fastdiff"] = modules.FastDiff
+sys.modules["modules.fastdiff.module"] = modules.FastDiff.module
+sys.modules["modules.fastdiff.module.modules"] = fd_modules
+sys.modules["modules.fastdiff.module.util"] = fd_util
+from modules.FastDiff.module.FastDiff_model import FastDiff  # noqa: E402
+
+OUT = HERE
+FASTDIFF_SCHEDULES = {   # component/vocoder/fastdiff.py:62-73
+    3: [9.0000e-05, 9.0000e-03, 6.0000e-01],
+    4: [3.2176e-04, 2.5743e-03, 2.5376e-02, 7.0414e-01],
+    6: [1.7838445955931093e-06, 2.7984189728158526e-05, 0.00043231004383414984,
+        0.006634317338466644, 0.09357017278671265, 0.6000000238418579],
+    8: [6.689325005027058e-07, 1.0033881153503899e-05, 0.00015496854030061513,
+        0.002387222135439515, 0.035597629845142365, 0.3681158423423767, 0.4735414385795593, 0.5],
+}
+
+
+def load_synth(model, shapes, seed):
+    sd = model.state_dict()
+    params = synth.synth_params(shapes, seed)
+    assert set(params) <= set(sd), set(params) - set(sd)
+    missing = [k for k in sd if k not in params]
+    assert all(k in ("spec_min", "spec_max") or "timesteps" in k or "timescale" in k
+               or k.startswith(("betas", "alphas", "sqrt", "log_", "posterior"))
+               for k in missing), missing
+    for k, v in params.items():
+        assert tuple(sd[k].shape) == tuple(v.shape), (k, sd[k].shape, v.shape)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    return params
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print(f"  wrote {name}.npz  ({os.path.getsize(path) / 1024:.0f} KiB)")
+
+
+# --------------------------------------------------------------------------
+# WaveNet denoiser (wavenet.py:74-123)
+# --------------------------------------------------------------------------
+WAVENET_CASES = {
+    # name: (in_dims, hidden, layers, channels, cycle, B, T, seed, steps)
+    "wavenet_m80_c256_l20_cyc1": (80, 256, 20, 256, 1, 2, 48, 11, [0, 1]),
+    "wavenet_m80_c256_l20_float": (80, 256, 20, 256, 1, 2, 48, 11, [537.5, 12.25]),
+    "wavenet_m64_c256_l20_cyc5": (64, 256, 20, 256, 5, 2, 64, 12, [3, 900]),
+    "wavenet_m128_c256_l20_cyc1": (128, 256, 20, 256, 1, 1, 37, 13, [2]),
+    "wavenet_m80_c64_l4_cyc2": (80, 32, 4, 64, 2, 3, 29, 14, [0, 1, 3]),
+}
+
+
+def gen_wavenet():
+    for name, (M, H, L, C, cyc, B, T, seed, steps) in WAVENET_CASES.items():
+        net = WaveNet(M, H, L, C, cyc).eval()
+        load_synth(net, synth.wavenet_param_shapes(M, H, L, C), seed)
+        spec = synth.synth_inputs(seed + 100, (B, 1, M, T))
+        cond = synth.synth_inputs(seed + 200, (B, H, T))
+        is_float = any(isinstance(s, float) for s in steps)
+        st = torch.tensor(steps, dtype=torch.float32 if is_float else torch.long)
+        with torch.no_grad():
+            out = net(torch.from_numpy(spec), st, torch.from_numpy(cond)).numpy()
+        save(name, dims=np.array([M, H, L, C, cyc]), seed=seed, spec=spec, cond=cond,
+             steps=np.array(steps, dtype=np.float32), out=out)
+
+
+# --------------------------------------------------------------------------
+# ProDiff sampler (prodiff.py:48-153)
+# --------------------------------------------------------------------------
+class Recorder:
+    """Replace torch.rand / torch.randn with seeded draws and record them."""
+
+    def __init__(self, seed):
+        self.seed = seed
+        self.n = 0
+        self.rand = []
+        self.randn = []
+
+    def __enter__(self):
+        self._r, self._rn = torch.rand, torch.randn
+
+        def rand(*size, device=None, **kw):
+            a = synth.synth_inputs(self.seed * 1000 + self.n, tuple(size), kind="uniform")
+            self.n += 1
+            self.rand.append(a.copy())
+            return torch.from_numpy(a)
+
+        def randn(size, device=None, **kw):
+            a = synth.synth_inputs(self.seed * 1000 + self.n, tuple(size))
+            self.n += 1
+            self.randn.append(a.copy())
+            return torch.from_numpy(a)
+
+        torch.rand, torch.randn = rand, randn
+        return self
+
+    def __exit__(self, *a):
+        torch.rand, torch.randn = self._r, self._rn
+
+
+PRODIFF_CASES = {
+    # name: (timesteps, max_beta, M, B, T, seed)
+    "prodiff_t2_m80": (2, 40.0, 80, 2, 40, 21),     # C2-shape sampler (2-iter)
+    "prodiff_t4_m80": (4, 40.0, 80, 1, 33, 22),     # C1-shape teacher (4-iter)
+    "prodiff_t4_m128": (4, 40.0, 128, 2, 24, 23),   # C5-shape (SVS, 128 mel bins)
+}
+
+
+def gen_prodiff():
+    for name, (ts, mb, M, B, T, seed) in PRODIFF_CASES.items():
+        H, L, C = 256, 20, 256
+        net = WaveNet(M, H, L, C, 1)
+        gd = GaussianDiffusion(out_dims=M, denoise_fn=net, timesteps=ts, time_scale=1000,
+                               schedule_type="vpsde", max_beta=mb,
+                               spec_min=[-12], spec_max=[0]).eval()
+        load_synth(net, synth.wavenet_param_shapes(M, H, L, C), seed)
+        cond = synth.synth_inputs(seed + 300, (B, T, H))
+        with torch.no_grad(), Recorder(seed) as rec:
+            mel = gd(torch.from_numpy(cond), infer=True).numpy()
+        assert len(rec.rand) == 1 and len(rec.randn) == min(4, ts)
+        bufs = {k: v.numpy() for k, v in gd.state_dict().items() if not k.startswith("denoise_fn")}
+        save(name, timesteps=ts, max_beta=mb, seed=seed, cond=cond, x_T=rec.rand[0],
+             noise=np.stack(rec.randn), mel=mel, **{"buf_" + k: v for k, v in bufs.items()})
+
+
+def gen_schedules():
+    out = {}
+    for ts in (1, 2, 4, 8, 100):
+        for mb in (40.0, 0.06):
+            gd = GaussianDiffusion(out_dims=4, denoise_fn=None, timesteps=ts, max_beta=mb,
+                                   spec_min=[-12], spec_max=[0])
+            for k, v in gd.state_dict().items():
+                out[f"t{ts}_mb{mb}_{k}"] = v.numpy()
+    # FastDiff: training linear schedule (fastdiff.py:44-51) and the reverse
+    # schedules (fastdiff.py:62-73) mapped to fractional steps (util.py:187-206)
+    beta = torch.linspace(1e-6, 0.01, 1000)
+    dh = fd_util.compute_hyperparams_given_schedule(beta)
+    out["fd_train_alpha"] = dh["alpha"].numpy()
+    out["fd_train_sigma"] = dh["sigma"].numpy()
+    for n, sched in FASTDIFF_SCHEDULES.items():
+        b = torch.FloatTensor(sched)
+        a = 1 - b
+        sg = b + 0
+        for i in range(1, len(b)):
+            a[i] *= a[i - 1]
+            sg[i] *= (1 - a[i - 1]) / (1 - a[i])
+        a, sg = torch.sqrt(a), torch.sqrt(sg)
+        steps = [fd_util.map_noise_scale_to_time_step(a[i], dh["alpha"]) for i in range(len(b))]
+        out[f"fd_n{n}_beta"] = b.numpy()
+        out[f"fd_n{n}_alpha"] = a.numpy()
+        out[f"fd_n{n}_sigma"] = sg.numpy()
+        out[f"fd_n{n}_steps"] = np.array(steps, dtype=np.float32)
+    save("schedules", **out)
+
+
+# --------------------------------------------------------------------------
+# FastDiff network (FastDiff_model.py:74-102) and sampler (util.py:158-232)
+# --------------------------------------------------------------------------
+def build_fastdiff(seed):
+    m = FastDiff()           # base.yaml defaults, weight norm on (FastDiff_model.py:70-71)
+    params = load_synth(m, synth.fastdiff_param_shapes(), seed)
+    m.remove_weight_norm()   # fastdiff.py:82
+    return m.eval(), params
+
+
+def gen_fastdiff():
+    seed = 31
+    m, _ = build_fastdiff(seed)
+    B, Tc = 2, 8
+    L = Tc * 256
+    audio = synth.synth_inputs(seed + 1, (B, 1, L))
+    c = synth.synth_inputs(seed + 2, (B, 80, Tc), loc=-5.0, scale=2.0)
+    steps = np.array([[7.41324], [498.054]], dtype=np.float32)
+    caps = {}
+
+    def hook(name):
+        def f(mod, inp, out):
+            if isinstance(out, tuple):
+                for i, o in enumerate(out):
+                    caps[f"{name}.out{i}"] = o.detach().numpy().copy()
+            else:
+                caps[name] = out.detach().numpy().copy()
+        return f
+
+    hs = [m.first_audio_conv.register_forward_hook(hook("first_audio_conv"))]
+    for n in range(3):
+        hs.append(m.downsample[n].register_forward_hook(hook(f"downsample{n}")))
+        hs.append(m.lvc_blocks[n].register_forward_hook(hook(f"lvc{n}")))
+        hs.append(m.lvc_blocks[n].upsample.register_forward_hook(hook(f"upsample{n}")))
+        hs.append(m.lvc_blocks[n].kernel_predictor.register_forward_hook(hook(f"kp{n}")))
+    with torch.no_grad():
+        eps = m((torch.from_numpy(audio), torch.from_numpy(c), torch.from_numpy(steps))).numpy()
+    for h in hs:
+        h.remove()
+    keep = {k: v for k, v in caps.items() if not k.startswith("kp")}
+    keep["kp0_kernels_b0"] = caps["kp0.out0"][0]          # [4,32,64,3,T'] of batch 0
+    keep["kp2_bias"] = caps["kp2.out1"]
+    keep["kp1_kernels_b1_f3"] = caps["kp1.out0"][1, ..., 3]
+    save("fastdiff_fwd", seed=seed, audio=audio, c=c, steps=steps, eps=eps,
+         **{"cap_" + k: v for k, v in keep.items()})
+
+    # sampler, 4-iter and 3-iter schedules
+    for n_iter, (B, Tc, seed_s) in {4: (2, 6, 41), 3: (1, 5, 42)}.items():
+        L = Tc * 256
+        c = synth.synth_inputs(seed_s + 2, (B, 80, Tc), loc=-5.0, scale=2.0)
+        dh = fd_util.compute_hyperparams_given_schedule(torch.linspace(1e-6, 0.01, 1000))
+        sched = torch.FloatTensor(FASTDIFF_SCHEDULES[n_iter])
+        draws, seen_steps = [], []
+        cnt = [0]
+
+        def std_normal(size):
+            a = synth.synth_inputs(seed_s * 1000 + cnt[0], tuple(size))
+            cnt[0] += 1
+            draws.append(a.copy())
+            return torch.from_numpy(a)
+
+        class Spy(torch.nn.Module):
+            def forward(self, data):
+                seen_steps.append(data[2][0, 0].item())
+                return m(data)
+
+        orig = fd_util.std_normal
+        fd_util.std_normal = std_normal
+        try:
+            with torch.no_grad():
+                wav = fd_util.sampling_given_noise_schedule(
+                    Spy(), (B, 1, L), dh, sched, condition=torch.from_numpy(c)).numpy()
+        finally:
+            fd_util.std_normal = orig
+        assert len(draws) == n_iter
+        save(f"fastdiff_sample_n{n_iter}", seed=seed, c=c, x_T=draws[0],
+             noise=np.stack(draws[1:]), steps_seen=np.array(seen_steps, dtype=np.float32),
+             wav=wav)
+
+
+if __name__ == "__main__":
+    gen_schedules()
+    gen_wavenet()
+    gen_prodiff()
+    gen_fastdiff()

@@ -1,0 +1,34 @@
+"""Helpers to load the committed golden vectors and regenerate their weights."""
+import os
+
+import numpy as np
+
+from prodiff_amd import synth
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz")) as d:
+        return {k: d[k] for k in d.files}
+
+
+def wavenet_params(dims, seed):
+    M, H, L, C, _ = [int(v) for v in dims]
+    return synth.synth_params(synth.wavenet_param_shapes(M, H, L, C), int(seed))
+
+
+def fastdiff_params(seed):
+    return synth.synth_params(synth.fastdiff_param_shapes(), int(seed))
+
+
+PRODIFF_SEEDS = {"prodiff_t2_m80": (80, 21), "prodiff_t4_m80": (80, 22), "prodiff_t4_m128": (128, 23)}
+
+
+def prodiff_params(name):
+    M, seed = PRODIFF_SEEDS[name]
+    return synth.synth_params(synth.wavenet_param_shapes(M, 256, 20, 256), seed)
+
+
+def prodiff_buffers(d):
+    return {k[4:]: v for k, v in d.items() if k.startswith("buf_")}

@@ -1,0 +1,99 @@
+"""The oracle (CPU restatement) against the reference's own outputs.
+
+The golden vectors were produced by running the reference PyTorch code
+(tests/golden/gen_golden.py); matching them pins the oracle before it is used
+to check the HIP path at other sizes.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle_fastdiff as OF
+from oracle import oracle_prodiff as OP
+from tests import golden_io as G
+
+WAVENET = ["wavenet_m80_c256_l20_cyc1", "wavenet_m80_c256_l20_float",
+           "wavenet_m64_c256_l20_cyc5", "wavenet_m128_c256_l20_cyc1", "wavenet_m80_c64_l4_cyc2"]
+
+
+@pytest.mark.parametrize("name", WAVENET)
+def test_wavenet_oracle(name):
+    d = G.load(name)
+    p = G.wavenet_params(d["dims"], d["seed"])
+    L, cyc = int(d["dims"][2]), int(d["dims"][4])
+    out = OP.wavenet_forward(p, d["spec"], d["steps"], d["cond"], L, cyc)
+    assert np.abs(out - d["out"]).max() < 2e-5
+
+
+def test_prodiff_schedule():
+    s = G.load("schedules")
+    for ts in (1, 2, 4, 8, 100):
+        for mb in (40.0, 0.06):
+            bufs = OP.diffusion_buffers(OP.vpsde_betas(ts, mb))
+            for k, v in bufs.items():
+                ref = s[f"t{ts}_mb{mb}_{k}"]
+                np.testing.assert_allclose(v, ref, rtol=1e-6, atol=0, err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["prodiff_t2_m80", "prodiff_t4_m80", "prodiff_t4_m128"])
+def test_prodiff_sample_oracle(name):
+    d = G.load(name)
+    p = G.prodiff_params(name)
+    bufs = G.prodiff_buffers(d)
+    mel = OP.prodiff_sample(p, bufs, d["cond"], d["x_T"], d["noise"])
+    assert mel.shape == d["mel"].shape
+    assert np.abs(mel - d["mel"]).max() < 2e-5
+
+
+def test_fastdiff_schedules():
+    s = G.load("schedules")
+    at = OF.train_alpha()
+    np.testing.assert_allclose(at, s["fd_train_alpha"], rtol=0, atol=1e-7)
+    for n in (3, 4, 6, 8):
+        b, a, sg, st = OF.infer_schedule(s[f"fd_n{n}_beta"], s["fd_train_alpha"])
+        np.testing.assert_allclose(a, s[f"fd_n{n}_alpha"], rtol=1e-6)
+        np.testing.assert_allclose(sg, s[f"fd_n{n}_sigma"], rtol=1e-6)
+        np.testing.assert_allclose(st, s[f"fd_n{n}_steps"], rtol=0, atol=1e-3)
+
+
+@pytest.fixture(scope="module")
+def fd():
+    d = G.load("fastdiff_fwd")
+    p = OF.fold_weight_norm(G.fastdiff_params(d["seed"]))
+    return d, p
+
+
+def test_fastdiff_forward_oracle(fd):
+    d, p = fd
+    cap = {}
+    eps = OF.fastdiff_forward(p, d["audio"], d["c"], d["steps"], capture=cap)
+    for n in range(3):
+        np.testing.assert_allclose(cap[f"downsample{n}"], d[f"cap_downsample{n}"], atol=2e-5, rtol=0)
+        # block outputs reach |x|~30; the fp32 reference itself drifts ~5e-6 relative there
+        ref = d[f"cap_lvc{n}"]
+        assert np.abs(cap[f"lvc{n}"] - ref).max() < 1e-5 * np.abs(ref).max()
+    assert np.abs(eps - d["eps"]).max() < 2e-5
+
+
+def test_fastdiff_ops_oracle(fd):
+    d, p = fd
+    e = OF.step_embedding(d["steps"])
+    e = OF.swish(OF.linear(e, p["fc_t1.weight"], p["fc_t1.bias"]))
+    e = OF.swish(OF.linear(e, p["fc_t2.weight"], p["fc_t2.bias"]))
+    q = "lvc_blocks.0."
+    noise = OF.linear(e, p[q + "fc_t.weight"], p[q + "fc_t.bias"])[:, :, None]
+    k, b = OF.kernel_predictor(p, q + "kernel_predictor.", d["c"] + noise)
+    np.testing.assert_allclose(k[0], d["cap_kp0_kernels_b0"], atol=2e-5, rtol=0)
+    x = OF.lrelu(d["cap_downsample2"], 0.2)
+    up = OF.conv_transpose1d(x, p[q + "upsample.weight"], p[q + "upsample.bias"], 8, 4, 0)
+    np.testing.assert_allclose(up, d["cap_upsample0"], atol=2e-5, rtol=0)
+
+
+@pytest.mark.parametrize("n_iter", [4, 3])
+def test_fastdiff_sample_oracle(n_iter):
+    d = G.load(f"fastdiff_sample_n{n_iter}")
+    s = G.load("schedules")
+    p = OF.fold_weight_norm(G.fastdiff_params(31))
+    b, a, sg, st = OF.infer_schedule(s[f"fd_n{n_iter}_beta"], s["fd_train_alpha"])
+    np.testing.assert_allclose(st[::-1], d["steps_seen"], atol=1e-4)
+    wav = OF.fastdiff_sample(p, d["c"], d["x_T"], d["noise"], b, a, sg, st)
+    assert np.abs(wav - d["wav"]).max() < 1e-4
