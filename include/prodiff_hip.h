@@ -1,0 +1,162 @@
+/*
+ * prodiff_hip.h -- C-ABI of libprodiff_hip.so, the MI355X (gfx950) ProDiff/FastDiff
+ * inference hot path.
+ *
+ * Conventions
+ *  - Every tensor pointer is a caller-owned DEVICE buffer (e.g. torch.cuda tensors),
+ *    float32, contiguous, 16-byte aligned.  Host pointers appear only where a
+ *    parameter is documented as "host" (per-step scalars).
+ *  - Calls are asynchronous and stream-ordered on `stream` (a hipStream_t; NULL =
+ *    the default stream).  Nothing allocates or synchronises inside forward/sample
+ *    calls, so they can be captured into a hipGraph.  Scratch memory is passed in
+ *    (`workspace`, at least *_workspace_size() bytes).
+ *  - Handles are immutable after create; concurrent calls on different streams
+ *    need separate workspaces.
+ *  - Return 0 (PD_OK) or an error code; pd_last_error() gives a thread-local text.
+ *    Argument checks mirror the reference's assert points (e.g. the LVC length
+ *    check, modules/FastDiff/module/modules.py:236).
+ *  - Layouts: "time-major" = [batch][time][channel] (channels contiguous), the
+ *    layout ProDiff's condition/mel already have at the sampler boundary
+ *    (prodiff.py:136-138 receives cond [B,T,H]; :151 returns mel [B,T,M]).
+ *    "channel-major" = PyTorch Conv1d layout [batch][channel][time].
+ */
+#ifndef PRODIFF_HIP_H
+#define PRODIFF_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PD_OK 0
+#define PD_ERR_ARG 1
+#define PD_ERR_HIP 2
+#define PD_ERR_WORKSPACE 3
+#define PD_ERR_UNSUPPORTED 4
+
+#define PD_DTYPE_F32 0
+#define PD_DTYPE_BF16 1
+
+const char* pd_last_error(void);
+int pd_version(void);
+
+/* ===================================================================== ProDiff
+ * WaveNet denoiser -- replaces modules/decoder/wavenet.py:74-123 (WaveNet) as the
+ * `denoise_fn` of GaussianDiffusion (modules/diffusion/prodiff.py:49-54,125).
+ */
+typedef struct pd_wavenet pd_wavenet;
+
+typedef struct {
+  int in_dims;               /* M: mel bins (80 LJSpeech, 128 SVS)          wavenet.py:75 */
+  int hidden_size;           /* H: condition channels (encoder_hidden)                   */
+  int residual_layers;       /* L: 20 (handler/base_config.yaml:210)                     */
+  int residual_channels;     /* C: 256 (base_config.yaml:211), multiple of 32            */
+  int dilation_cycle_length; /* dilation 2^(l % cycle) (wavenet.py:93-96)                */
+} pd_wavenet_dims;
+
+/* Parameter order = the reference state-dict order (wavenet.py:84-99), all float32
+ * in their PyTorch shapes:
+ *   input_projection.{weight[C,M,1],bias[C]}, mlp.0.{weight[4C,C],bias},
+ *   mlp.2.{weight[C,4C],bias},
+ *   for l < L: residual_layers.l.{dilated_conv.weight[2C,C,3], dilated_conv.bias,
+ *              diffusion_projection.weight[C,C], diffusion_projection.bias,
+ *              conditioner_projection.weight[2C,H,1], conditioner_projection.bias,
+ *              output_projection.weight[2C,C,1], output_projection.bias},
+ *   skip_projection.{weight[C,C,1],bias}, output_projection.{weight[M,C,1],bias}. */
+#define PD_WAVENET_NUM_PARAMS(L) (6 + 8 * (L) + 4)
+
+/* Packs the weights into the kernels' layouts (device-to-device, on `stream`). */
+int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, int dtype,
+                      void* stream, pd_wavenet** out);
+void pd_wavenet_destroy(pd_wavenet* h);
+/* S = number of reverse steps the workspace must serve (1 for pd_wavenet_forward). */
+size_t pd_wavenet_workspace_size(const pd_wavenet* h, int B, int T, int S);
+
+/* One denoiser call, reference signature WaveNet.forward(spec, diffusion_step, cond)
+ * (wavenet.py:100-123):
+ *   spec  [B,1,M,T] channel-major, steps [B] (float; integer steps as floats),
+ *   cond  [B,H,T] channel-major  ->  out [B,1,M,T]. */
+int pd_wavenet_forward(const pd_wavenet* h, const float* spec, const float* steps,
+                       const float* cond, float* out, int B, int T, void* workspace,
+                       size_t ws_bytes, void* stream);
+
+/* The whole x0-predict reverse sampler, GaussianDiffusion.forward(cond, infer=True)
+ * (prodiff.py:136-153) for S = clip(infer_step, 1, timesteps) steps:
+ *   x ~ U[0,1); for i = S-1..0: x0 = WaveNet(x, i, cond);
+ *   x = coef1[i]*x0 + coef2[i]*x + [i>0]*sigma[i]*n_i
+ * with coef1/coef2 = posterior_mean_coef1/2 and sigma = exp(0.5*posterior_log_variance_clipped)
+ * (host arrays of length >= S, taken from the checkpoint buffers).
+ *   cond  [B,T,H] time-major (as the teacher hands it, prodiff_teacher.py:167)
+ *   x_T   [B,T,M] time-major draw, or NULL -> Philox U[0,1) from `seed`
+ *   noise [S][B,T,M] time-major draws (pass j uses noise[j]), or NULL -> Philox N(0,1)
+ *   mel   [B,T,M] output (the reference's x[:,0].transpose(1,2), prodiff.py:151). */
+int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1,
+                      const float* coef2, const float* sigma, int S, const float* x_T,
+                      const float* noise, unsigned long long seed, float* mel, int B, int T,
+                      void* workspace, size_t ws_bytes, void* stream);
+
+/* ==================================================================== FastDiff
+ * eps-network -- replaces modules/FastDiff/module/FastDiff_model.py:10-102 (FastDiff)
+ * and the sampler util.py:158-232 (sampling_given_noise_schedule, ddim=False).
+ */
+typedef struct fd_model fd_model;
+
+typedef struct {
+  int audio_channels;        /* 1    (modules/FastDiff/config/base.yaml:20) */
+  int inner_channels;        /* 32   */
+  int cond_channels;         /* 80   */
+  int num_blocks;            /* len(upsample_ratios) = 3 */
+  int upsample_ratios[4];    /* 8, 8, 4 (hop 256) */
+  int lvc_layers_each_block; /* 4    */
+  int lvc_kernel_size;       /* 3    */
+  int kpnet_hidden_channels; /* 64   */
+  int kpnet_conv_size;       /* 3    */
+  int step_embed_in;         /* 128  */
+  int step_embed_mid;        /* 512  */
+  int step_embed_out;        /* 512  */
+} fd_dims;
+
+/* Parameter order (weight-norm already folded, w = g*v/||v||, FastDiff_model.py:104-113;
+ * fd_fold_weight_norm does it on device): for every Conv1d "weight" then "bias":
+ *   first_audio_conv, fc_t1.{weight,bias}, fc_t2.{weight,bias},
+ *   for n < num_blocks (lvc_blocks.n): upsample.{weight[32,32,2r],bias},
+ *       kernel_predictor.input_conv.0, kernel_predictor.residual_conv.{1,3,6,8,11,13},
+ *       kernel_predictor.kernel_conv, kernel_predictor.bias_conv, fc_t.{weight,bias},
+ *       convs.{0..3},
+ *   for n < num_blocks (downsample.n): residual_dense, conv.{0,1,2},
+ *   final_conv.0. */
+#define FD_NUM_PARAMS(nb) (2 + 4 + 30 * (nb) + 8 * (nb) + 2)
+
+int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* stream,
+              fd_model** out);
+void fd_destroy(fd_model* m);
+int fd_hop(const fd_model* m);   /* prod(upsample_ratios) = samples per mel frame */
+size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
+
+/* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */
+int fd_fold_weight_norm(float* w, const float* g, const float* v, int cout, int per_row,
+                        void* stream);
+
+/* One network call, reference net((audio, c, steps)) (FastDiff_model.py:74-102):
+ *   audio [B,1,L] (L = Tc*hop), cond [B,80,Tc] channel-major, steps [B] float
+ *   -> eps [B,1,L]. */
+int fd_forward(const fd_model* m, const float* audio, const float* cond, const float* steps,
+               float* eps, int B, int Tc, void* workspace, size_t ws_bytes, void* stream);
+
+/* sampling_given_noise_schedule(net, (B,1,L), dh, schedule, condition) (util.py:158-232):
+ *   x ~ N(0,1); for n = N-1..0: x = (x - beta[n]/sqrt(1-alpha[n]^2) eps(x,c,steps[n]))
+ *                                     / sqrt(1-beta[n]) + [n>0] sigma[n] z
+ *   mel   [B,Tc,80] time-major (the ProDiff sampler's output, no transpose needed)
+ *   beta/alpha/sigma/steps: host arrays of length N (util.py:181-206)
+ *   x_T   [B,L] draw or NULL -> Philox N(0,1); noise [N-1][B,L] (pass j uses noise[j])
+ *   or NULL -> Philox;  wav [B,L] output. */
+int fd_sample(const fd_model* m, const float* mel, const float* beta, const float* alpha,
+              const float* sigma, const float* steps, int N, const float* x_T,
+              const float* noise, unsigned long long seed, float* wav, int B, int Tc,
+              void* workspace, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRODIFF_HIP_H */

@@ -1,0 +1,116 @@
+"""ctypes binding of libprodiff_hip.so (the C-ABI declared in include/prodiff_hip.h).
+
+The product path has no CPU fallback: if the library is missing or fails to
+load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PRODIFF_HIP_LIB", os.path.join(_HERE, "libprodiff_hip.so"))
+
+PD_DTYPE_F32 = 0
+PD_DTYPE_BF16 = 1
+
+
+class HipError(RuntimeError):
+    pass
+
+
+class pd_wavenet_dims(C.Structure):
+    _fields_ = [("in_dims", C.c_int), ("hidden_size", C.c_int), ("residual_layers", C.c_int),
+                ("residual_channels", C.c_int), ("dilation_cycle_length", C.c_int)]
+
+
+class fd_dims(C.Structure):
+    _fields_ = [("audio_channels", C.c_int), ("inner_channels", C.c_int),
+                ("cond_channels", C.c_int), ("num_blocks", C.c_int),
+                ("upsample_ratios", C.c_int * 4), ("lvc_layers_each_block", C.c_int),
+                ("lvc_kernel_size", C.c_int), ("kpnet_hidden_channels", C.c_int),
+                ("kpnet_conv_size", C.c_int), ("step_embed_in", C.c_int),
+                ("step_embed_mid", C.c_int), ("step_embed_out", C.c_int)]
+
+
+_VP = C.c_void_p
+_SIGS = {
+    "pd_last_error": (C.c_char_p, []),
+    "pd_version": (C.c_int, []),
+    "pd_wavenet_create": (C.c_int, [C.POINTER(pd_wavenet_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
+    "pd_wavenet_destroy": (None, [_VP]),
+    "pd_wavenet_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
+    "pd_wavenet_forward": (C.c_int, [_VP, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
+    "pd_prodiff_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                    C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP,
+                                    C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
+    "fd_create": (C.c_int, [C.POINTER(fd_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
+    "fd_destroy": (None, [_VP]),
+    "fd_hop": (C.c_int, [_VP]),
+    "fd_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
+    "fd_fold_weight_norm": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, _VP]),
+    "fd_forward": (C.c_int, [_VP, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
+    "fd_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                            C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, C.c_int,
+                            C.c_int, _VP, C.c_size_t, _VP]),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the library; raise loudly if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipError(f"libprodiff_hip.so not found at {LIB_PATH}: run "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        l = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().pd_last_error().decode(errors="replace")
+        raise HipError(f"libprodiff_hip error {rc}: {msg}")
+
+
+def fptr(t):
+    """Device pointer of a contiguous float32 CUDA(HIP) tensor, or None."""
+    if t is None:
+        return None
+    import torch
+    if not t.is_cuda:
+        raise HipError("libprodiff_hip needs device tensors (got a CPU tensor)")
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise HipError(f"expected contiguous float32 tensor, got {t.dtype} contiguous={t.is_contiguous()}")
+    return C.c_void_p(t.data_ptr())
+
+
+def farr(vals):
+    arr = (C.c_float * len(vals))(*[float(v) for v in vals])
+    return arr
+
+
+def stream_ptr(device=None):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Workspace:
+    """Grow-only device scratch buffer (torch caching allocator)."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes, device):
+        import torch
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        return C.c_void_p(self.buf.data_ptr()), self.buf.numel()

@@ -1,0 +1,112 @@
+// Common helpers for the ProDiff/FastDiff gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#define PD_OK 0
+#define PD_ERR_ARG 1
+#define PD_ERR_HIP 2
+#define PD_ERR_WORKSPACE 3
+#define PD_ERR_UNSUPPORTED 4
+
+namespace pd {
+
+void set_error(const std::string& msg);
+const char* get_error();
+
+}  // namespace pd
+
+#define PD_CHECK_ARG(cond, msg)                       \
+  do {                                                \
+    if (!(cond)) {                                    \
+      pd::set_error(std::string("argument: ") + msg); \
+      return PD_ERR_ARG;                              \
+    }                                                 \
+  } while (0)
+
+#define PD_HIP(expr)                                                               \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) {                                                        \
+      pd::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));           \
+      return PD_ERR_HIP;                                                           \
+    }                                                                              \
+  } while (0)
+
+#define PD_LAUNCH_CHECK()                                                          \
+  do {                                                                             \
+    hipError_t _e = hipGetLastError();                                             \
+    if (_e != hipSuccess) {                                                        \
+      pd::set_error(std::string("kernel launch: ") + hipGetErrorString(_e) +      \
+                    " at " + __FILE__ + ":" + std::to_string(__LINE__));          \
+      return PD_ERR_HIP;                                                           \
+    }                                                                              \
+  } while (0)
+
+#define PD_TRY(expr)                \
+  do {                              \
+    int _rc = (expr);               \
+    if (_rc != PD_OK) return _rc;   \
+  } while (0)
+
+namespace pd {
+
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_MISH = 3, ACT_SWISH = 4 };
+
+__device__ __forceinline__ float act_apply(float v, int act, float alpha) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_LRELU: return v >= 0.f ? v : alpha * v;
+    case ACT_MISH: {
+      // x * tanh(softplus(x)), softplus threshold 20 (torch default)
+      float sp = v > 20.f ? v : log1pf(expf(v));
+      return v * tanhf(sp);
+    }
+    case ACT_SWISH: return v / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
+
+// ---------------------------------------------------------------------------
+// Counter-based normal/uniform draws (Philox4x32-10), used when the caller does
+// not hand in explicit noise.  key = seed, counter = (index, stream id).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+    uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += W0; k1 += W1;
+  }
+}
+
+__device__ __forceinline__ float u01_from(uint32_t x) {
+  // (0,1]: never 0, so log() is finite
+  return (float)((x >> 8) + 1u) * (1.0f / 16777216.0f);
+}
+
+// One standard-normal draw per (idx, stream) under `seed`.
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t idx, uint32_t stream) {
+  uint32_t c[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), stream, 0x5EEDu};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  float u1 = u01_from(c[0]), u2 = u01_from(c[1]);
+  return sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+}
+
+// One U[0,1) draw per (idx, stream).
+__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t idx, uint32_t stream) {
+  uint32_t c[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), stream, 0x0F00u};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+}
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+}  // namespace pd

@@ -1,0 +1,631 @@
+// FastDiff eps-network + 4-step DDPM sampler on gfx950.
+//
+// Reference: modules/FastDiff/module/FastDiff_model.py:74-102 (network),
+// modules/FastDiff/module/modules.py:116-343 (DBlock, TimeAware_LVCBlock,
+// location_variable_convolution, KernelPredictor), util.py:158-232 (sampler).
+//
+// Activations are time-major [B][time][32]; the kernel predictor writes the
+// location-variable kernels FRAME-major ([B][T'][64 out][3 tap][32 in]), so the
+// LVC consumer reads one contiguous 24 KB block per frame.
+#include <cmath>
+#include <vector>
+
+#include "../../include/prodiff_hip.h"
+#include "gemm.h"
+#include "kernels.h"
+
+using namespace pd;
+
+namespace {
+constexpr int CI = 32;   // inner channels (base.yaml:21)
+constexpr int CC = 80;   // cond channels
+constexpr int HK = 64;   // kpnet hidden
+constexpr int NLY = 4;   // lvc layers per block
+constexpr int KPERLAYER = 2 * CI * CI * 3;   // 6144 kernel values per frame per layer
+constexpr int EMB_IN = 128, EMB_MID = 512, EMB_OUT = 512;
+}  // namespace
+
+struct fd_model {
+  int nblocks;
+  int ratios[4];
+  int hops[4];
+  int dtype;
+  float* pool = nullptr;
+  // step MLP
+  float *fc1_w, *fc1_b, *fc2_w, *fc2_b;
+  float *first_w, *first_b;          // [32][7]
+  float *final_w, *final_b;          // [7][32], [1]
+  struct Block {
+    float *up_w, *up_b;              // [2r][32 ci][32 co]
+    float *fct_w, *fct_b;            // [80][512]
+    float *kin_w, *kin_b;            // [64][5*96]
+    float *kres_w[6], *kres_b[6];    // [64][3*64]
+    float *kk_w, *kk_b;              // [4*6144][3*64] frame-major rows
+    float *kb_w, *kb_b;              // [256][3*64]
+    float *cv_w[NLY], *cv_b[NLY];    // [32][96]
+  } blk[4];
+  struct Down {
+    float *c0_w, *c0_b, *c1_w, *c1_b;   // [32][96]
+    float *c2_w, *c2_b;                 // [32][96 + 32] : conv.2 taps ++ residual_dense
+  } dn[4];
+};
+
+namespace {
+
+// ------------------------------------------------------------------ kernels
+// a0[b][t][c] = bias[c] + sum_k w[c][k] x[b][t+k-3]        (FastDiff_model.py:34-36,90)
+__global__ __launch_bounds__(256) void first_conv_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ bias,
+                                                         float* __restrict__ out, int L) {
+  __shared__ float xs[32 + 6];
+  const int b = blockIdx.y, t0 = blockIdx.x * 32, tid = threadIdx.x;
+  if (tid < 38) {
+    int t = t0 - 3 + tid;
+    xs[tid] = (t >= 0 && t < L) ? x[(long long)b * L + t] : 0.f;
+  }
+  __syncthreads();
+  const int s = tid >> 3, q = (tid & 7) * 4, t = t0 + s;
+  if (t >= L) return;
+  float o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float acc = bias[q + j];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) acc = fmaf(w[(q + j) * 7 + k], xs[s + k], acc);
+    o[j] = acc;
+  }
+  *reinterpret_cast<float4*>(out + ((long long)b * L + t) * CI + q) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// ConvTranspose1d(32,32,k=2r,s=r,p=r/2+r%2,op=r%2) of lrelu_0.2(x)   (modules.py:163-166,205-206)
+// Output phase phi = blockIdx.y: t = r*m + phi uses taps k0 = (phi+p)%r (input m+d) and
+// k0+r (input m+d-1), d = (phi+p)/r.
+__global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ Wt,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ out, int Tin, int r,
+                                                       int p) {
+  __shared__ __attribute__((aligned(16))) float w0[CI * CI], w1[CI * CI];
+  __shared__ float xw[34][CI];
+  const int b = blockIdx.z, phi = blockIdx.y, m0 = blockIdx.x * 32, tid = threadIdx.x;
+  const int k0 = (phi + p) % r, d = (phi + p) / r;
+  for (int i = tid; i < CI * CI; i += 256) {
+    w0[i] = Wt[k0 * CI * CI + i];
+    w1[i] = Wt[(k0 + r) * CI * CI + i];
+  }
+  // rows j = m0 + d - 1 + jj, jj < 34
+  for (int i = tid; i < 34 * CI; i += 256) {
+    int jj = i / CI, c = i - jj * CI;
+    int j = m0 + d - 1 + jj;
+    float v = (j >= 0 && j < Tin) ? x[((long long)b * Tin + j) * CI + c] : 0.f;
+    xw[jj][c] = v >= 0.f ? v : 0.2f * v;
+  }
+  __syncthreads();
+  const int ml = tid >> 3, q = (tid & 7) * 4, m = m0 + ml;
+  if (m >= Tin) return;
+  float4 o = *reinterpret_cast<const float4*>(bias + q);
+#pragma unroll 8
+  for (int ci = 0; ci < CI; ++ci) {
+    float xa = xw[ml + 1][ci];   // input m+d
+    float xb = xw[ml][ci];       // input m+d-1
+    float4 wa = *reinterpret_cast<const float4*>(&w0[ci * CI + q]);
+    float4 wb = *reinterpret_cast<const float4*>(&w1[ci * CI + q]);
+    o.x = fmaf(wa.x, xa, fmaf(wb.x, xb, o.x));
+    o.y = fmaf(wa.y, xa, fmaf(wb.y, xb, o.y));
+    o.z = fmaf(wa.z, xa, fmaf(wb.z, xb, o.z));
+    o.w = fmaf(wa.w, xa, fmaf(wb.w, xb, o.w));
+  }
+  const long long t = (long long)r * m + phi;
+  *reinterpret_cast<float4*>(out + ((long long)b * Tin * r + t) * CI + q) = o;
+}
+
+// x += a + sigmoid(o[:32]) * tanh(o[32:]),  o[t] = Bias_l + K_l . [y[t-1]; y[t]; y[t+1]]
+// one block per frame l (modules.py:208-217, 220-253).  Kf rows: o*96 + tap*32 + ci.
+__global__ __launch_bounds__(256) void lvc_kernel(float* __restrict__ x, const float* __restrict__ a,
+                                                  const float* __restrict__ y,
+                                                  const float* __restrict__ Kf, int kf_ld,
+                                                  const float* __restrict__ Bf, int bf_ld, int Tc,
+                                                  int hop) {
+  __shared__ float ks[64 * 97];
+  __shared__ float bs[64];
+  __shared__ float ys[34 * 33];
+  const int g = blockIdx.x, b = g / Tc, l = g - b * Tc, tid = threadIdx.x;
+  const long long L = (long long)Tc * hop;
+  const float* kf = Kf + (long long)g * kf_ld;
+  for (int i = tid; i < 64 * 96; i += 256) {
+    int o = i / 96, qq = i - o * 96;
+    ks[o * 97 + qq] = kf[i];
+  }
+  if (tid < 64) bs[tid] = Bf[(long long)g * bf_ld + tid];
+  const int c = tid & 31, sg = tid >> 5;
+  for (int s0 = 0; s0 < hop; s0 += 32) {
+    const int chunk = hop - s0 < 32 ? hop - s0 : 32;
+    __syncthreads();
+    for (int i = tid; i < (chunk + 2) * 32; i += 256) {
+      int rr = i >> 5, ci = i & 31;
+      long long t = (long long)l * hop + s0 - 1 + rr;
+      ys[rr * 33 + ci] = (t >= 0 && t < L) ? y[((long long)b * L + t) * CI + ci] : 0.f;
+    }
+    __syncthreads();
+    for (int s = sg; s < chunk; s += 8) {
+      float og = bs[c], of = bs[c + 32];
+      const float* kg = ks + c * 97;
+      const float* kfp = ks + (c + 32) * 97;
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap) {
+        const float* yr = ys + (s + tap) * 33;
+#pragma unroll 8
+        for (int ci = 0; ci < 32; ++ci) {
+          float yv = yr[ci];
+          og = fmaf(kg[tap * 32 + ci], yv, og);
+          of = fmaf(kfp[tap * 32 + ci], yv, of);
+        }
+      }
+      long long idx = ((long long)b * L + (long long)l * hop + s0 + s) * CI + c;
+      x[idx] = x[idx] + a[idx] + sigmoidf_(og) * tanhf(of);
+    }
+  }
+}
+
+// eps[b][t] = bias + sum_{k<7,c<32} w[k][c] x[b][t+k-3][c]      (FastDiff_model.py:67-68,100)
+// mode 0: eps_out = eps.  mode 1 (sampler, util.py:222-226):
+//   xa = (xa - ce*eps) / den + sig * z
+__global__ __launch_bounds__(256) void final_conv_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ w, const float* bias,
+                                                         float* eps_out, float* xa, float ce, float den,
+                                                         float sig, const float* noise,
+                                                         unsigned long long seed, unsigned stream,
+                                                         long long L) {
+  __shared__ float xs[262 * 33];
+  __shared__ float wsh[7 * 32];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const long long t0 = (long long)blockIdx.x * 256;
+  if (tid < 224) wsh[tid] = w[tid];
+  for (int i = tid; i < 262 * 32; i += 256) {
+    int rr = i >> 5, c = i & 31;
+    long long t = t0 - 3 + rr;
+    xs[rr * 33 + c] = (t >= 0 && t < L) ? x[((long long)b * L + t) * CI + c] : 0.f;
+  }
+  __syncthreads();
+  const long long t = t0 + tid;
+  if (t >= L) return;
+  float e = bias[0];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const float* xr = xs + (tid + k) * 33;
+#pragma unroll 8
+    for (int c = 0; c < 32; ++c) e = fmaf(wsh[k * 32 + c], xr[c], e);
+  }
+  const long long idx = (long long)b * L + t;
+  if (eps_out) eps_out[idx] = e;
+  if (xa) {
+    float v = (xa[idx] - ce * e) / den;
+    if (sig != 0.f) v += sig * (noise ? noise[idx] : philox_normal(seed, (unsigned long long)idx, stream));
+    xa[idx] = v;
+  }
+}
+
+// kernel_conv pack: dst row (i*6144 + o*96 + tap*32 + ci), col (kt*64 + h)
+//   <- src [(((i*32+ci)*64+o)*3+tap)][h][kt]            (modules.py:335-340 view)
+__global__ void pack_kernel_conv_kernel(float* dst, float* dst_b, const float* src, const float* src_b) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)NLY * KPERLAYER * HK * 3;
+  if (i >= total) return;
+  int kt = (int)(i % 3);
+  long long r = i / 3;
+  int h = (int)(r % HK);
+  int ch = (int)(r / HK);
+  int tap = ch % 3, o = (ch / 3) % 64, ci = (ch / 192) % 32, layer = ch / (192 * 32);
+  long long row = (long long)layer * KPERLAYER + o * 96 + tap * 32 + ci;
+  dst[row * (3 * HK) + kt * HK + h] = src[i];
+  if (kt == 0 && h == 0) dst_b[row] = src_b[ch];
+}
+
+// upsample weight [ci][co][k] -> [k][ci][co]
+__global__ void pack_upsample_kernel(float* dst, const float* src, int K) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= CI * CI * K) return;
+  int k = i % K, co = (i / K) % CI, ci = i / (K * CI);
+  dst[(k * CI + ci) * CI + co] = src[i];
+}
+
+// final conv weight [1][32][7] -> [7][32]
+__global__ void pack_final_kernel(float* dst, const float* src) {
+  int i = threadIdx.x;
+  if (i < 224) dst[(i % 7) * 32 + i / 7] = src[i];
+}
+
+// ------------------------------------------------------------------ workspace
+struct FdWs {
+  size_t steps, e128, e512a, e512, nz;  // step MLP (nvec = S*B)
+  size_t a0, d[3], dtmp0, dtmp1, xs;
+  size_t X0, X1, y, h0, ra, rb, Bf, Kf, condT, total;
+};
+
+FdWs fd_layout(const fd_model* m, int B, int Tc, int S) {
+  FdWs w{};
+  size_t off = 0;
+  auto take = [&](size_t n) { size_t o = off; off += (n + 63) / 64 * 64; return o; };
+  const size_t L = (size_t)Tc * m->hops[m->nblocks - 1];
+  const size_t nv = (size_t)S * B;
+  w.steps = take(nv);
+  w.e128 = take(nv * EMB_IN);
+  w.e512a = take(nv * EMB_MID);
+  w.e512 = take(nv * EMB_OUT);
+  w.nz = take(nv * m->nblocks * CC);
+  w.a0 = take((size_t)B * L * CI);
+  size_t Ld = L;
+  for (int n = 0; n < m->nblocks; ++n) {
+    Ld /= m->ratios[m->nblocks - 1 - n];
+    w.d[n] = take((size_t)B * Ld * CI);
+  }
+  w.dtmp0 = take((size_t)B * (L / m->ratios[m->nblocks - 1]) * CI);
+  w.dtmp1 = take((size_t)B * (L / m->ratios[m->nblocks - 1]) * CI);
+  w.X0 = take((size_t)B * L * CI);
+  w.X1 = take((size_t)B * L * CI);
+  w.y = take((size_t)B * L * CI);
+  w.h0 = take((size_t)B * Tc * HK);
+  w.ra = take((size_t)B * Tc * HK);
+  w.rb = take((size_t)B * Tc * HK);
+  w.Bf = take((size_t)B * Tc * 2 * CI * NLY);
+  w.Kf = take((size_t)B * Tc * KPERLAYER);
+  w.condT = take((size_t)B * Tc * CC);
+  w.total = off * sizeof(float);
+  return w;
+}
+
+// step embedding -> fc_t1/swish -> fc_t2/swish -> per-block fc_t   (util.py:404-429,
+// FastDiff_model.py:85-87, modules.py:202)
+int fd_step_mlp(const fd_model* m, float* ws, const FdWs& W, int nv, hipStream_t st) {
+  PD_TRY(sinusoidal_embed(ws + W.steps, ws + W.e128, nv, EMB_IN, st));
+  PD_TRY(matvec(m->fc1_w, m->fc1_b, ws + W.e128, EMB_IN, ws + W.e512a, EMB_MID, EMB_MID, EMB_IN, nv, ACT_SWISH, st));
+  PD_TRY(matvec(m->fc2_w, m->fc2_b, ws + W.e512a, EMB_MID, ws + W.e512, EMB_OUT, EMB_OUT, EMB_MID, nv, ACT_SWISH, st));
+  for (int n = 0; n < m->nblocks; ++n)
+    PD_TRY(matvec(m->blk[n].fct_w, m->blk[n].fct_b, ws + W.e512, EMB_OUT, ws + W.nz + n * CC,
+                  m->nblocks * CC, CC, EMB_OUT, nv, ACT_NONE, st));
+  return PD_OK;
+}
+
+// DiffusionDBlock (modules.py:131-138): out = conv_d4(lr(conv_d2(lr(conv_d1(lr(x[f i])))))) + Wr x[f i]
+int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, float* t1, int B, int Tout,
+           int f, hipStream_t st) {
+  const long long bsi = (long long)Tout * f * CI, bso = (long long)Tout * CI;
+  {
+    GemmArgs a = make_gemm(B, Tout, CI, D.c0_w, 96, D.c0_b, t0, bso, CI);
+    for (int tap = 0; tap < 3; ++tap) {
+      Seg s = make_seg(in, bsi, CI, CI, tap - 1, f);
+      s.act = ACT_LRELU; s.alpha = 0.2f;
+      add_seg(a, s);
+    }
+    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE>(a, st)));
+  }
+  {
+    GemmArgs a = make_gemm(B, Tout, CI, D.c1_w, 96, D.c1_b, t1, bso, CI);
+    for (int tap = 0; tap < 3; ++tap) {
+      Seg s = make_seg(t0, bso, CI, CI, (tap - 1) * 2);
+      s.act = ACT_LRELU; s.alpha = 0.2f;
+      add_seg(a, s);
+    }
+    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE>(a, st)));
+  }
+  {
+    GemmArgs a = make_gemm(B, Tout, CI, D.c2_w, 128, D.c2_b, out, bso, CI);
+    for (int tap = 0; tap < 3; ++tap) {
+      Seg s = make_seg(t1, bso, CI, CI, (tap - 1) * 4);
+      s.act = ACT_LRELU; s.alpha = 0.2f;
+      add_seg(a, s);
+    }
+    add_seg(a, make_seg(in, bsi, CI, CI, 0, f));   // residual_dense on x[f i]
+    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE>(a, st)));
+  }
+  return PD_OK;
+}
+
+// One eps-network evaluation.  xa: audio [B][L]; condT: [B][Tc][80];
+// nz: this step's per-block fc_t(emb) rows ([B][nblocks*80]).  Leaves the LVC output in *xout.
+int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const float* condT,
+           const float* nz, int B, int Tc, float** xout, hipStream_t st) {
+  const int nb = m->nblocks;
+  const long long L = (long long)Tc * m->hops[nb - 1];
+  float* a0 = ws + W.a0;
+  hipLaunchKernelGGL(first_conv_kernel, dim3(cdiv(L, 32), B), dim3(256), 0, st, xa, m->first_w,
+                     m->first_b, a0, (int)L);
+  PD_LAUNCH_CHECK();
+  // downsample chain: a0 -> d[0] -> ... -> d[nb-1]   (FastDiff_model.py:89-93)
+  const float* cur = a0;
+  long long Lc = L;
+  const float* downs[4];
+  for (int n = 0; n < nb; ++n) {
+    downs[n] = cur;
+    const int f = m->ratios[nb - 1 - n];
+    Lc /= f;
+    PD_TRY(dblock(m->dn[n], cur, ws + W.d[n], ws + W.dtmp0, ws + W.dtmp1, B, (int)Lc, f, st));
+    cur = ws + W.d[n];
+  }
+  // LVC blocks (FastDiff_model.py:95-97)
+  const float* x = cur;   // [B][Tc][32]
+  float* bufs[2] = {ws + W.X0, ws + W.X1};
+  long long Tin = Tc;
+  for (int n = 0; n < nb; ++n) {
+    const fd_model::Block& K = m->blk[n];
+    const int r = m->ratios[n], hop = m->hops[n];
+    const float* ad = downs[nb - 1 - n];
+    float* xn = bufs[n & 1];
+    const long long Tout = Tin * r;
+    const long long bsC = (long long)Tc * CC, bsH = (long long)Tc * HK;
+    // --- kernel predictor on c + fc_t(emb)   (modules.py:202-204, 320-343)
+    {
+      GemmArgs a = make_gemm(B, Tc, HK, K.kin_w, 5 * 96, K.kin_b, ws + W.h0, bsH, HK);
+      for (int tap = 0; tap < 5; ++tap) {
+        Seg s = make_seg(condT, bsC, CC, CC, tap - 2);
+        s.add_vec = nz + n * CC;
+        s.add_ld = nb * CC;
+        add_seg(a, s);
+      }
+      a.act = ACT_LRELU; a.alpha = 0.1f;
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+    }
+    const float* src = ws + W.h0;
+    float* rbuf[2] = {ws + W.ra, ws + W.rb};
+    for (int j = 0; j < 6; ++j) {
+      float* dst = rbuf[j & 1];
+      GemmArgs a = make_gemm(B, Tc, HK, K.kres_w[j], 3 * HK, K.kres_b[j], dst, bsH, HK);
+      for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(src, bsH, HK, HK, tap - 1));
+      a.act = ACT_LRELU; a.alpha = 0.1f;
+      if (j == 5) { a.res = ws + W.h0; a.res_bs = bsH; a.res_ld = HK; }   // h + R(h)
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+      src = dst;
+    }
+    const float* hk = src;   // final h  [B][Tc][64]
+    {
+      GemmArgs a = make_gemm(B, Tc, 2 * CI * NLY, K.kb_w, 3 * HK, K.kb_b, ws + W.Bf,
+                             (long long)Tc * 2 * CI * NLY, 2 * CI * NLY);
+      for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+    }
+    // --- upsample (modules.py:205-206)
+    {
+      const int p = r / 2 + r % 2;
+      hipLaunchKernelGGL(upsample_kernel, dim3(cdiv(Tin, 32), r, B), dim3(256), 0, st, x, K.up_w, K.up_b,
+                         xn, (int)Tin, r, p);
+      PD_LAUNCH_CHECK();
+    }
+    // --- 4 LVC layers (modules.py:208-217)
+    for (int i = 0; i < NLY; ++i) {
+      {  // this layer's kernels, frame-major
+        GemmArgs a = make_gemm(B, Tc, KPERLAYER, K.kk_w + (size_t)i * KPERLAYER * 3 * HK, 3 * HK,
+                               K.kk_b + (size_t)i * KPERLAYER, ws + W.Kf, (long long)Tc * KPERLAYER,
+                               KPERLAYER);
+        for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
+        PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+      }
+      {  // y = lrelu(conv_dil3^i(lrelu(x + a)) + b)
+        const int dil = (int)std::pow(3, i);
+        GemmArgs a = make_gemm(B, (int)Tout, CI, K.cv_w[i], 96, K.cv_b[i], ws + W.y, Tout * CI, CI);
+        for (int tap = 0; tap < 3; ++tap) {
+          Seg s = make_seg(xn, Tout * CI, CI, CI, (tap - 1) * dil);
+          s.add_ten = ad;
+          s.act = ACT_LRELU; s.alpha = 0.2f;
+          add_seg(a, s);
+        }
+        a.act = ACT_LRELU; a.alpha = 0.2f;
+        PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE>(a, st)));
+      }
+      hipLaunchKernelGGL(lvc_kernel, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y, ws + W.Kf,
+                         KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Tc, hop);
+      PD_LAUNCH_CHECK();
+    }
+    x = xn;
+    Tin = Tout;
+  }
+  *xout = const_cast<float*>(x);
+  return PD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* stream, fd_model** out) {
+  PD_CHECK_ARG(dims && params && out, "null pointer");
+  PD_CHECK_ARG(dtype == PD_DTYPE_F32, "only PD_DTYPE_F32 is implemented for the FastDiff path");
+  PD_CHECK_ARG(dims->audio_channels == 1 && dims->inner_channels == CI && dims->cond_channels == CC &&
+                   dims->lvc_layers_each_block == NLY && dims->lvc_kernel_size == 3 &&
+                   dims->kpnet_hidden_channels == HK && dims->kpnet_conv_size == 3 &&
+                   dims->step_embed_in == EMB_IN && dims->step_embed_mid == EMB_MID &&
+                   dims->step_embed_out == EMB_OUT,
+               "only the FastDiff base.yaml architecture (32/80/64, 4 LVC layers) is supported");
+  PD_CHECK_ARG(dims->num_blocks >= 1 && dims->num_blocks <= 4, "num_blocks in [1,4]");
+  hipStream_t st = (hipStream_t)stream;
+  fd_model* m = new fd_model();
+  m->nblocks = dims->num_blocks;
+  m->dtype = dtype;
+  int hop = 1;
+  for (int n = 0; n < m->nblocks; ++n) {
+    m->ratios[n] = dims->upsample_ratios[n];
+    if (m->ratios[n] < 2 || m->ratios[n] > 16) { delete m; set_error("upsample ratio in [2,16]"); return PD_ERR_ARG; }
+    hop *= m->ratios[n];
+    m->hops[n] = hop;
+  }
+  // allocation plan
+  std::vector<std::pair<float**, size_t>> plan;
+  plan.push_back({&m->fc1_w, (size_t)EMB_MID * EMB_IN}); plan.push_back({&m->fc1_b, EMB_MID});
+  plan.push_back({&m->fc2_w, (size_t)EMB_OUT * EMB_MID}); plan.push_back({&m->fc2_b, EMB_OUT});
+  plan.push_back({&m->first_w, 224}); plan.push_back({&m->first_b, CI});
+  plan.push_back({&m->final_w, 224}); plan.push_back({&m->final_b, 1});
+  for (int n = 0; n < m->nblocks; ++n) {
+    auto& K = m->blk[n];
+    plan.push_back({&K.up_w, (size_t)2 * m->ratios[n] * CI * CI}); plan.push_back({&K.up_b, CI});
+    plan.push_back({&K.fct_w, (size_t)CC * EMB_OUT}); plan.push_back({&K.fct_b, CC});
+    plan.push_back({&K.kin_w, (size_t)HK * 5 * 96}); plan.push_back({&K.kin_b, HK});
+    for (int j = 0; j < 6; ++j) { plan.push_back({&K.kres_w[j], (size_t)HK * 3 * HK}); plan.push_back({&K.kres_b[j], HK}); }
+    plan.push_back({&K.kk_w, (size_t)NLY * KPERLAYER * 3 * HK}); plan.push_back({&K.kk_b, (size_t)NLY * KPERLAYER});
+    plan.push_back({&K.kb_w, (size_t)2 * CI * NLY * 3 * HK}); plan.push_back({&K.kb_b, (size_t)2 * CI * NLY});
+    for (int i = 0; i < NLY; ++i) { plan.push_back({&K.cv_w[i], (size_t)CI * 96}); plan.push_back({&K.cv_b[i], CI}); }
+  }
+  for (int n = 0; n < m->nblocks; ++n) {
+    auto& D = m->dn[n];
+    plan.push_back({&D.c0_w, (size_t)CI * 96}); plan.push_back({&D.c0_b, CI});
+    plan.push_back({&D.c1_w, (size_t)CI * 96}); plan.push_back({&D.c1_b, CI});
+    plan.push_back({&D.c2_w, (size_t)CI * 128}); plan.push_back({&D.c2_b, CI});
+  }
+  size_t off = 0;
+  std::vector<size_t> offs;
+  for (auto& p : plan) { offs.push_back(off); off += (p.second + 63) / 64 * 64; }
+  if (hipMalloc(&m->pool, off * sizeof(float)) != hipSuccess) {
+    delete m; set_error("hipMalloc failed for FastDiff weights"); return PD_ERR_HIP;
+  }
+  for (size_t i = 0; i < plan.size(); ++i) *plan[i].first = m->pool + offs[i];
+
+  auto run = [&]() -> int {
+    PD_HIP(hipMemsetAsync(m->pool, 0, off * sizeof(float), st));
+    auto cp = [&](float* dst, const float* src, size_t n) -> int {
+      PD_HIP(hipMemcpyAsync(dst, src, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+      return PD_OK;
+    };
+    int p = 0;
+    auto nxt = [&]() { const float* q = params[p++]; return q; };
+    // order: see include/prodiff_hip.h (FD_PARAM_ORDER)
+    {
+      const float* w = nxt(); const float* b = nxt();
+      PD_TRY(cp(m->first_w, w, 224)); PD_TRY(cp(m->first_b, b, CI));
+    }
+    PD_TRY(cp(m->fc1_w, nxt(), (size_t)EMB_MID * EMB_IN)); PD_TRY(cp(m->fc1_b, nxt(), EMB_MID));
+    PD_TRY(cp(m->fc2_w, nxt(), (size_t)EMB_OUT * EMB_MID)); PD_TRY(cp(m->fc2_b, nxt(), EMB_OUT));
+    for (int n = 0; n < m->nblocks; ++n) {
+      auto& K = m->blk[n];
+      const int r = m->ratios[n];
+      {
+        const float* w = nxt();
+        hipLaunchKernelGGL(pack_upsample_kernel, dim3(cdiv(CI * CI * 2 * r, 256)), dim3(256), 0, st, K.up_w, w, 2 * r);
+        PD_LAUNCH_CHECK();
+        PD_TRY(cp(K.up_b, nxt(), CI));
+      }
+      PD_TRY(pack_conv(K.kin_w, 5 * 96, 0, 0, 96, nxt(), HK, CC, 5, st));
+      PD_TRY(cp(K.kin_b, nxt(), HK));
+      for (int j = 0; j < 6; ++j) {
+        PD_TRY(pack_conv(K.kres_w[j], 3 * HK, 0, 0, HK, nxt(), HK, HK, 3, st));
+        PD_TRY(cp(K.kres_b[j], nxt(), HK));
+      }
+      {
+        const float* w = nxt(); const float* b = nxt();
+        const long long total = (long long)NLY * KPERLAYER * HK * 3;
+        hipLaunchKernelGGL(pack_kernel_conv_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, K.kk_w, K.kk_b, w, b);
+        PD_LAUNCH_CHECK();
+      }
+      PD_TRY(pack_conv(K.kb_w, 3 * HK, 0, 0, HK, nxt(), 2 * CI * NLY, HK, 3, st));
+      PD_TRY(cp(K.kb_b, nxt(), 2 * CI * NLY));
+      PD_TRY(cp(K.fct_w, nxt(), (size_t)CC * EMB_OUT));
+      PD_TRY(cp(K.fct_b, nxt(), CC));
+      for (int i = 0; i < NLY; ++i) {
+        PD_TRY(pack_conv(K.cv_w[i], 96, 0, 0, CI, nxt(), CI, CI, 3, st));
+        PD_TRY(cp(K.cv_b[i], nxt(), CI));
+      }
+    }
+    for (int n = 0; n < m->nblocks; ++n) {
+      auto& D = m->dn[n];
+      const float* rw = nxt(); const float* rb = nxt();
+      const float* w0 = nxt(); const float* b0 = nxt();
+      const float* w1 = nxt(); const float* b1 = nxt();
+      const float* w2 = nxt(); const float* b2 = nxt();
+      PD_TRY(pack_conv(D.c0_w, 96, 0, 0, CI, w0, CI, CI, 3, st)); PD_TRY(cp(D.c0_b, b0, CI));
+      PD_TRY(pack_conv(D.c1_w, 96, 0, 0, CI, w1, CI, CI, 3, st)); PD_TRY(cp(D.c1_b, b1, CI));
+      PD_TRY(pack_conv(D.c2_w, 128, 0, 0, CI, w2, CI, CI, 3, st));
+      PD_TRY(pack_conv(D.c2_w, 128, 0, 96, CI, rw, CI, CI, 1, st));
+      PD_TRY(add_vectors(D.c2_b, b2, rb, CI, st));
+    }
+    {
+      const float* w = nxt(); const float* b = nxt();
+      hipLaunchKernelGGL(pack_final_kernel, dim3(1), dim3(256), 0, st, m->final_w, w);
+      PD_LAUNCH_CHECK();
+      PD_TRY(cp(m->final_b, b, 1));
+    }
+    if (p != FD_NUM_PARAMS(m->nblocks)) { set_error("fd_create: parameter count mismatch"); return PD_ERR_ARG; }
+    return PD_OK;
+  };
+  for (int i = 0; i < FD_NUM_PARAMS(m->nblocks); ++i)
+    if (!params[i]) { hipFree(m->pool); delete m; set_error("null parameter " + std::to_string(i)); return PD_ERR_ARG; }
+  int rc = run();
+  if (rc != PD_OK) { hipFree(m->pool); delete m; return rc; }
+  *out = m;
+  return PD_OK;
+}
+
+void fd_destroy(fd_model* m) {
+  if (!m) return;
+  hipFree(m->pool);
+  delete m;
+}
+
+int fd_hop(const fd_model* m) { return m ? m->hops[m->nblocks - 1] : 0; }
+
+size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S) {
+  if (!m || B < 0 || Tc < 0 || S < 1) return 0;
+  return fd_layout(m, B, Tc, S).total;
+}
+
+int fd_forward(const fd_model* m, const float* audio, const float* cond, const float* steps, float* eps,
+               int B, int Tc, void* workspace, size_t ws_bytes, void* stream) {
+  PD_CHECK_ARG(m && audio && cond && steps && eps && workspace, "null pointer");
+  PD_CHECK_ARG(B > 0 && Tc > 0, "B and T' must be positive");
+  FdWs W = fd_layout(m, B, Tc, 1);
+  if (ws_bytes < W.total) { set_error("workspace too small"); return PD_ERR_WORKSPACE; }
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  const long long L = (long long)Tc * m->hops[m->nblocks - 1];
+  PD_HIP(hipMemcpyAsync(ws + W.steps, steps, sizeof(float) * B, hipMemcpyDeviceToDevice, st));
+  PD_TRY(fd_step_mlp(m, ws, W, B, st));
+  PD_TRY(transpose_ct_to_tc(cond, ws + W.condT, B, CC, Tc, st));
+  float* x = nullptr;
+  PD_TRY(fd_net(m, ws, W, audio, ws + W.condT, ws + W.nz, B, Tc, &x, st));
+  hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w, m->final_b,
+                     eps, (float*)nullptr, 0.f, 0.f, 0.f, (const float*)nullptr, 0ull, 0u, L);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+int fd_sample(const fd_model* m, const float* mel, const float* beta, const float* alpha, const float* sigma,
+              const float* steps, int N, const float* x_T, const float* noise, unsigned long long seed,
+              float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream) {
+  PD_CHECK_ARG(m && mel && beta && alpha && sigma && steps && wav && workspace, "null pointer");
+  PD_CHECK_ARG(B > 0 && Tc > 0 && N >= 1 && N <= 16, "bad B/T'/N");
+  FdWs W = fd_layout(m, B, Tc, N);
+  if (ws_bytes < W.total) { set_error("workspace too small"); return PD_ERR_WORKSPACE; }
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  const long long L = (long long)Tc * m->hops[m->nblocks - 1];
+  // x_T ~ N(0,1)  (util.py:208)
+  if (x_T) {
+    PD_HIP(hipMemcpyAsync(wav, x_T, sizeof(float) * B * L, hipMemcpyDeviceToDevice, st));
+  } else {
+    PD_TRY(fill_normal(wav, B * L, seed, 0xFFFF0001u, st));
+  }
+  // every step's embedding at once: pass j uses n = N-1-j
+  std::vector<float> sv(N);
+  for (int j = 0; j < N; ++j) sv[j] = steps[N - 1 - j];
+  PD_TRY(fill_steps(ws + W.steps, sv.data(), N, B, st));
+  PD_TRY(fd_step_mlp(m, ws, W, N * B, st));
+  for (int j = 0; j < N; ++j) {
+    const int n = N - 1 - j;
+    float* x = nullptr;
+    PD_TRY(fd_net(m, ws, W, wav, mel, ws + W.nz + (size_t)j * B * m->nblocks * CC, B, Tc, &x, st));
+    // x = (x - beta/sqrt(1-alpha^2) eps) / sqrt(1-beta) + [n>0] sigma z   (util.py:222-226)
+    const float ce = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
+    const float den = sqrtf(1.f - beta[n]);
+    const float sg = n > 0 ? sigma[n] : 0.f;
+    hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w,
+                       m->final_b, (float*)nullptr, wav, ce, den, sg,
+                       noise ? noise + (size_t)j * B * L : (const float*)nullptr, seed, 0x10000u + j, L);
+    PD_LAUNCH_CHECK();
+  }
+  return PD_OK;
+}
+
+}  // extern "C"
+
+extern "C" int fd_fold_weight_norm(float* w, const float* g, const float* v, int cout, int per_row,
+                                   void* stream) {
+  PD_CHECK_ARG(w && g && v && cout > 0 && per_row > 0, "bad weight-norm arguments");
+  return pd::weight_norm_fold(w, g, v, cout, per_row, (hipStream_t)stream);
+}

@@ -1,0 +1,301 @@
+// Implicit-GEMM Conv1d engine for gfx950 (fp32 in / fp32 accumulate on MFMA).
+//
+// Every Conv1d/Linear on the ProDiff/FastDiff hot path is computed here as
+//     out[b, t, n] = epilogue( sum_k A(b, t, k) * W[n][k] )
+// over TIME-MAJOR activations ([batch][time][channel], channels contiguous).
+// The reduction axis k is a concatenation of "segments": each segment is one
+// conv tap (or one extra input tensor) read at row  v*row_mul  with
+// v = t + row_off, zero outside [0, T) of its utterance (the conv zero
+// padding), optionally pre-processed on load (per-(b,c) add, tensor add,
+// activation, scale).  Weights are pre-packed once as W[n][sum(kpad)].
+//
+// Tile: 256 threads = 4 waves; each wave owns WM_T x WN_T 32x32 accumulator
+// tiles of v_mfma_f32_32x32x2_f32 (exact f32 fmaf chain).
+// K is staged through LDS 32 deep, double-buffered, the next chunk's global
+// loads in flight under the current chunk's MFMAs.
+#pragma once
+#include "common.h"
+
+namespace pd {
+
+constexpr int GEMM_BK = 32;
+constexpr int MAX_SEGS = 8;
+
+struct Seg {
+  const float* src;        // points at channel c_off of batch 0, row 0
+  long long bstride;       // elements between utterances
+  int ld;                  // elements between rows
+  int cs;                  // channels read (multiple of 4)
+  int row_mul;             // source row = v * row_mul
+  int row_off;             // v = t + row_off  (zero padding outside [0,T))
+  const float* add_vec;    // optional [B][add_ld] per-(b,c) add (before act)
+  int add_ld;
+  const float* add_ten;    // optional tensor add, same layout as src (before act)
+  int act;
+  float alpha;
+  float scale;
+  int kpad;                // cs rounded up to GEMM_BK
+};
+
+enum Epi { EPI_STORE = 0, EPI_GATE = 1, EPI_RESSKIP = 2, EPI_POSTERIOR = 3 };
+
+struct GemmArgs {
+  int B, T, N, nseg;
+  Seg seg[MAX_SEGS];
+  const float* W;           // packed [N][ldw]
+  int ldw;                  // = sum of seg kpad
+  const float* bias;        // [N]
+  float* out;
+  long long out_bs;
+  int out_ld;
+  int act;
+  float alpha, scale;
+  const float* res;         // STORE: added after act/scale; POSTERIOR: x_t
+  long long res_bs;
+  int res_ld;
+  int half;                 // paired modes: columns n and n+half combine
+  float* out2;              // RESSKIP: skip accumulator
+  long long out2_bs;
+  int out2_ld;
+  int flag;                 // RESSKIP: 1 -> first layer (skip = value)
+  float c1, c2, sigma;      // POSTERIOR: x = c1*x0 + c2*x_t + sigma*n
+  const float* noise;       // POSTERIOR: explicit draws (time-major) or null -> Philox
+  long long noise_bs;
+  int noise_ld;
+  unsigned long long seed;
+  unsigned int stream_id;
+};
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
+  constexpr int BM = 32 * WM_T * WAVES_M;
+  constexpr int BN = 32 * WN_T * WAVES_N;
+  constexpr int BK = GEMM_BK;
+  constexpr int LDL = BK + 4;  // padded LDS row (conflict-free ds_read_b128)
+  constexpr bool PAIRED = (EPI == EPI_GATE || EPI == EPI_RESSKIP);
+  static_assert(!PAIRED || (WN_T == 2 && WAVES_N == 1), "paired epilogue layout");
+  constexpr int A_IT = BM / 32, B_IT = BN / 32;
+
+  __shared__ __attribute__((aligned(16))) float smem[2][(BM + BN) * LDL];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int rows = a.B * a.T;
+  const int row0 = blockIdx.x * BM;
+  const int nb = PAIRED ? blockIdx.y * (BN / 2) : blockIdx.y * BN;
+  const int q4 = (tid & 7) * 4;
+
+  int a_b[A_IT], a_t[A_IT];
+  bool a_ok[A_IT];
+#pragma unroll
+  for (int i = 0; i < A_IT; ++i) {
+    int R = row0 + (tid >> 3) + 32 * i;
+    a_ok[i] = R < rows;
+    int b = a_ok[i] ? R / a.T : 0;
+    a_b[i] = b;
+    a_t[i] = R - b * a.T;
+  }
+  const float* w_ptr[B_IT];
+  bool w_ok[B_IT];
+#pragma unroll
+  for (int i = 0; i < B_IT; ++i) {
+    int local = (tid >> 3) + 32 * i;
+    int n = PAIRED ? (local < BN / 2 ? nb + local : a.half + nb + local - BN / 2) : nb + local;
+    w_ok[i] = n < a.N;
+    w_ptr[i] = a.W + (long long)(w_ok[i] ? n : 0) * a.ldw + q4;
+  }
+
+  float4 ra[A_IT], rb[B_IT];
+  auto load_chunk = [&](int s, int c0, int kg) {
+    const Seg& sg = a.seg[s];
+    const int c = c0 + q4;
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      int vv = a_t[i] + sg.row_off;
+      if (a_ok[i] && c < sg.cs && vv >= 0 && vv < a.T) {
+        long long off = (long long)a_b[i] * sg.bstride + (long long)vv * sg.row_mul * sg.ld + c;
+        v = *reinterpret_cast<const float4*>(sg.src + off);
+        if (sg.add_ten) {
+          float4 w = *reinterpret_cast<const float4*>(sg.add_ten + off);
+          v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+        }
+        if (sg.add_vec) {
+          float4 w = *reinterpret_cast<const float4*>(sg.add_vec + (long long)a_b[i] * sg.add_ld + c);
+          v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+        }
+        if (sg.act != ACT_NONE) {
+          v.x = act_apply(v.x, sg.act, sg.alpha); v.y = act_apply(v.y, sg.act, sg.alpha);
+          v.z = act_apply(v.z, sg.act, sg.alpha); v.w = act_apply(v.w, sg.act, sg.alpha);
+        }
+        if (sg.scale != 1.f) { v.x *= sg.scale; v.y *= sg.scale; v.z *= sg.scale; v.w *= sg.scale; }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i)
+      rb[i] = w_ok[i] ? *reinterpret_cast<const float4*>(w_ptr[i] + kg) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto store_chunk = [&](int buf) {
+    float* As = smem[buf];
+    float* Bs = smem[buf] + BM * LDL;
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i)
+      *reinterpret_cast<float4*>(As + ((tid >> 3) + 32 * i) * LDL + q4) = ra[i];
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i)
+      *reinterpret_cast<float4*>(Bs + ((tid >> 3) + 32 * i) * LDL + q4) = rb[i];
+  };
+
+  f32x16 acc[WM_T][WN_T];
+#pragma unroll
+  for (int i = 0; i < WM_T; ++i)
+#pragma unroll
+    for (int j = 0; j < WN_T; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nchunks = a.ldw / BK;
+  int s = 0, c0 = 0;
+  load_chunk(0, 0, 0);
+  store_chunk(0);
+  __syncthreads();
+  const int r32 = lane & 31, h = lane >> 5;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const bool more = ch + 1 < nchunks;
+    if (more) {
+      c0 += BK;
+      if (c0 >= a.seg[s].kpad) { ++s; c0 = 0; }
+      load_chunk(s, c0, (ch + 1) * BK);
+    }
+    const float* As = smem[ch & 1];
+    const float* Bs = smem[ch & 1] + BM * LDL;
+    float af[WM_T][16], bf[WN_T][16];
+#pragma unroll
+    for (int i = 0; i < WM_T; ++i) {
+      const float* p = As + (wm * 32 * WM_T + i * 32 + r32) * LDL + h * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
+        af[i][4 * q] = v.x; af[i][4 * q + 1] = v.y; af[i][4 * q + 2] = v.z; af[i][4 * q + 3] = v.w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < WN_T; ++j) {
+      const float* p = Bs + (wn * 32 * WN_T + j * 32 + r32) * LDL + h * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
+        bf[j][4 * q] = v.x; bf[j][4 * q + 1] = v.y; bf[j][4 * q + 2] = v.z; bf[j][4 * q + 3] = v.w;
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int i = 0; i < WM_T; ++i)
+#pragma unroll
+        for (int j = 0; j < WN_T; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bf[j][kk], acc[i][j], 0, 0, 0);
+    if (more) store_chunk((ch + 1) & 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------ epilogue
+  // C/D map of 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+  const float rs2 = 0.70710678118654752440f;
+#pragma unroll
+  for (int i = 0; i < WM_T; ++i) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int rl = wm * 32 * WM_T + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      const int R = row0 + rl;
+      if (R >= rows) continue;
+      const int b = R / a.T, t = R - b * a.T;
+      if constexpr (EPI == EPI_GATE) {
+        const int n = nb + r32;
+        float v0 = acc[i][0][reg] + a.bias[n];
+        float v1 = acc[i][1][reg] + a.bias[a.half + n];
+        a.out[(long long)b * a.out_bs + (long long)t * a.out_ld + n] = sigmoidf_(v0) * tanhf(v1);
+      } else if constexpr (EPI == EPI_RESSKIP) {
+        const int n = nb + r32;
+        float v0 = acc[i][0][reg] + a.bias[n];
+        float v1 = acc[i][1][reg] + a.bias[a.half + n];
+        float* xp = a.out + (long long)b * a.out_bs + (long long)t * a.out_ld + n;
+        *xp = (*xp + v0) * rs2;
+        float* sp = a.out2 + (long long)b * a.out2_bs + (long long)t * a.out2_ld + n;
+        *sp = a.flag ? v1 : (*sp + v1);
+      } else {
+#pragma unroll
+        for (int j = 0; j < WN_T; ++j) {
+          const int n = nb + wn * 32 * WN_T + j * 32 + r32;
+          if (n >= a.N) continue;
+          float v = acc[i][j][reg] + (a.bias ? a.bias[n] : 0.f);
+          if constexpr (EPI == EPI_POSTERIOR) {
+            float xt = a.res[(long long)b * a.res_bs + (long long)t * a.res_ld + n];
+            float x = a.c1 * v + a.c2 * xt;
+            if (a.sigma != 0.f) {
+              float z = a.noise ? a.noise[(long long)b * a.noise_bs + (long long)t * a.noise_ld + n]
+                                : philox_normal(a.seed, ((unsigned long long)R) * a.N + n, a.stream_id);
+              x += a.sigma * z;
+            }
+            a.out[(long long)b * a.out_bs + (long long)t * a.out_ld + n] = x;
+          } else {
+            v = act_apply(v, a.act, a.alpha) * a.scale;
+            if (a.res) v += a.res[(long long)b * a.res_bs + (long long)t * a.res_ld + n];
+            a.out[(long long)b * a.out_bs + (long long)t * a.out_ld + n] = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Host-side validation + launch.  Returns PD_OK or an error code.
+int validate_gemm(const GemmArgs& a);
+
+template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI>
+int launch_gemm(const GemmArgs& a, hipStream_t st) {
+  PD_TRY(validate_gemm(a));
+  constexpr int BM = 32 * WM_T * WAVES_M;
+  constexpr int BN = 32 * WN_T * WAVES_N;
+  constexpr bool PAIRED = (EPI == EPI_GATE || EPI == EPI_RESSKIP);
+  const long long rows = (long long)a.B * a.T;
+  if (rows == 0) return PD_OK;
+  dim3 grid(cdiv(rows, BM), PAIRED ? a.half / 32 : cdiv(a.N, BN));
+  if (PAIRED && (a.half % 32 != 0 || a.N != 2 * a.half)) {
+    set_error("paired gemm needs N == 2*half, half % 32 == 0");
+    return PD_ERR_ARG;
+  }
+  hipLaunchKernelGGL((gemm_f32_kernel<WM_T, WN_T, WAVES_M, WAVES_N, EPI>), grid, dim3(256), 0, st, a);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// Convenience constructors ---------------------------------------------------
+inline Seg make_seg(const float* src, long long bstride, int ld, int cs, int row_off,
+                    int row_mul = 1) {
+  Seg s{};
+  s.src = src; s.bstride = bstride; s.ld = ld; s.cs = cs;
+  s.row_mul = row_mul; s.row_off = row_off;
+  s.add_vec = nullptr; s.add_ld = 0; s.add_ten = nullptr;
+  s.act = ACT_NONE; s.alpha = 0.f; s.scale = 1.f;
+  s.kpad = round_up(cs, GEMM_BK);
+  return s;
+}
+
+inline GemmArgs make_gemm(int B, int T, int N, const float* W, int ldw, const float* bias,
+                          float* out, long long out_bs, int out_ld) {
+  GemmArgs a{};
+  a.B = B; a.T = T; a.N = N; a.nseg = 0;
+  a.W = W; a.ldw = ldw; a.bias = bias;
+  a.out = out; a.out_bs = out_bs; a.out_ld = out_ld;
+  a.act = ACT_NONE; a.alpha = 0.f; a.scale = 1.f;
+  return a;
+}
+
+inline void add_seg(GemmArgs& a, const Seg& s) { a.seg[a.nseg++] = s; }
+
+}  // namespace pd

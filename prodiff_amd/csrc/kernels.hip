@@ -1,0 +1,234 @@
+// Small utility kernels + error plumbing.
+#include <cmath>
+#include <cstring>
+
+#include "gemm.h"
+#include "kernels.h"
+
+namespace pd {
+
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+const char* get_error() { return g_err.c_str(); }
+
+int validate_gemm(const GemmArgs& a) {
+  if (a.B < 0 || a.T < 0 || a.N <= 0) { set_error("gemm: bad B/T/N"); return PD_ERR_ARG; }
+  if (a.nseg <= 0 || a.nseg > MAX_SEGS) { set_error("gemm: bad segment count"); return PD_ERR_ARG; }
+  int k = 0;
+  for (int i = 0; i < a.nseg; ++i) {
+    const Seg& s = a.seg[i];
+    if (!s.src || s.cs <= 0 || (s.cs & 3) || (s.ld & 3) || (s.bstride & 3) ||
+        (reinterpret_cast<uintptr_t>(s.src) & 15) || s.kpad % GEMM_BK || s.kpad < s.cs ||
+        s.row_mul < 1) {
+      set_error("gemm: segment " + std::to_string(i) + " not 16-byte aligned / padded");
+      return PD_ERR_ARG;
+    }
+    if (s.add_vec && ((s.add_ld & 3) || (reinterpret_cast<uintptr_t>(s.add_vec) & 15))) {
+      set_error("gemm: add_vec alignment"); return PD_ERR_ARG;
+    }
+    if (s.add_ten && (reinterpret_cast<uintptr_t>(s.add_ten) & 15)) {
+      set_error("gemm: add_ten alignment"); return PD_ERR_ARG;
+    }
+    k += s.kpad;
+  }
+  if (k != a.ldw) { set_error("gemm: sum(kpad) != ldw"); return PD_ERR_ARG; }
+  if (reinterpret_cast<uintptr_t>(a.W) & 15) { set_error("gemm: W alignment"); return PD_ERR_ARG; }
+  return PD_OK;
+}
+
+// ---------------------------------------------------------------- matvec
+__global__ __launch_bounds__(256) void matvec_kernel(const float* __restrict__ W,
+                                                     const float* __restrict__ bias,
+                                                     const float* __restrict__ in, int in_ld,
+                                                     float* __restrict__ out, int out_ld, int N,
+                                                     int K, int nvec, int act) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const float* w = W + (long long)n * K;
+  for (int v = 0; v < nvec; ++v) {
+    const float* x = in + (long long)v * in_ld;
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s = fmaf(w[k], x[k], s);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) out[(long long)v * out_ld + n] = act_apply(s + (bias ? bias[n] : 0.f), act, 0.f);
+  }
+}
+
+int matvec(const float* W, const float* bias, const float* in, int in_ld, float* out, int out_ld,
+           int N, int K, int nvec, int act, hipStream_t st) {
+  if (nvec <= 0) return PD_OK;
+  hipLaunchKernelGGL(matvec_kernel, dim3(cdiv(N, 4)), dim3(256), 0, st, W, bias, in, in_ld, out,
+                     out_ld, N, K, nvec, act);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// ---------------------------------------------------------------- embeddings
+__global__ void sinusoidal_kernel(const float* __restrict__ steps, float* __restrict__ out, int nvec,
+                                  int dim, float neg_e) {
+  const int half = dim / 2;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nvec * half) return;
+  int v = i / half, k = i - v * half;
+  float f = expf((float)k * neg_e);          // torch: exp(arange(half) * -e) in fp32
+  float arg = steps[v] * f;                  // long/float step * fp32 freq -> fp32
+  out[(long long)v * dim + k] = sinf(arg);
+  out[(long long)v * dim + half + k] = cosf(arg);
+}
+
+int sinusoidal_embed(const float* steps, float* out, int nvec, int dim, hipStream_t st) {
+  const int half = dim / 2;
+  float neg_e = -(float)(std::log(10000.0) / (half - 1));
+  int n = nvec * half;
+  if (n == 0) return PD_OK;
+  hipLaunchKernelGGL(sinusoidal_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, steps, out, nvec, dim,
+                     neg_e);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+__global__ void rev_steps_kernel(float* steps, int S, int B, int first) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < S * B) steps[i] = (float)(first - i / B);
+}
+
+int fill_reverse_steps(float* steps, int S, int B, int first, hipStream_t st) {
+  hipLaunchKernelGGL(rev_steps_kernel, dim3(cdiv(S * B, 256)), dim3(256), 0, st, steps, S, B, first);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+struct StepVals { float v[16]; };
+__global__ void steps_kernel(float* steps, StepVals vals, int S, int B) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < S * B) steps[i] = vals.v[i / B];
+}
+
+int fill_steps(float* steps, const float* host_vals, int S, int B, hipStream_t st) {
+  if (S > 16) { set_error("fill_steps: at most 16 steps"); return PD_ERR_ARG; }
+  StepVals sv{};
+  for (int j = 0; j < S; ++j) sv.v[j] = host_vals[j];
+  hipLaunchKernelGGL(steps_kernel, dim3(cdiv(S * B, 256)), dim3(256), 0, st, steps, sv, S, B);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// ---------------------------------------------------------------- transposes
+// in [B][R][Cc] -> out [B][Cc][R] via 32x32 LDS tiles
+__global__ void transpose_kernel(const float* __restrict__ in, float* __restrict__ out, int R, int Cc) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const float* src = in + (long long)b * R * Cc;
+  float* dst = out + (long long)b * R * Cc;
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    int r = r0 + i, c = c0 + threadIdx.x;
+    tile[i][threadIdx.x] = (r < R && c < Cc) ? src[(long long)r * Cc + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    int c = c0 + i, r = r0 + threadIdx.x;
+    if (r < R && c < Cc) dst[(long long)c * R + r] = tile[threadIdx.x][i];
+  }
+}
+
+int transpose_ct_to_tc(const float* in, float* out, int B, int C, int T, hipStream_t st) {
+  if (B * C * T == 0) return PD_OK;
+  hipLaunchKernelGGL(transpose_kernel, dim3(cdiv(T, 32), cdiv(C, 32), B), dim3(32, 8), 0, st, in, out,
+                     C, T);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+int transpose_tc_to_ct(const float* in, float* out, int B, int T, int C, hipStream_t st) {
+  if (B * C * T == 0) return PD_OK;
+  hipLaunchKernelGGL(transpose_kernel, dim3(cdiv(C, 32), cdiv(T, 32), B), dim3(32, 8), 0, st, in, out,
+                     T, C);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// ---------------------------------------------------------------- packing
+__global__ void pack_conv_kernel(float* dst, int ldw, int n_off, int k_off, int cpad,
+                                 const float* src, int Cout, int Cin, int taps) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)Cout * Cin * taps;
+  if (i >= total) return;
+  int tap = (int)(i % taps);
+  long long r = i / taps;
+  int ci = (int)(r % Cin);
+  int co = (int)(r / Cin);
+  dst[(long long)(n_off + co) * ldw + k_off + tap * cpad + ci] = src[i];
+}
+
+int pack_conv(float* dst, int ldw, int n_off, int k_off, int cpad, const float* src, int Cout, int Cin,
+              int taps, hipStream_t st) {
+  long long total = (long long)Cout * Cin * taps;
+  hipLaunchKernelGGL(pack_conv_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, dst, ldw, n_off, k_off,
+                     cpad, src, Cout, Cin, taps);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+__global__ void add_vec_kernel(float* d, const float* a, const float* b, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = a[i] + b[i];
+}
+
+int add_vectors(float* dst, const float* a, const float* b, int n, hipStream_t st) {
+  hipLaunchKernelGGL(add_vec_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dst, a, b, n);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+__global__ void wn_fold_kernel(float* w, const float* g, const float* v, int per_row) {
+  const int co = blockIdx.x;
+  const float* vr = v + (long long)co * per_row;
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < per_row; i += blockDim.x) s += (double)vr[i] * vr[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float scale = (float)((double)g[co] / sqrt(red[0]));
+  for (int i = threadIdx.x; i < per_row; i += blockDim.x) w[(long long)co * per_row + i] = vr[i] * scale;
+}
+
+int weight_norm_fold(float* w, const float* g, const float* v, int Cout, int per_row, hipStream_t st) {
+  hipLaunchKernelGGL(wn_fold_kernel, dim3(Cout), dim3(256), 0, st, w, g, v, per_row);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// ---------------------------------------------------------------- RNG fills
+__global__ void fill_uniform_kernel(float* out, long long n, unsigned long long seed, unsigned stream) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = philox_uniform(seed, (unsigned long long)i, stream);
+}
+__global__ void fill_normal_kernel(float* out, long long n, unsigned long long seed, unsigned stream) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = philox_normal(seed, (unsigned long long)i, stream);
+}
+
+int fill_uniform(float* out, long long n, unsigned long long seed, unsigned stream, hipStream_t st) {
+  if (n == 0) return PD_OK;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, out, n, seed, stream);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+int fill_normal(float* out, long long n, unsigned long long seed, unsigned stream, hipStream_t st) {
+  if (n == 0) return PD_OK;
+  hipLaunchKernelGGL(fill_normal_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, out, n, seed, stream);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+}  // namespace pd
+
+extern "C" const char* pd_last_error(void) { return pd::get_error(); }
+extern "C" int pd_version(void) { return 1; }

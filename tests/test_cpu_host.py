@@ -1,0 +1,112 @@
+"""CPU-only checks: the C-ABI library loads and exports what include/*.h declares,
+the host-side mirrors of the reference interfaces (names, shapes, schedules,
+registry) match the reference.  No device compute here."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from prodiff_amd import FastDiff, GaussianDiffusion, WaveNet, _lib, synth
+from prodiff_amd import schedules as S
+from prodiff_amd import vocoder as V
+from tests import golden_io as G
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "prodiff_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(pd_\w+|fd_\w+)\s*\(", txt, flags=re.M))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.lib()
+    declared = header_functions()
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.pd_version() == 1
+
+
+def test_null_arguments_fail_loudly():
+    lib = _lib.lib()
+    rc = lib.pd_wavenet_forward(None, None, None, None, None, 1, 1, None, 0, None)
+    assert rc == 1 and b"null" in lib.pd_last_error()
+    assert lib.fd_sample(None, None, None, None, None, None, 4, None, None, 0, None, 1, 1, None, 0, None) == 1
+
+
+def test_wavenet_state_dict_matches_reference_names():
+    for (M, H, L, C, cyc) in [(80, 256, 20, 256, 1), (64, 256, 20, 256, 5), (80, 32, 4, 64, 2)]:
+        net = WaveNet(M, H, L, C, cyc)
+        ref = synth.wavenet_param_shapes(M, H, L, C)
+        sd = net.state_dict()
+        assert list(sd) == list(ref)
+        assert all(tuple(sd[k].shape) == tuple(v) for k, v in ref.items())
+        assert len(net.ordered_params()) == 6 + 8 * L + 4
+
+
+def test_gaussian_diffusion_buffers_match_reference():
+    d = G.load("prodiff_t2_m80")
+    gd = GaussianDiffusion(80, WaveNet(80, 256, 20, 256, 1), timesteps=2, time_scale=1000, max_beta=40.0)
+    bufs = {k: v for k, v in gd.state_dict().items() if not k.startswith("denoise_fn")}
+    ref = G.prodiff_buffers(d)
+    assert set(bufs) == set(ref)
+    for k in ref:
+        np.testing.assert_allclose(bufs[k].numpy(), ref[k], rtol=1e-6, err_msg=k)
+
+
+def test_fastdiff_state_dict_matches_reference_names():
+    m = FastDiff()
+    ref = synth.fastdiff_param_shapes()
+    sd = m.state_dict()
+    assert set(sd) == set(ref)
+    assert all(tuple(sd[k].shape) == tuple(v) for k, v in ref.items())
+    m.remove_weight_norm()
+    ref2 = synth.fastdiff_param_shapes(weight_norm=False)
+    assert set(m.state_dict()) == set(ref2)
+    assert len(m._convs_in_order()) * 2 == 2 + 4 + 30 * 3 + 8 * 3 + 2
+
+
+def test_prodiff_schedules_match_reference():
+    s = G.load("schedules")
+    for ts in (1, 2, 4, 8, 100):
+        for mb in (40.0, 0.06):
+            betas = S.get_noise_schedule_list("vpsde", ts + 1, min_beta=0.1, max_beta=mb)
+            for k, v in S.diffusion_buffers(betas).items():
+                np.testing.assert_allclose(v, s[f"t{ts}_mb{mb}_{k}"], rtol=1e-6, atol=0, err_msg=k)
+
+
+def test_fastdiff_schedules_match_reference():
+    s = G.load("schedules")
+    at = S.fastdiff_train_alpha()
+    np.testing.assert_array_equal(at, s["fd_train_alpha"])
+    for n in (3, 4, 6, 8):
+        b, a, sg, st = S.fastdiff_infer_params(S.fastdiff_reverse_schedule(n), at)
+        np.testing.assert_allclose(a, s[f"fd_n{n}_alpha"], rtol=1e-6)
+        np.testing.assert_allclose(sg, s[f"fd_n{n}_sigma"], rtol=1e-6)
+        np.testing.assert_allclose(st, s[f"fd_n{n}_steps"], atol=1e-4)
+
+
+def test_vocoder_registry():
+    assert V.get_vocoder_cls("FastDiff") is V.FastDiff
+    assert V.get_vocoder_cls("fastdiff") is V.FastDiff
+    with pytest.raises(ValueError):
+        V.get_vocoder_cls("nope")
+
+
+def test_no_cpu_fallback_on_cpu_tensors():
+    net = WaveNet(80, 32, 2, 64, 1)
+    with pytest.raises(_lib.HipError):
+        net(torch.zeros(1, 1, 80, 4), torch.zeros(1), torch.zeros(1, 32, 4))
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, "prodiff_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith(".py"):
+                src = open(os.path.join(dp, f)).read()
+                assert "oracle" not in re.sub(r"#.*", "", src).replace('"""', ""), f
