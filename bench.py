@@ -1,0 +1,210 @@
+#!/usr/bin/env python
+"""ProDiff 2-iter + FastDiff 4-iter end-to-end synthesis throughput on MI355X.
+
+One step = one pass of the hot path over one batch per GPU: the ProDiff x0-predict
+sampler (WaveNet 20x256, M=80, 2 reverse steps) turns cond [B,861,256] into mel
+[B,861,80], the FastDiff sampler (base.yaml, 4 reverse steps) turns that into
+wav [B,220416] (10 s at 22.05 kHz, hop 256).  For N>1 every rank runs its own
+shard (weak scaling, no data-path collective) and the step ends with the
+point-to-point gather of mel+wav to rank 0 (RCCL over xGMI).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--frames T]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  Synthetic inputs and random-init weights of the
+reference architectures (no checkpoints or datasets offline).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "mel-frames/sec + audio RTF, 2-iter ProDiff + 4-iter FastDiff @1/2/4/8 GPU"
+FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
+    """Algorithmic FLOPs (2 x MAC) of ONE launch of each tagged kernel.
+    Tags used by several block sizes report the mean over their launches in one call."""
+    F = B * T
+    rows = [F * h for h in hops]
+    d_rows = [F * 64, F * 8, F]                       # DBlock output rates (L/4, L/32, L/256)
+    dblock = sum(2 * r * 32 * 96 * 2 + 2 * r * 32 * 128 for r in d_rows) / 9.0
+    return {
+        "wn_inproj": 2 * F * M * C,
+        "wn_gate": 2 * F * 2 * C * (3 * C + H),
+        "wn_resskip": 2 * F * 2 * C * C,
+        "wn_skiphead": 2 * F * C * C,
+        "wn_outproj_posterior": 2 * F * M * C,
+        "fd_first_conv": 2 * F * 256 * 32 * 7,
+        "fd_dblock": dblock,
+        "fd_kp_in": 2 * F * 64 * 80 * 5,
+        "fd_kp_res": 2 * F * 64 * 64 * 3,
+        "fd_kp_bias": 2 * F * 256 * 64 * 3,
+        "fd_kp_kernel": 2 * F * 6144 * 64 * 3,
+        "fd_upsample": sum(2 * r * 32 * 64 for r in rows) / 3.0,
+        "fd_lvc_preconv": sum(2 * r * 32 * 96 for r in rows) / 3.0,
+        "fd_lvc": sum(2 * r * 64 * 96 for r in rows) / 3.0,
+        "fd_final_update": 2 * F * 256 * 32 * 7,
+    }
+
+
+def step_flops(B, T):
+    """Whole-step algorithmic FLOPs: 2 x 26.43 + 4 x 56.98 MFLOP per frame."""
+    f = flops_per_launch(B, T)
+    per_prodiff_step = f["wn_inproj"] + 20 * (f["wn_gate"] + f["wn_resskip"]) + f["wn_skiphead"] + \
+        f["wn_outproj_posterior"]
+    per_fd_call = f["fd_first_conv"] + 9 * f["fd_dblock"] + 3 * (f["fd_kp_in"] + 6 * f["fd_kp_res"] +
+                                                             f["fd_kp_bias"] + 4 * f["fd_kp_kernel"] +
+                                                             f["fd_upsample"] + 4 * f["fd_lvc_preconv"] +
+                                                             4 * f["fd_lvc"]) + f["fd_final_update"]
+    return 2 * per_prodiff_step + 4 * per_fd_call
+
+
+def cpu_baseline(frames=200):
+    """The numpy oracle (a CPU port of the reference math, float64) on a bounded
+    sample: ONE utterance of `frames` mel frames through the same 2+4-iter pipeline."""
+    from oracle import oracle_fastdiff as OF
+    from oracle import oracle_prodiff as OP
+    from prodiff_amd import schedules as S
+    from prodiff_amd import synth
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+    except Exception:
+        cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    p = synth.synth_params(synth.wavenet_param_shapes(80, 256, 20, 256), 0)
+    bufs = OP.diffusion_buffers(OP.vpsde_betas(2, 40.0))
+    bufs["timesteps"] = 2
+    fp = OF.fold_weight_norm(synth.synth_params(synth.fastdiff_param_shapes(), 1))
+    b, a, s, st = S.fastdiff_infer_params(S.fastdiff_reverse_schedule(4), S.fastdiff_train_alpha())
+    cond = synth.synth_inputs(0, (1, frames, 256))
+    t0 = time.perf_counter()
+    mel = OP.prodiff_sample(p, bufs, cond, synth.synth_inputs(1, (1, 1, 80, frames), kind="uniform"),
+                            synth.synth_inputs(2, (2, 1, 1, 80, frames)))
+    OF.fastdiff_sample(fp, np.transpose(mel, (0, 2, 1)), synth.synth_inputs(3, (1, 1, frames * 256)),
+                       synth.synth_inputs(4, (3, 1, 1, frames * 256)), b, a, s, st)
+    dt = time.perf_counter() - t0
+    return {"value": round(frames / dt, 3), "unit": "mel-frames/s", "cores": int(cores), "kind": "port",
+            "sample": f"numpy float64 oracle, 1 utterance x {frames} frames ({frames * 256 / 22050:.2f} s audio), "
+                      f"2-iter ProDiff + 4-iter FastDiff, {dt:.1f} s wall",
+            "rtf": round(dt / (frames * 256 / 22050), 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=8, help="utterances per GPU (C3: 8)")
+    ap.add_argument("--frames", type=int, default=861, help="mel frames per utterance (10 s @ 22.05 kHz/256)")
+    ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline sample length (0 = skip)")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from prodiff_amd import _lib
+    from prodiff_amd.pipeline import HOP, SAMPLE_RATE, Synthesizer, gather_to_root
+
+    B, T = args.batch, args.frames
+    syn = Synthesizer.synthetic(dev, seed=0)
+    cond = torch.from_numpy(np.random.default_rng(1000 + rank).standard_normal((B, T, 256), dtype=np.float32)).to(dev)
+
+    def step(i):
+        mel, wav = syn(cond, seed=10_000 * rank + i)
+        if world > 1:
+            gather_to_root(mel)
+            gather_to_root(wav)
+        return mel, wav
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timing = not args.no_kernel_timing
+    if timing:
+        _lib.profile_enable(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        mel, wav = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kern = _lib.profile_summary() if timing else {}
+    _lib.profile_enable(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    assert torch.isfinite(wav).all() and torch.isfinite(mel).all()
+
+    frames = B * T * world * args.steps
+    audio_s = frames * HOP / SAMPLE_RATE
+    ms_step = dt / args.steps * 1e3
+    fl = flops_per_launch(B, T)
+    roofline, kernels = None, {}
+    if kern:
+        for tag, (cnt, ms) in sorted(kern.items(), key=lambda kv: -kv[1][1]):
+            tf = fl.get(tag, 0.0) * cnt / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+            kernels[tag] = {"launches": cnt, "ms_total": round(ms, 3), "avg_us": round(ms / cnt * 1e3, 2),
+                            "tflops": round(tf, 2)}
+        dom = max(kern.items(), key=lambda kv: kv[1][1])[0]
+        cnt, ms = kern[dom]
+        ach = fl[dom] * cnt / (ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                    "flop_per_launch": fl[dom], "avg_launch_us": round(ms / cnt * 1e3, 2),
+                    "share_of_step": round(ms / (dt * 1e3), 3)}
+    out = {
+        "metric": METRIC,
+        "value": round(frames / dt, 1),
+        "unit": "mel-frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (cond ~ N(0,1)); random-init weights of the reference architectures; on-device Philox draws",
+        "config": {"workload": f"C3: ProDiff 2-iter (WaveNet 20x256, M=80, vpsde max_beta 40) + FastDiff 4-iter "
+                               f"(base.yaml, hop 256), {B} x {T}-frame utterances per GPU",
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world} (utterance shards, "
+                                                                           f"RCCL gather to rank 0)"},
+        "rtf": round(dt / audio_s, 6),
+        "x_realtime": round(audio_s / dt, 1),
+        "model_tflops": round(step_flops(B, T) * world * args.steps / dt / 1e12, 2),
+        "roofline": roofline,
+        "kernels": kernels,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_frames > 0:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_frames)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

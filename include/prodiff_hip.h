@@ -41,6 +41,14 @@ extern "C" {
 const char* pd_last_error(void);
 int pd_version(void);
 
+/* Per-launch timing for benchmarks: when enabled, HIP events are recorded on the
+ * launch stream around every hot-path kernel (tagged by use, e.g. "fd_kp_kernel").
+ * pd_profile_enable(1) also clears previous records.  pd_profile_summary waits
+ * for the recorded events and writes "tag count total_ms" lines; it returns the
+ * buffer size needed (including the NUL), or -1 on error. */
+int pd_profile_enable(int on);
+int pd_profile_summary(char* buf, int buflen);
+
 /* ===================================================================== ProDiff
  * WaveNet denoiser -- replaces modules/decoder/wavenet.py:74-123 (WaveNet) as the
  * `denoise_fn` of GaussianDiffusion (modules/diffusion/prodiff.py:49-54,125).

@@ -37,6 +37,8 @@ _VP = C.c_void_p
 _SIGS = {
     "pd_last_error": (C.c_char_p, []),
     "pd_version": (C.c_int, []),
+    "pd_profile_enable": (C.c_int, [C.c_int]),
+    "pd_profile_summary": (C.c_int, [C.c_char_p, C.c_int]),
     "pd_wavenet_create": (C.c_int, [C.POINTER(pd_wavenet_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
     "pd_wavenet_destroy": (None, [_VP]),
     "pd_wavenet_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
@@ -101,6 +103,25 @@ def farr(vals):
 def stream_ptr(device=None):
     import torch
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def profile_enable(on=True):
+    check(lib().pd_profile_enable(1 if on else 0))
+
+
+def profile_summary():
+    """{tag: (launch count, total ms)} of the launches recorded since profile_enable."""
+    l = lib()
+    n = l.pd_profile_summary(None, 0)
+    if n < 0:
+        raise HipError(l.pd_last_error().decode())
+    buf = C.create_string_buffer(n + 16)
+    l.pd_profile_summary(buf, n + 16)
+    out = {}
+    for line in buf.value.decode().splitlines():
+        tag, cnt, ms = line.split()
+        out[tag] = (int(cnt), float(ms))
+    return out
 
 
 class Workspace:

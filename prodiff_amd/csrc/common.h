@@ -106,6 +106,16 @@ __device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t idx, uin
   return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
 }
 
+// Optional per-launch timing (pd_profile_enable): HIP events recorded on the
+// launch stream around every tagged kernel; read back after the timed region.
+struct ProfScope {
+  ProfScope(const char* tag, hipStream_t st);
+  ~ProfScope();
+  const char* tag_;
+  hipStream_t st_;
+  int slot_;
+};
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 

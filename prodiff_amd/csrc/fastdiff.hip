@@ -298,7 +298,7 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
       s.act = ACT_LRELU; s.alpha = 0.2f;
       add_seg(a, s);
     }
-    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE>(a, st)));
+    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_DBLOCK>(a, st, "fd_dblock")));
   }
   {
     GemmArgs a = make_gemm(B, Tout, CI, D.c1_w, 96, D.c1_b, t1, bso, CI);
@@ -307,7 +307,7 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
       s.act = ACT_LRELU; s.alpha = 0.2f;
       add_seg(a, s);
     }
-    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE>(a, st)));
+    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_DBLOCK>(a, st, "fd_dblock")));
   }
   {
     GemmArgs a = make_gemm(B, Tout, CI, D.c2_w, 128, D.c2_b, out, bso, CI);
@@ -317,7 +317,7 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
       add_seg(a, s);
     }
     add_seg(a, make_seg(in, bsi, CI, CI, 0, f));   // residual_dense on x[f i]
-    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE>(a, st)));
+    PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_DBLOCK>(a, st, "fd_dblock")));
   }
   return PD_OK;
 }
@@ -329,8 +329,11 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
   const int nb = m->nblocks;
   const long long L = (long long)Tc * m->hops[nb - 1];
   float* a0 = ws + W.a0;
+  {
+  ProfScope ps("fd_first_conv", st);
   hipLaunchKernelGGL(first_conv_kernel, dim3(cdiv(L, 32), B), dim3(256), 0, st, xa, m->first_w,
                      m->first_b, a0, (int)L);
+  }
   PD_LAUNCH_CHECK();
   // downsample chain: a0 -> d[0] -> ... -> d[nb-1]   (FastDiff_model.py:89-93)
   const float* cur = a0;
@@ -364,7 +367,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         add_seg(a, s);
       }
       a.act = ACT_LRELU; a.alpha = 0.1f;
-      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_IN>(a, st, "fd_kp_in")));
     }
     const float* src = ws + W.h0;
     float* rbuf[2] = {ws + W.ra, ws + W.rb};
@@ -374,7 +377,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(src, bsH, HK, HK, tap - 1));
       a.act = ACT_LRELU; a.alpha = 0.1f;
       if (j == 5) { a.res = ws + W.h0; a.res_bs = bsH; a.res_ld = HK; }   // h + R(h)
-      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_RES>(a, st, "fd_kp_res")));
       src = dst;
     }
     const float* hk = src;   // final h  [B][Tc][64]
@@ -382,11 +385,12 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       GemmArgs a = make_gemm(B, Tc, 2 * CI * NLY, K.kb_w, 3 * HK, K.kb_b, ws + W.Bf,
                              (long long)Tc * 2 * CI * NLY, 2 * CI * NLY);
       for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
-      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_BIAS>(a, st, "fd_kp_bias")));
     }
     // --- upsample (modules.py:205-206)
     {
       const int p = r / 2 + r % 2;
+      ProfScope ps("fd_upsample", st);
       hipLaunchKernelGGL(upsample_kernel, dim3(cdiv(Tin, 32), r, B), dim3(256), 0, st, x, K.up_w, K.up_b,
                          xn, (int)Tin, r, p);
       PD_LAUNCH_CHECK();
@@ -398,7 +402,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
                                K.kk_b + (size_t)i * KPERLAYER, ws + W.Kf, (long long)Tc * KPERLAYER,
                                KPERLAYER);
         for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
-        PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+        PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_KERNEL>(a, st, "fd_kp_kernel")));
       }
       {  // y = lrelu(conv_dil3^i(lrelu(x + a)) + b)
         const int dil = (int)std::pow(3, i);
@@ -410,10 +414,13 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
           add_seg(a, s);
         }
         a.act = ACT_LRELU; a.alpha = 0.2f;
-        PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE>(a, st)));
+        PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_LVC_PRECONV>(a, st, "fd_lvc_preconv")));
       }
+      {
+      ProfScope ps("fd_lvc", st);
       hipLaunchKernelGGL(lvc_kernel, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y, ws + W.Kf,
                          KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Tc, hop);
+      }
       PD_LAUNCH_CHECK();
     }
     x = xn;
@@ -614,9 +621,12 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
     const float ce = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
     const float den = sqrtf(1.f - beta[n]);
     const float sg = n > 0 ? sigma[n] : 0.f;
+    {
+    ProfScope ps("fd_final_update", st);
     hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w,
                        m->final_b, (float*)nullptr, wav, ce, den, sg,
                        noise ? noise + (size_t)j * B * L : (const float*)nullptr, seed, 0x10000u + j, L);
+    }
     PD_LAUNCH_CHECK();
   }
   return PD_OK;

@@ -39,6 +39,13 @@ struct Seg {
 
 enum Epi { EPI_STORE = 0, EPI_GATE = 1, EPI_RESSKIP = 2, EPI_POSTERIOR = 3 };
 
+// GEMM uses on the hot path (template ID -> distinct kernel symbol per use)
+enum GemmUse {
+  U_WN_INPROJ = 0, U_WN_GATE = 1, U_WN_RESSKIP = 2, U_WN_SKIP = 3, U_WN_OUT = 4, U_WN_POSTERIOR = 5,
+  U_FD_DBLOCK = 10, U_FD_KP_IN = 11, U_FD_KP_RES = 12, U_FD_KP_BIAS = 13, U_FD_KP_KERNEL = 14,
+  U_FD_LVC_PRECONV = 15
+};
+
 struct GemmArgs {
   int B, T, N, nseg;
   Seg seg[MAX_SEGS];
@@ -68,7 +75,8 @@ struct GemmArgs {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI>
+// ID only makes each hot-path use a distinct symbol in rocprof traces (DESIGN.md lists them).
+template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI, int ID>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
   constexpr int BM = 32 * WM_T * WAVES_M;
@@ -256,8 +264,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
 // Host-side validation + launch.  Returns PD_OK or an error code.
 int validate_gemm(const GemmArgs& a);
 
-template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI>
-int launch_gemm(const GemmArgs& a, hipStream_t st) {
+template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI, int ID>
+int launch_gemm(const GemmArgs& a, hipStream_t st, const char* tag) {
   PD_TRY(validate_gemm(a));
   constexpr int BM = 32 * WM_T * WAVES_M;
   constexpr int BN = 32 * WN_T * WAVES_N;
@@ -269,7 +277,10 @@ int launch_gemm(const GemmArgs& a, hipStream_t st) {
     set_error("paired gemm needs N == 2*half, half % 32 == 0");
     return PD_ERR_ARG;
   }
-  hipLaunchKernelGGL((gemm_f32_kernel<WM_T, WN_T, WAVES_M, WAVES_N, EPI>), grid, dim3(256), 0, st, a);
+  {
+    ProfScope ps(tag, st);
+    hipLaunchKernelGGL((gemm_f32_kernel<WM_T, WN_T, WAVES_M, WAVES_N, EPI, ID>), grid, dim3(256), 0, st, a);
+  }
   PD_LAUNCH_CHECK();
   return PD_OK;
 }

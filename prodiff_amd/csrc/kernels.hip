@@ -1,6 +1,9 @@
 // Small utility kernels + error plumbing.
 #include <cmath>
+#include <cstdio>
 #include <cstring>
+#include <map>
+#include <vector>
 
 #include "gemm.h"
 #include "kernels.h"
@@ -228,7 +231,64 @@ int fill_normal(float* out, long long n, unsigned long long seed, unsigned strea
   return PD_OK;
 }
 
+// ---------------------------------------------------------------- profiling
+namespace {
+struct ProfRec { const char* tag; int slot; };
+bool g_prof_on = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pool;
+std::vector<ProfRec> g_recs;
+}  // namespace
+
+ProfScope::ProfScope(const char* tag, hipStream_t st) : tag_(tag), st_(st), slot_(-1) {
+  if (!g_prof_on || !tag) return;
+  slot_ = (int)g_recs.size();
+  if ((size_t)slot_ >= g_pool.size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { slot_ = -1; return; }
+    g_pool.push_back({a, b});
+  }
+  g_recs.push_back({tag, slot_});
+  (void)hipEventRecord(g_pool[slot_].first, st_);
+}
+
+ProfScope::~ProfScope() {
+  if (slot_ >= 0) (void)hipEventRecord(g_pool[slot_].second, st_);
+}
+
 }  // namespace pd
+
+extern "C" int pd_profile_enable(int on) {
+  pd::g_prof_on = on != 0;
+  pd::g_recs.clear();
+  return PD_OK;
+}
+
+// Waits for every recorded launch, then writes "tag count total_ms\n" lines
+// (sorted by tag) into buf.  Returns the number of bytes needed (incl. NUL).
+extern "C" int pd_profile_summary(char* buf, int buflen) {
+  std::map<std::string, std::pair<int, double>> agg;
+  for (auto& r : pd::g_recs) {
+    auto& ev = pd::g_pool[r.slot];
+    if (hipEventSynchronize(ev.second) != hipSuccess) { pd::set_error("hipEventSynchronize failed"); return -1; }
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev.first, ev.second) != hipSuccess) { pd::set_error("hipEventElapsedTime failed"); return -1; }
+    auto& a = agg[r.tag];
+    a.first += 1;
+    a.second += ms;
+  }
+  std::string out;
+  char line[256];
+  for (auto& kv : agg) {
+    snprintf(line, sizeof line, "%s %d %.6f\n", kv.first.c_str(), kv.second.first, kv.second.second);
+    out += line;
+  }
+  if (buf && buflen > 0) {
+    size_t n = std::min((size_t)buflen - 1, out.size());
+    memcpy(buf, out.data(), n);
+    buf[n] = 0;
+  }
+  return (int)out.size() + 1;
+}
 
 extern "C" const char* pd_last_error(void) { return pd::get_error(); }
 extern "C" int pd_version(void) { return 1; }

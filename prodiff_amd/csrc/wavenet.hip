@@ -81,7 +81,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     GemmArgs a = make_gemm(B, T, C, h->Win, h->ldw_in, h->b_in, x, BTs * C, C);
     add_seg(a, make_seg(xin, BTs * M, M, M, 0));
     a.act = ACT_RELU;
-    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_WN_INPROJ>(a, st, "wn_inproj")));
   }
   for (int l = 0; l < Ly; ++l) {
     const int dil = 1 << (l % h->cyc);
@@ -96,7 +96,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       }
       add_seg(a, make_seg(cond, BTs * H, H, H, 0));
       a.half = C;
-      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_GATE>(a, st)));
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_GATE, U_WN_GATE>(a, st, "wn_gate")));
     }
     {  // o = W_out g + b ; x = (x + o[:C]) / sqrt2 ; skip += o[C:]   (wavenet.py:69-72)
       GemmArgs a = make_gemm(B, T, 2 * C, h->Wl2 + (size_t)l * 2 * C * C, C, h->bl2 + (size_t)l * 2 * C,
@@ -105,7 +105,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       a.half = C;
       a.out2 = skip; a.out2_bs = BTs * C; a.out2_ld = C;
       a.flag = (l == 0);
-      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_RESSKIP>(a, st)));
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_RESSKIP, U_WN_RESSKIP>(a, st, "wn_resskip")));
     }
   }
   {  // hs = relu(W_skip (sum skip / sqrt(L)) + b)   (wavenet.py:119-121)
@@ -114,7 +114,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     s.scale = 1.0f / sqrtf((float)Ly);
     add_seg(a, s);
     a.act = ACT_RELU;
-    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_WN_SKIP>(a, st, "wn_skiphead")));
   }
   return PD_OK;
 }
@@ -234,7 +234,7 @@ int pd_wavenet_forward(const pd_wavenet* h, const float* spec, const float* step
   const long long BTs = T;
   GemmArgs a = make_gemm(B, T, h->M, h->Wo, h->C, h->bo, ws + Lw.outT, BTs * h->M, h->M);
   add_seg(a, make_seg(ws + Lw.hs, BTs * h->C, h->C, h->C, 0));
-  PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE>(a, st)));
+  PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_WN_OUT>(a, st, "wn_outproj")));
   PD_TRY(transpose_tc_to_ct(ws + Lw.outT, out, B, T, h->M, st));
   return PD_OK;
 }
@@ -273,7 +273,7 @@ int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1
     a.noise = noise ? noise + (size_t)j * BTM : nullptr;
     a.noise_bs = BTs * M; a.noise_ld = M;
     a.seed = seed; a.stream_id = (unsigned)j;
-    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_POSTERIOR>(a, st)));
+    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_POSTERIOR, U_WN_POSTERIOR>(a, st, "wn_outproj_posterior")));
   }
   return PD_OK;
 }

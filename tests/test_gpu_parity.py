@@ -83,6 +83,8 @@ def test_prodiff_sample_golden(name):
 def test_prodiff_forward_infer_api():
     """forward(cond, infer=True) -- the teacher's call (prodiff_teacher.py:167) -- on-device draws."""
     net = WaveNet(80, 256, 20, 256, 1)
+    p = synth.synth_params(synth.wavenet_param_shapes(80, 256, 20, 256), 4)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})   # (reference zero-inits output_projection)
     gd = GaussianDiffusion(80, net, timesteps=2, max_beta=40.0).to(DEV)
     cond = tt(synth.synth_inputs(7, (2, 50, 256)))
     torch.manual_seed(0)
