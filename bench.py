@@ -29,6 +29,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "mel-frames/sec + audio RTF, 2-iter ProDiff + 4-iter FastDiff @1/2/4/8 GPU"
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+BF16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -54,6 +55,8 @@ def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_upsample": sum(2 * r * 32 * 64 for r in rows) / 3.0,
         "fd_lvc_preconv": sum(2 * r * 32 * 96 for r in rows) / 3.0,
         "fd_lvc": sum(2 * r * 64 * 96 for r in rows) / 3.0,
+        # fused pre-conv + LVC, launched for the hop >= 64 blocks only (bf16 path)
+        "fd_lvc_fused": sum(2 * r * 32 * 96 + 2 * r * 64 * 96 for r in rows[1:]) / 2.0,
         "fd_final_update": 2 * F * 256 * 32 * 7,
     }
 
@@ -108,6 +111,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="utterances per GPU (C3: 8)")
     ap.add_argument("--frames", type=int, default=861, help="mel frames per utterance (10 s @ 22.05 kHz/256)")
     ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline sample length (0 = skip)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute dtype (C3 is specified in bf16; fp32 is the exact parity path)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
 
@@ -123,7 +128,7 @@ def main():
     from prodiff_amd.pipeline import HOP, SAMPLE_RATE, Synthesizer, gather_to_root
 
     B, T = args.batch, args.frames
-    syn = Synthesizer.synthetic(dev, seed=0)
+    syn = Synthesizer.synthetic(dev, seed=0, dtype=args.dtype)
     cond = torch.from_numpy(np.random.default_rng(1000 + rank).standard_normal((B, T, 256), dtype=np.float32)).to(dev)
 
     def step(i):
@@ -170,8 +175,9 @@ def main():
         dom = max(kern.items(), key=lambda kv: kv[1][1])[0]
         cnt, ms = kern[dom]
         ach = fl[dom] * cnt / (ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": None,
+        peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
+        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
                     "flop_per_launch": fl[dom], "avg_launch_us": round(ms / cnt * 1e3, 2),
                     "share_of_step": round(ms / (dt * 1e3), 3)}
     out = {
@@ -185,7 +191,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": args.dtype,
         "data": "synthetic (cond ~ N(0,1)); random-init weights of the reference architectures; on-device Philox draws",
         "config": {"workload": f"C3: ProDiff 2-iter (WaveNet 20x256, M=80, vpsde max_beta 40) + FastDiff 4-iter "
                                f"(base.yaml, hop 256), {B} x {T}-frame utterances per GPU",

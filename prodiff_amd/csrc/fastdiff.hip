@@ -31,6 +31,7 @@ struct fd_model {
   int hops[4];
   int dtype;
   float* pool = nullptr;
+  __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
   // step MLP
   float *fc1_w, *fc1_b, *fc2_w, *fc2_b;
   float *first_w, *first_b;          // [32][7]
@@ -122,9 +123,10 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
 
 // x += a + sigmoid(o[:32]) * tanh(o[32:]),  o[t] = Bias_l + K_l . [y[t-1]; y[t]; y[t+1]]
 // one block per frame l (modules.py:208-217, 220-253).  Kf rows: o*96 + tap*32 + ci.
+template <typename KT>
 __global__ __launch_bounds__(256) void lvc_kernel(float* __restrict__ x, const float* __restrict__ a,
                                                   const float* __restrict__ y,
-                                                  const float* __restrict__ Kf, int kf_ld,
+                                                  const KT* __restrict__ Kf, int kf_ld,
                                                   const float* __restrict__ Bf, int bf_ld, int Tc,
                                                   int hop) {
   __shared__ float ks[64 * 97];
@@ -132,10 +134,10 @@ __global__ __launch_bounds__(256) void lvc_kernel(float* __restrict__ x, const f
   __shared__ float ys[34 * 33];
   const int g = blockIdx.x, b = g / Tc, l = g - b * Tc, tid = threadIdx.x;
   const long long L = (long long)Tc * hop;
-  const float* kf = Kf + (long long)g * kf_ld;
+  const KT* kf = Kf + (long long)g * kf_ld;
   for (int i = tid; i < 64 * 96; i += 256) {
     int o = i / 96, qq = i - o * 96;
-    ks[o * 97 + qq] = kf[i];
+    ks[o * 97 + qq] = (float)kf[i];
   }
   if (tid < 64) bs[tid] = Bf[(long long)g * bf_ld + tid];
   const int c = tid & 31, sg = tid >> 5;
@@ -164,6 +166,108 @@ __global__ __launch_bounds__(256) void lvc_kernel(float* __restrict__ x, const f
       }
       long long idx = ((long long)b * L + (long long)l * hop + s0 + s) * CI + c;
       x[idx] = x[idx] + a[idx] + sigmoidf_(og) * tanhf(of);
+    }
+  }
+}
+
+// Fused LVC layer on bf16 MFMA (hop >= 64), one launch per layer (modules.py:208-217, 220-253):
+//   u = lrelu_.2(x + a); y = lrelu_.2(conv3_dil(u) + bc); o = Bf_l + K_l . [y(t-1); y(t); y(t+1)]
+//   x <- x + a + sigmoid(o[:32]) * tanh(o[32:])
+// Block = TS consecutive samples of ONE frame (so one 64x96 kernel K_l), TS/32 waves.
+// u (TS + 2 + 2 dil rows) and y (TS + 2 rows) live only in LDS; K_l fragments are
+// read straight from the frame-major kernel tensor (16 B per lane per k-step).
+template <int TS>
+__global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
+    float* __restrict__ x, const float* __restrict__ a, const __bf16* __restrict__ Kf, int kf_ld,
+    const float* __restrict__ Bf, int bf_ld, const __bf16* __restrict__ Wc, const float* __restrict__ bc,
+    int Tc, int hop, int dil) {
+  constexpr int NT = TS * 2;
+  constexpr int LD = 40;                     // bf16 per staged row: 32 + 8 pad (80 B, conflict-free b128 reads)
+  constexpr int NMT = (TS + 2 + 31) / 32;    // pre-conv row tiles (TS + 2 rows of y)
+  constexpr int YROWS = NMT * 32;
+  constexpr int UROWS = YROWS + 2 * 27;      // + 2*dil, dil <= 27 (3^3)
+  __shared__ __attribute__((aligned(16))) __bf16 U[UROWS * LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Y[YROWS * LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int per_frame = hop / TS;
+  const int frame = blockIdx.x / per_frame, sub = blockIdx.x - frame * per_frame;
+  const int b = frame / Tc, l = frame - b * Tc;
+  const long long Lh = (long long)Tc * hop;
+  const long long t0 = (long long)l * hop + (long long)sub * TS;
+  const long long base = (long long)b * Lh;
+
+  // 1. U[r] = lrelu(x + a) at t = t0 - 1 - dil + r, zero outside the utterance (conv padding)
+  const int nU = YROWS + 2 * dil;
+  for (int i = tid; i < nU * 8; i += NT) {
+    const int r = i >> 3, q = (i & 7) * 4;
+    const long long t = t0 - 1 - dil + r;
+    bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+    if (t >= 0 && t < Lh) {
+      const float4 xv = *reinterpret_cast<const float4*>(x + (base + t) * CI + q);
+      const float4 av = *reinterpret_cast<const float4*>(a + (base + t) * CI + q);
+      float u0 = xv.x + av.x, u1 = xv.y + av.y, u2 = xv.z + av.z, u3 = xv.w + av.w;
+      u0 = u0 >= 0.f ? u0 : 0.2f * u0; u1 = u1 >= 0.f ? u1 : 0.2f * u1;
+      u2 = u2 >= 0.f ? u2 : 0.2f * u2; u3 = u3 >= 0.f ? u3 : 0.2f * u3;
+      v = bf16x4{(__bf16)u0, (__bf16)u1, (__bf16)u2, (__bf16)u3};
+    }
+    *reinterpret_cast<bf16x4*>(U + r * LD + q) = v;
+  }
+  __syncthreads();
+
+  // 2. pre-conv (32 -> 32, k3, dilation dil): Y[r] = lrelu(W_c . [U(r); U(r+dil); U(r+2dil)] + b)
+  {
+    bf16x8 wf[6];
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const bf16x8*>(Wc + r32 * 96 + kk * 16 + h * 8);
+    const float bias = bc[r32];
+    for (int mt = wave; mt < NMT; mt += NT / 64) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) {
+        const int tap = kk >> 1, ci0 = (kk & 1) * 16;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(U + (mt * 32 + r32 + tap * dil) * LD + ci0 + h * 8);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wf[kk], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int r = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const long long t = t0 - 1 + r;
+        float y = acc[reg] + bias;
+        y = y >= 0.f ? y : 0.2f * y;
+        if (t < 0 || t >= Lh) y = 0.f;        // the LVC zero-pads y at utterance edges
+        Y[r * LD + r32] = (__bf16)y;
+      }
+    }
+  }
+  __syncthreads();
+
+  // 3. location-variable conv with this frame's kernel: rows = TS samples, cols = 64
+  //    outputs as a gate tile (o = c) and a filter tile (o = 32 + c) in the same lanes.
+  {
+    const __bf16* kf = Kf + (long long)frame * kf_ld;
+    const float* bfp = Bf + (long long)frame * bf_ld;
+    const int mt = wave;
+    f32x16 ag, afl;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { ag[r] = 0.f; afl[r] = 0.f; }
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      const int tap = kk >> 1, ci0 = (kk & 1) * 16;
+      const bf16x8 yf = *reinterpret_cast<const bf16x8*>(Y + (mt * 32 + r32 + tap) * LD + ci0 + h * 8);
+      const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kf + r32 * 96 + kk * 16 + h * 8);
+      const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kf + (32 + r32) * 96 + kk * 16 + h * 8);
+      ag = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf, kg, ag, 0, 0, 0);
+      afl = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf, kl, afl, 0, 0, 0);
+    }
+    const float bg = bfp[r32], bl = bfp[32 + r32];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int s = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      const long long idx = (base + t0 + s) * CI + r32;
+      x[idx] = x[idx] + a[idx] + sigmoidf_(ag[reg] + bg) * tanhf(afl[reg] + bl);
     }
   }
 }
@@ -402,24 +506,42 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
                                K.kk_b + (size_t)i * KPERLAYER, ws + W.Kf, (long long)Tc * KPERLAYER,
                                KPERLAYER);
         for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
+        a.out_bf16 = m->pool_bf != nullptr;   // bf16 kernels halve the K_l round trip
         PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_KERNEL>(a, st, "fd_kp_kernel")));
       }
-      {  // y = lrelu(conv_dil3^i(lrelu(x + a)) + b)
-        const int dil = (int)std::pow(3, i);
-        GemmArgs a = make_gemm(B, (int)Tout, CI, K.cv_w[i], 96, K.cv_b[i], ws + W.y, Tout * CI, CI);
-        for (int tap = 0; tap < 3; ++tap) {
-          Seg s = make_seg(xn, Tout * CI, CI, CI, (tap - 1) * dil);
-          s.add_ten = ad;
-          s.act = ACT_LRELU; s.alpha = 0.2f;
-          add_seg(a, s);
+      const int dil = (int)std::pow(3, i);
+      const bool bf = m->pool_bf != nullptr;
+      if (bf && hop % 64 == 0) {
+        // one fused launch: pre-conv + LVC + gate (bf16 MFMA)
+        ProfScope ps("fd_lvc_fused", st);
+        const __bf16* Kb = reinterpret_cast<const __bf16*>(ws + W.Kf);
+        const __bf16* Wc = lookup_bf16(K.cv_w[i]);
+        if (hop % 128 == 0)
+          hipLaunchKernelGGL(lvc_fused_bf16_kernel<128>, dim3(B * Tc * (hop / 128)), dim3(256), 0, st, xn, ad, Kb,
+                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
+        else
+          hipLaunchKernelGGL(lvc_fused_bf16_kernel<64>, dim3(B * Tc * (hop / 64)), dim3(128), 0, st, xn, ad, Kb,
+                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
+      } else {
+        {  // y = lrelu(conv_dil3^i(lrelu(x + a)) + b)
+          GemmArgs a = make_gemm(B, (int)Tout, CI, K.cv_w[i], 96, K.cv_b[i], ws + W.y, Tout * CI, CI);
+          for (int tap = 0; tap < 3; ++tap) {
+            Seg sg = make_seg(xn, Tout * CI, CI, CI, (tap - 1) * dil);
+            sg.add_ten = ad;
+            sg.act = ACT_LRELU; sg.alpha = 0.2f;
+            add_seg(a, sg);
+          }
+          a.act = ACT_LRELU; a.alpha = 0.2f;
+          PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_LVC_PRECONV>(a, st, "fd_lvc_preconv")));
         }
-        a.act = ACT_LRELU; a.alpha = 0.2f;
-        PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_LVC_PRECONV>(a, st, "fd_lvc_preconv")));
-      }
-      {
-      ProfScope ps("fd_lvc", st);
-      hipLaunchKernelGGL(lvc_kernel, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y, ws + W.Kf,
-                         KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Tc, hop);
+        ProfScope ps("fd_lvc", st);
+        if (bf)
+          hipLaunchKernelGGL(lvc_kernel<__bf16>, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y,
+                             reinterpret_cast<const __bf16*>(ws + W.Kf), KPERLAYER, ws + W.Bf + i * 2 * CI,
+                             2 * CI * NLY, Tc, hop);
+        else
+          hipLaunchKernelGGL(lvc_kernel<float>, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y, ws + W.Kf,
+                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Tc, hop);
       }
       PD_LAUNCH_CHECK();
     }
@@ -436,7 +558,7 @@ extern "C" {
 
 int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* stream, fd_model** out) {
   PD_CHECK_ARG(dims && params && out, "null pointer");
-  PD_CHECK_ARG(dtype == PD_DTYPE_F32, "only PD_DTYPE_F32 is implemented for the FastDiff path");
+  PD_CHECK_ARG(dtype == PD_DTYPE_F32 || dtype == PD_DTYPE_BF16, "dtype must be PD_DTYPE_F32 or PD_DTYPE_BF16");
   PD_CHECK_ARG(dims->audio_channels == 1 && dims->inner_channels == CI && dims->cond_channels == CC &&
                    dims->lvc_layers_each_block == NLY && dims->lvc_kernel_size == 3 &&
                    dims->kpnet_hidden_channels == HK && dims->kpnet_conv_size == 3 &&
@@ -480,7 +602,7 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   size_t off = 0;
   std::vector<size_t> offs;
   for (auto& p : plan) { offs.push_back(off); off += (p.second + 63) / 64 * 64; }
-  if (hipMalloc(&m->pool, off * sizeof(float)) != hipSuccess) {
+  if (hipMalloc((void**)&m->pool, off * sizeof(float)) != hipSuccess) {
     delete m; set_error("hipMalloc failed for FastDiff weights"); return PD_ERR_HIP;
   }
   for (size_t i = 0; i < plan.size(); ++i) *plan[i].first = m->pool + offs[i];
@@ -549,19 +671,33 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
       PD_TRY(cp(m->final_b, b, 1));
     }
     if (p != FD_NUM_PARAMS(m->nblocks)) { set_error("fd_create: parameter count mismatch"); return PD_ERR_ARG; }
+    if (dtype == PD_DTYPE_BF16) {
+      PD_HIP(hipMalloc((void**)&m->pool_bf, off * sizeof(__bf16)));
+      PD_TRY(convert_f32_bf16(m->pool, m->pool_bf, (long long)off, st));
+      register_bf16_pool(m->pool, off, m->pool_bf);
+    }
     return PD_OK;
   };
   for (int i = 0; i < FD_NUM_PARAMS(m->nblocks); ++i)
-    if (!params[i]) { hipFree(m->pool); delete m; set_error("null parameter " + std::to_string(i)); return PD_ERR_ARG; }
+    if (!params[i]) { (void)hipFree(m->pool); delete m; set_error("null parameter " + std::to_string(i)); return PD_ERR_ARG; }
   int rc = run();
-  if (rc != PD_OK) { hipFree(m->pool); delete m; return rc; }
+  if (rc != PD_OK) {
+    (void)hipFree(m->pool);
+    if (m->pool_bf) (void)hipFree(m->pool_bf);
+    delete m;
+    return rc;
+  }
   *out = m;
   return PD_OK;
 }
 
 void fd_destroy(fd_model* m) {
   if (!m) return;
-  hipFree(m->pool);
+  if (m->pool_bf) {
+    unregister_bf16_pool(m->pool);
+    (void)hipFree(m->pool_bf);
+  }
+  (void)hipFree(m->pool);
   delete m;
 }
 

@@ -14,6 +14,8 @@
 // K is staged through LDS 32 deep, double-buffered, the next chunk's global
 // loads in flight under the current chunk's MFMAs.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace pd {
@@ -49,7 +51,9 @@ enum GemmUse {
 struct GemmArgs {
   int B, T, N, nseg;
   Seg seg[MAX_SEGS];
-  const float* W;           // packed [N][ldw]
+  const float* W;           // packed fp32 [N][ldw]  (fp32 path)
+  const __bf16* Wb;         // packed bf16 [N][ldw]  (bf16 path; selects it when non-null)
+  int out_bf16;             // STORE: write `out` as bf16
   int ldw;                  // = sum of seg kpad
   const float* bias;        // [N]
   float* out;
@@ -74,20 +78,28 @@ struct GemmArgs {
 };
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+// TW = float : v_mfma_f32_32x32x2_f32 (exact fp32, the parity path)
+// TW = __bf16: v_mfma_f32_32x32x16_bf16 (weights bf16, activations rounded to bf16
+//              when staged into LDS, fp32 accumulate/epilogue)
 // ID only makes each hot-path use a distinct symbol in rocprof traces (DESIGN.md lists them).
-template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI, int ID>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
+template <typename TW, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI, int ID>
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
+  constexpr bool BF = !std::is_same<TW, float>::value;
   constexpr int BM = 32 * WM_T * WAVES_M;
   constexpr int BN = 32 * WN_T * WAVES_N;
   constexpr int BK = GEMM_BK;
-  constexpr int LDL = BK + 4;  // padded LDS row (conflict-free ds_read_b128)
+  // padded LDS rows: 144 B (fp32) / 80 B (bf16) keep the ds_read_b128 fragment reads
+  // conflict-free (16-B slot = 9r (fp32) or 5r (bf16) + const mod 16)
+  constexpr int LDL = BF ? BK + 8 : BK + 4;
   constexpr bool PAIRED = (EPI == EPI_GATE || EPI == EPI_RESSKIP);
   static_assert(!PAIRED || (WN_T == 2 && WAVES_N == 1), "paired epilogue layout");
   constexpr int A_IT = BM / 32, B_IT = BN / 32;
 
-  __shared__ __attribute__((aligned(16))) float smem[2][(BM + BN) * LDL];
+  __shared__ __attribute__((aligned(16))) TW smem[2][(BM + BN) * LDL];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WAVES_M, wn = wave / WAVES_M;
@@ -106,17 +118,20 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
     a_b[i] = b;
     a_t[i] = R - b * a.T;
   }
-  const float* w_ptr[B_IT];
+  const TW* w_ptr[B_IT];
   bool w_ok[B_IT];
 #pragma unroll
   for (int i = 0; i < B_IT; ++i) {
     int local = (tid >> 3) + 32 * i;
     int n = PAIRED ? (local < BN / 2 ? nb + local : a.half + nb + local - BN / 2) : nb + local;
     w_ok[i] = n < a.N;
-    w_ptr[i] = a.W + (long long)(w_ok[i] ? n : 0) * a.ldw + q4;
+    const TW* W;
+    if constexpr (BF) W = a.Wb; else W = a.W;
+    w_ptr[i] = W + (long long)(w_ok[i] ? n : 0) * a.ldw + q4;
   }
 
-  float4 ra[A_IT], rb[B_IT];
+  float4 ra[A_IT];
+  typename std::conditional<BF, uint2, float4>::type rb[B_IT];
   auto load_chunk = [&](int s, int c0, int kg) {
     const Seg& sg = a.seg[s];
     const int c = c0 + q4;
@@ -144,18 +159,32 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
       ra[i] = v;
     }
 #pragma unroll
-    for (int i = 0; i < B_IT; ++i)
-      rb[i] = w_ok[i] ? *reinterpret_cast<const float4*>(w_ptr[i] + kg) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < B_IT; ++i) {
+      if constexpr (BF)
+        rb[i] = w_ok[i] ? *reinterpret_cast<const uint2*>(w_ptr[i] + kg) : make_uint2(0u, 0u);
+      else
+        rb[i] = w_ok[i] ? *reinterpret_cast<const float4*>(w_ptr[i] + kg) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   auto store_chunk = [&](int buf) {
-    float* As = smem[buf];
-    float* Bs = smem[buf] + BM * LDL;
+    TW* As = smem[buf];
+    TW* Bs = smem[buf] + BM * LDL;
 #pragma unroll
-    for (int i = 0; i < A_IT; ++i)
-      *reinterpret_cast<float4*>(As + ((tid >> 3) + 32 * i) * LDL + q4) = ra[i];
+    for (int i = 0; i < A_IT; ++i) {
+      TW* dst = As + ((tid >> 3) + 32 * i) * LDL + q4;
+      if constexpr (BF) {
+        bf16x4 v = {(__bf16)ra[i].x, (__bf16)ra[i].y, (__bf16)ra[i].z, (__bf16)ra[i].w};
+        *reinterpret_cast<bf16x4*>(dst) = v;
+      } else {
+        *reinterpret_cast<float4*>(dst) = ra[i];
+      }
+    }
 #pragma unroll
-    for (int i = 0; i < B_IT; ++i)
-      *reinterpret_cast<float4*>(Bs + ((tid >> 3) + 32 * i) * LDL + q4) = rb[i];
+    for (int i = 0; i < B_IT; ++i) {
+      TW* dst = Bs + ((tid >> 3) + 32 * i) * LDL + q4;
+      if constexpr (BF) *reinterpret_cast<uint2*>(dst) = rb[i];
+      else *reinterpret_cast<float4*>(dst) = rb[i];
+    }
   };
 
   f32x16 acc[WM_T][WN_T];
@@ -179,34 +208,55 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
       if (c0 >= a.seg[s].kpad) { ++s; c0 = 0; }
       load_chunk(s, c0, (ch + 1) * BK);
     }
-    const float* As = smem[ch & 1];
-    const float* Bs = smem[ch & 1] + BM * LDL;
-    float af[WM_T][16], bf[WN_T][16];
+    const TW* As = smem[ch & 1];
+    const TW* Bs = smem[ch & 1] + BM * LDL;
+    if constexpr (BF) {
+      // 32x32x16: lane (r, h) holds A[r][8h + j], B[8h + j][r]; two k-steps per 32-deep chunk
 #pragma unroll
-    for (int i = 0; i < WM_T; ++i) {
-      const float* p = As + (wm * 32 * WM_T + i * 32 + r32) * LDL + h * 16;
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[WM_T], bfr[WN_T];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
-        af[i][4 * q] = v.x; af[i][4 * q + 1] = v.y; af[i][4 * q + 2] = v.z; af[i][4 * q + 3] = v.w;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < WN_T; ++j) {
-      const float* p = Bs + (wn * 32 * WN_T + j * 32 + r32) * LDL + h * 16;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
-        bf[j][4 * q] = v.x; bf[j][4 * q + 1] = v.y; bf[j][4 * q + 2] = v.z; bf[j][4 * q + 3] = v.w;
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk)
-#pragma unroll
-      for (int i = 0; i < WM_T; ++i)
+        for (int i = 0; i < WM_T; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 32 * WM_T + i * 32 + r32) * LDL + kk * 16 + h * 8);
 #pragma unroll
         for (int j = 0; j < WN_T; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bf[j][kk], acc[i][j], 0, 0, 0);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 32 * WN_T + j * 32 + r32) * LDL + kk * 16 + h * 8);
+#pragma unroll
+        for (int i = 0; i < WM_T; ++i)
+#pragma unroll
+          for (int j = 0; j < WN_T; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // 32x32x2 f32: MFMA kk pairs k = kk (lanes h=0) with k = 16 + kk (h=1), so each
+      // lane reads 16 contiguous floats per operand
+      float af[WM_T][16], bf[WN_T][16];
+#pragma unroll
+      for (int i = 0; i < WM_T; ++i) {
+        const float* p = As + (wm * 32 * WM_T + i * 32 + r32) * LDL + h * 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
+          af[i][4 * q] = v.x; af[i][4 * q + 1] = v.y; af[i][4 * q + 2] = v.z; af[i][4 * q + 3] = v.w;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < WN_T; ++j) {
+        const float* p = Bs + (wn * 32 * WN_T + j * 32 + r32) * LDL + h * 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
+          bf[j][4 * q] = v.x; bf[j][4 * q + 1] = v.y; bf[j][4 * q + 2] = v.z; bf[j][4 * q + 3] = v.w;
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+        for (int i = 0; i < WM_T; ++i)
+#pragma unroll
+          for (int j = 0; j < WN_T; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bf[j][kk], acc[i][j], 0, 0, 0);
+    }
     if (more) store_chunk((ch + 1) & 1);
     __syncthreads();
   }
@@ -241,6 +291,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
           const int n = nb + wn * 32 * WN_T + j * 32 + r32;
           if (n >= a.N) continue;
           float v = acc[i][j][reg] + (a.bias ? a.bias[n] : 0.f);
+          const long long oi = (long long)b * a.out_bs + (long long)t * a.out_ld + n;
           if constexpr (EPI == EPI_POSTERIOR) {
             float xt = a.res[(long long)b * a.res_bs + (long long)t * a.res_ld + n];
             float x = a.c1 * v + a.c2 * xt;
@@ -249,11 +300,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
                                 : philox_normal(a.seed, ((unsigned long long)R) * a.N + n, a.stream_id);
               x += a.sigma * z;
             }
-            a.out[(long long)b * a.out_bs + (long long)t * a.out_ld + n] = x;
+            a.out[oi] = x;
           } else {
             v = act_apply(v, a.act, a.alpha) * a.scale;
             if (a.res) v += a.res[(long long)b * a.res_bs + (long long)t * a.res_ld + n];
-            a.out[(long long)b * a.out_bs + (long long)t * a.out_ld + n] = v;
+            if (a.out_bf16) reinterpret_cast<__bf16*>(a.out)[oi] = (__bf16)v;
+            else a.out[oi] = v;
           }
         }
       }
@@ -264,8 +316,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const GemmArgs a) {
 // Host-side validation + launch.  Returns PD_OK or an error code.
 int validate_gemm(const GemmArgs& a);
 
+const __bf16* lookup_bf16(const float* p);
+
 template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI, int ID>
-int launch_gemm(const GemmArgs& a, hipStream_t st, const char* tag) {
+int launch_gemm(const GemmArgs& a0, hipStream_t st, const char* tag) {
+  GemmArgs a = a0;
+  if (!a.Wb) a.Wb = lookup_bf16(a.W);   // bf16 handle -> bf16 MFMA path
   PD_TRY(validate_gemm(a));
   constexpr int BM = 32 * WM_T * WAVES_M;
   constexpr int BN = 32 * WN_T * WAVES_N;
@@ -279,7 +335,10 @@ int launch_gemm(const GemmArgs& a, hipStream_t st, const char* tag) {
   }
   {
     ProfScope ps(tag, st);
-    hipLaunchKernelGGL((gemm_f32_kernel<WM_T, WN_T, WAVES_M, WAVES_N, EPI, ID>), grid, dim3(256), 0, st, a);
+    if (a.Wb)
+      hipLaunchKernelGGL((gemm_kernel<__bf16, WM_T, WN_T, WAVES_M, WAVES_N, EPI, ID>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm_kernel<float, WM_T, WN_T, WAVES_M, WAVES_N, EPI, ID>), grid, dim3(256), 0, st, a);
   }
   PD_LAUNCH_CHECK();
   return PD_OK;

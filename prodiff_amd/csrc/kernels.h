@@ -31,6 +31,14 @@ int add_vectors(float* dst, const float* a, const float* b, int n, hipStream_t s
 // weight-norm fold on device: w[co,:] = g[co] * v[co,:] / ||v[co,:]||
 int weight_norm_fold(float* w, const float* g, const float* v, int Cout, int per_row, hipStream_t st);
 
+// fp32 -> bf16 (round to nearest even)
+int convert_f32_bf16(const float* src, __bf16* dst, long long n, hipStream_t st);
+// bf16 mirrors of packed fp32 weight pools: launch_gemm uses the bf16 copy of any
+// weight pointer inside a registered pool (same element offset).
+void register_bf16_pool(const float* base, size_t n, const __bf16* bf);
+void unregister_bf16_pool(const float* base);
+const __bf16* lookup_bf16(const float* p);
+
 // Philox fills: U[0,1) or N(0,1), element i of stream `stream` under `seed`.
 int fill_uniform(float* out, long long n, unsigned long long seed, unsigned stream, hipStream_t st);
 int fill_normal(float* out, long long n, unsigned long long seed, unsigned stream, hipStream_t st);

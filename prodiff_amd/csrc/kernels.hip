@@ -3,6 +3,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <vector>
 
 #include "gemm.h"
@@ -206,6 +207,43 @@ int weight_norm_fold(float* w, const float* g, const float* v, int Cout, int per
   hipLaunchKernelGGL(wn_fold_kernel, dim3(Cout), dim3(256), 0, st, w, g, v, per_row);
   PD_LAUNCH_CHECK();
   return PD_OK;
+}
+
+// ---------------------------------------------------------------- bf16 pools
+__global__ void f2bf_kernel(const float* s, __bf16* d, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = (__bf16)s[i];
+}
+
+int convert_f32_bf16(const float* src, __bf16* dst, long long n, hipStream_t st) {
+  if (n == 0) return PD_OK;
+  hipLaunchKernelGGL(f2bf_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, src, dst, n);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+namespace {
+struct PoolRec { const float* base; size_t n; const __bf16* bf; };
+std::vector<PoolRec> g_pools;
+std::mutex g_pool_mu;
+}  // namespace
+
+void register_bf16_pool(const float* base, size_t n, const __bf16* bf) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pools.push_back({base, n, bf});
+}
+
+void unregister_bf16_pool(const float* base) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (size_t i = 0; i < g_pools.size(); ++i)
+    if (g_pools[i].base == base) { g_pools.erase(g_pools.begin() + i); return; }
+}
+
+const __bf16* lookup_bf16(const float* p) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (auto& r : g_pools)
+    if (p >= r.base && p < r.base + r.n) return r.bf + (p - r.base);
+  return nullptr;
 }
 
 // ---------------------------------------------------------------- RNG fills

@@ -23,6 +23,8 @@ struct pd_wavenet {
   int M, H, L, C, cyc, dtype;
   int ldw_in, ldw1;
   float* pool = nullptr;
+  __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
+  size_t pool_n = 0;
   float *Win, *b_in, *W1, *b1, *W2, *b2, *Wd, *bd, *Wl1, *bl1, *Wl2, *bl2, *Ws, *bs, *Wo, *bo;
 };
 
@@ -126,7 +128,7 @@ extern "C" {
 int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, int dtype,
                       void* stream, pd_wavenet** out) {
   PD_CHECK_ARG(dims && params && out, "null pointer");
-  PD_CHECK_ARG(dtype == PD_DTYPE_F32, "only PD_DTYPE_F32 is implemented for the WaveNet path");
+  PD_CHECK_ARG(dtype == PD_DTYPE_F32 || dtype == PD_DTYPE_BF16, "dtype must be PD_DTYPE_F32 or PD_DTYPE_BF16");
   const int M = dims->in_dims, H = dims->hidden_size, L = dims->residual_layers,
             C = dims->residual_channels, cyc = dims->dilation_cycle_length;
   PD_CHECK_ARG(M > 0 && M % 4 == 0, "in_dims must be a positive multiple of 4");
@@ -153,7 +155,7 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
       {&h->Wo, (size_t)M * C}, {&h->bo, (size_t)M}};
   std::vector<size_t> offs;
   for (auto& p : plan) { offs.push_back(off); off += (p.second + 63) / 64 * 64; }
-  if (hipMalloc(&h->pool, off * sizeof(float)) != hipSuccess) {
+  if (hipMalloc((void**)&h->pool, off * sizeof(float)) != hipSuccess) {
     delete h;
     set_error("hipMalloc failed for WaveNet weights");
     return PD_ERR_HIP;
@@ -195,11 +197,18 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
     PD_TRY(cp(h->bs, params[p++], C));
     PD_TRY(cp(h->Wo, params[p++], (size_t)M * C));
     PD_TRY(cp(h->bo, params[p++], M));
+    h->pool_n = off;
+    if (dtype == PD_DTYPE_BF16) {
+      PD_HIP(hipMalloc(&h->pool_bf, off * sizeof(__bf16)));
+      PD_TRY(convert_f32_bf16(h->pool, h->pool_bf, (long long)off, st));
+      register_bf16_pool(h->pool, off, h->pool_bf);
+    }
     return PD_OK;
   };
   rc = run();
   if (rc != PD_OK) {
-    hipFree(h->pool);
+    (void)hipFree(h->pool);
+    if (h->pool_bf) (void)hipFree(h->pool_bf);
     delete h;
     return rc;
   }
@@ -209,7 +218,11 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
 
 void pd_wavenet_destroy(pd_wavenet* h) {
   if (!h) return;
-  hipFree(h->pool);
+  if (h->pool_bf) {
+    unregister_bf16_pool(h->pool);
+    (void)hipFree(h->pool_bf);
+  }
+  (void)hipFree(h->pool);
   delete h;
 }
 

@@ -132,9 +132,17 @@ class FastDiff(nn.Module):
                                                   dilation=1, bias=True))
         if use_weight_norm:
             self.apply_weight_norm()
+        self.compute_dtype = "fp32"
         self._h = None
         self._sig = None
         self._ws = _lib.Workspace()
+
+    def set_compute_dtype(self, dtype):
+        """'fp32' (exact, the parity path) or 'bf16' (bf16 MFMA, bf16 LVC kernels)."""
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(dtype)
+        self.compute_dtype = dtype
+        return self
 
     # ------------------------------------------------------- weight norm
     def apply_weight_norm(self):
@@ -167,7 +175,7 @@ class FastDiff(nn.Module):
         return seq
 
     def _param_sig(self):
-        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+        return (self.compute_dtype,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
 
     def handle(self):
         sig = self._param_sig()
@@ -199,7 +207,8 @@ class FastDiff(nn.Module):
                             d["kpnet_hidden_channels"], d["kpnet_conv_size"], d["step_embed_in"],
                             d["step_embed_mid"], d["step_embed_out"])
         h = _lib.C.c_void_p()
-        _lib.check(L.fd_create(_lib.C.byref(dims), arr, _lib.PD_DTYPE_F32, st, _lib.C.byref(h)))
+        dt = _lib.PD_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.PD_DTYPE_F32
+        _lib.check(L.fd_create(_lib.C.byref(dims), arr, dt, st, _lib.C.byref(h)))
         self._release()
         self._h, self._sig, self._keep = h, sig, keep
         return h

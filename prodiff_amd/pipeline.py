@@ -37,7 +37,7 @@ class Synthesizer:
         self.vocoder = vocoder
 
     @classmethod
-    def synthetic(cls, device, seed=0, **over):
+    def synthetic(cls, device, seed=0, dtype="fp32", **over):
         """Random-init weights of the reference architectures (no checkpoints offline)."""
         cfg = dict(PRODIFF_DEFAULTS, **over)
         net = WaveNet(cfg["in_dims"], cfg["hidden_size"], cfg["residual_layers"], cfg["residual_channels"],
@@ -51,6 +51,8 @@ class Synthesizer:
         fd.load_state_dict({k: torch.from_numpy(v)
                             for k, v in synth.synth_params(synth.fastdiff_param_shapes(), seed + 1).items()})
         fd.remove_weight_norm()
+        gd.set_compute_dtype(dtype)
+        fd.set_compute_dtype(dtype)
         voc = FastDiffVocoder({"hop_size": HOP}, model=fd.to(device), reverse_step=4, device=device)
         return cls(gd, voc)
 

@@ -56,9 +56,17 @@ class WaveNet(nn.Module):
         self.skip_projection = nn.Conv1d(C, C, 1)
         self.output_projection = nn.Conv1d(C, in_dims, 1)
         nn.init.zeros_(self.output_projection.weight)
+        self.compute_dtype = "fp32"
         self._h = None
         self._sig = None
         self._ws = _lib.Workspace()
+
+    def set_compute_dtype(self, dtype):
+        """'fp32' (exact, the parity path) or 'bf16' (bf16 MFMA, fp32 accumulate)."""
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(dtype)
+        self.compute_dtype = dtype
+        return self
 
     # ----------------------------------------------------------- packing
     def ordered_params(self):
@@ -77,7 +85,7 @@ class WaveNet(nn.Module):
     def handle(self):
         """The packed C handle; re-packed whenever a parameter is replaced or modified."""
         ps = self.ordered_params()
-        sig = tuple((p.data_ptr(), p._version) for p in ps)
+        sig = (self.compute_dtype,) + tuple((p.data_ptr(), p._version) for p in ps)
         if self._h is not None and sig == self._sig:
             return self._h
         L = _lib.lib()
@@ -89,7 +97,8 @@ class WaveNet(nn.Module):
         dims = _lib.pd_wavenet_dims(self.in_dims, self.hidden_size, self.n_layers,
                                     self.residual_channels, self.dilation_cycle_length)
         h = _lib.C.c_void_p()
-        _lib.check(L.pd_wavenet_create(_lib.C.byref(dims), arr, _lib.PD_DTYPE_F32,
+        dt = _lib.PD_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.PD_DTYPE_F32
+        _lib.check(L.pd_wavenet_create(_lib.C.byref(dims), arr, dt,
                                        _lib.stream_ptr(dev), _lib.C.byref(h)))
         self._release()
         self._h, self._sig = h, sig
@@ -160,6 +169,10 @@ class GaussianDiffusion(nn.Module):
                              persistent=False)
         self._ws = _lib.Workspace()
         self._coef_cache = None
+
+    def set_compute_dtype(self, dtype):
+        self.denoise_fn.set_compute_dtype(dtype)
+        return self
 
     def _step_scalars(self):
         key = tuple(b._version for b in (self.posterior_mean_coef1, self.posterior_mean_coef2,

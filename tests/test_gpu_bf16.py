@@ -1,0 +1,97 @@
+"""bf16 throughput path (C3) against the fp32 golden vectors / oracle.
+
+Stated tolerance (bf16 is judged against the fp32 oracle with a
+looser, stated bound): relative L2 error ||got - ref|| / ||ref|| <= 2e-2 and no
+element off by more than 10% of max|ref|.  bf16 keeps 8 significant bits, so
+per-GEMM rounding is ~4e-3 relative; the bounds allow the 20-layer / 12-layer
+stacks to compound it.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle_fastdiff as OF
+from prodiff_amd import FastDiff, GaussianDiffusion, WaveNet, synth
+from prodiff_amd.fastdiff import sampling_given_noise_schedule
+from tests import golden_io as G
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+REL_L2 = 2e-2
+REL_MAX = 0.1
+
+
+def tt(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def assert_bf16_close(got, ref):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape and np.isfinite(got).all()
+    rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    mx = np.abs(got - ref).max() / np.abs(ref).max()
+    assert rel <= REL_L2 and mx <= REL_MAX, f"rel-L2 {rel:.3e}, max-rel {mx:.3e}"
+
+
+@pytest.mark.parametrize("name", ["wavenet_m80_c256_l20_cyc1", "wavenet_m64_c256_l20_cyc5",
+                                  "wavenet_m80_c64_l4_cyc2"])
+def test_wavenet_bf16(name):
+    d = G.load(name)
+    M, H, L, C, cyc = [int(v) for v in d["dims"]]
+    net = WaveNet(M, H, L, C, cyc)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in G.wavenet_params(d["dims"], d["seed"]).items()})
+    net = net.to(DEV).set_compute_dtype("bf16")
+    out = net(tt(d["spec"]), tt(d["steps"]), tt(d["cond"])).cpu().numpy()
+    assert_bf16_close(out, d["out"])
+
+
+@pytest.mark.parametrize("name", ["prodiff_t2_m80", "prodiff_t4_m128"])
+def test_prodiff_sample_bf16(name):
+    d = G.load(name)
+    M = int(d["mel"].shape[-1])
+    gd = GaussianDiffusion(M, WaveNet(M, 256, 20, 256, 1), timesteps=int(d["timesteps"]), time_scale=1000,
+                           max_beta=float(d["max_beta"]))
+    sd = {"denoise_fn." + k: torch.from_numpy(v) for k, v in G.prodiff_params(name).items()}
+    sd.update({k: torch.from_numpy(v) for k, v in G.prodiff_buffers(d).items()})
+    gd.load_state_dict(sd)
+    gd = gd.to(DEV).set_compute_dtype("bf16")
+    mel = gd.sample(tt(d["cond"]), x_T=tt(d["x_T"]), noise=tt(d["noise"])).cpu().numpy()
+    assert_bf16_close(mel, d["mel"])
+
+
+@pytest.fixture(scope="module")
+def fd16():
+    p = G.fastdiff_params(31)
+    m = FastDiff()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+    return m.to(DEV).set_compute_dtype("bf16"), OF.fold_weight_norm(p)
+
+
+def test_fastdiff_forward_bf16(fd16):
+    m, _ = fd16
+    d = G.load("fastdiff_fwd")
+    eps = m((tt(d["audio"]), tt(d["c"]), tt(d["steps"]))).cpu().numpy()
+    assert_bf16_close(eps, d["eps"])
+
+
+@pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5)])
+def test_fastdiff_forward_bf16_oracle(fd16, B, Tc):
+    """Utterance edges inside fused-LVC blocks (1 frame = 2 blocks at hop 256)."""
+    m, pf = fd16
+    audio = synth.synth_inputs(B + 50 * Tc, (B, 1, Tc * 256))
+    c = synth.synth_inputs(B + 50 * Tc + 1, (B, 80, Tc), loc=-5.0, scale=2.0)
+    st = np.full((B, 1), 23.4676, np.float32)
+    eps = m((tt(audio), tt(c), tt(st))).cpu().numpy()
+    assert_bf16_close(eps, OF.fastdiff_forward(pf, audio, c, st))
+
+
+def test_fastdiff_sample_bf16(fd16):
+    m, _ = fd16
+    d = G.load("fastdiff_sample_n4")
+    s = G.load("schedules")
+    B, _, Tc = d["c"].shape
+    wav = sampling_given_noise_schedule(m, (B, 1, Tc * 256), {"alpha": torch.from_numpy(s["fd_train_alpha"])},
+                                        torch.from_numpy(s["fd_n4_beta"]), condition=tt(d["c"]),
+                                        x_T=tt(d["x_T"]), noise=tt(d["noise"])).cpu().numpy()
+    assert_bf16_close(wav, d["wav"])
