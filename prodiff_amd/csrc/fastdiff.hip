@@ -272,6 +272,191 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
   }
 }
 
+// ------------------------------------------------------------------ kernel predictor (bf16)
+struct KPArgs {
+  const float* condT;       // [B][Tc][80] mel, time-major
+  const float* nz;          // fc_t(emb) rows for this block: nz[b*nz_ld + c]
+  int nz_ld;
+  const __bf16* Win;        // [64][5*96]   (tap*96 + ci)
+  const float* bin;
+  const __bf16* Wr[6];      // [64][3*64]
+  const float* br[6];
+  const __bf16* Wb;         // [256][3*64]  bias_conv
+  const float* bb;
+  float* hout;              // [B][Tc][64]  h = h0 + R(h0)
+  float* Bf;                // [B][Tc][256] LVC biases
+  int Tc;
+};
+
+// Fused KernelPredictor hidden stack (modules.py:320-333 + bias_conv :338-342):
+//   h0 = lrelu_.1(conv5(c + fc_t(e))), r = 6 x lrelu_.1(conv3(.)), h = h0 + r, Bf = conv3(h)
+// Block: 64 output frames of one utterance.  Every stage runs on 96 local rows
+// (local row p <-> frame f0 - 16 + p) held in LDS as bf16, and rows outside the
+// utterance are zeroed after every stage -- exactly each reference conv's zero
+// padding.  The halo shrinks by 1 row per conv (9 rows needed, 16 kept).
+__global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
+  constexpr int LDC = 104, LDH = 72;               // 208 B / 144 B rows: conflict-free b128 reads
+  __shared__ __attribute__((aligned(16))) __bf16 Cs[100 * LDC];
+  __shared__ __attribute__((aligned(16))) __bf16 Hb[3][98 * LDH];   // H0, R0, R1 (+1 zero row each side)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int b = blockIdx.y, f0 = blockIdx.x * 64, Tc = A.Tc;
+  const long long rb = (long long)b * Tc;
+
+  // c' = c + fc_t(e) on frames f0-18 .. f0+81 (channels 80..95 zero)
+  for (int i = tid; i < 100 * 24; i += 256) {
+    const int p = i / 24, g = (i - p * 24) * 4, f = f0 - 18 + p;
+    bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+    if (g < CC && f >= 0 && f < Tc) {
+      const float4 c = *reinterpret_cast<const float4*>(A.condT + (rb + f) * CC + g);
+      const float4 n = *reinterpret_cast<const float4*>(A.nz + (long long)b * A.nz_ld + g);
+      v = bf16x4{(__bf16)(c.x + n.x), (__bf16)(c.y + n.y), (__bf16)(c.z + n.z), (__bf16)(c.w + n.w)};
+    }
+    *reinterpret_cast<bf16x4*>(Cs + p * LDC + g) = v;
+  }
+  for (int i = tid; i < 3 * 2 * LDH; i += 256) {   // zero guard rows 0 and 97
+    const int buf = i / (2 * LDH), j = i - buf * 2 * LDH;
+    Hb[buf][(j < LDH ? 0 : 97 * LDH) + (j % LDH)] = (__bf16)0.f;
+  }
+  __syncthreads();
+
+  float keep[2][16];   // h0 in fp32 for the residual add (same job->wave map in every stage)
+  // stage 0: h0 = lrelu(conv5(c')) ; jobs = 3 row tiles x 2 column tiles
+  for (int job = wave, q = 0; job < 6; job += 4, ++q) {
+    const int mt = job >> 1, nt = job & 1;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const __bf16* wrow = A.Win + (nt * 32 + r32) * 480 + h * 8;
+#pragma unroll 6
+    for (int kk = 0; kk < 30; ++kk) {
+      const int tap = kk / 6, kc = kk - tap * 6;
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(Cs + (mt * 32 + r32 + tap) * LDC + kc * 16 + h * 8);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
+    }
+    const int n = nt * 32 + r32;
+    const float bias = A.bin[n];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int p = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, f = f0 - 16 + p;
+      float v = acc[reg] + bias;
+      v = v >= 0.f ? v : 0.1f * v;
+      if (f < 0 || f >= Tc) v = 0.f;
+      keep[q][reg] = v;
+      Hb[0][(p + 1) * LDH + n] = (__bf16)v;
+    }
+  }
+  __syncthreads();
+  // stages 1..6: residual convs H0 -> R0 -> R1 -> R0 -> R1 -> R0 -> R1
+  for (int j = 0; j < 6; ++j) {
+    const __bf16* In = Hb[j == 0 ? 0 : (j & 1 ? 1 : 2)];
+    __bf16* Out = Hb[j & 1 ? 2 : 1];
+    for (int job = wave, q = 0; job < 6; job += 4, ++q) {
+      const int mt = job >> 1, nt = job & 1;
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const __bf16* wrow = A.Wr[j] + (nt * 32 + r32) * 192 + h * 8;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) {
+        const int tap = kk >> 2, kc = kk & 3;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(In + (mt * 32 + r32 + tap) * LDH + kc * 16 + h * 8);
+        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
+      }
+      const int n = nt * 32 + r32;
+      const float bias = A.br[j][n];
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int p = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, f = f0 - 16 + p;
+        float v = acc[reg] + bias;
+        v = v >= 0.f ? v : 0.1f * v;
+        if (j == 5) v += keep[q][reg];           // h = h0 + R(h0)
+        if (f < 0 || f >= Tc) v = 0.f;
+        Out[(p + 1) * LDH + n] = (__bf16)v;
+        if (j == 5 && p >= 16 && p < 80 && f < Tc) A.hout[(rb + f) * HK + n] = v;
+      }
+    }
+    __syncthreads();
+  }
+  // bias_conv on the 64 output frames: 2 row tiles x 8 column tiles
+  for (int job = wave; job < 16; job += 4) {
+    const int mt = job >> 3, nt = job & 7;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const __bf16* wrow = A.Wb + (nt * 32 + r32) * 192 + h * 8;
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk) {
+      const int tap = kk >> 2, kc = kk & 3;
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(Hb[2] + (16 + mt * 32 + r32 + tap) * LDH + kc * 16 + h * 8);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
+    }
+    const int n = nt * 32 + r32;
+    const float bias = A.bb[n];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int f = f0 + mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (f < Tc) A.Bf[(rb + f) * (2 * CI * NLY) + n] = acc[reg] + bias;
+    }
+  }
+}
+
+// Location-variable kernels of one LVC layer, frame-major bf16 (modules.py:335-340):
+//   Kf[f][n] = b[n] + W[n] . [h(f-1); h(f); h(f+1)]      n < 6144, K = 192
+// Block: 64 frames x 256 kernel rows, 2x2 waves.  The A operand (64 x 192) is loaded
+// once into registers; each wave streams its 4 weight column tiles from L2.
+__global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __restrict__ hin,
+                                                             const __bf16* __restrict__ W,
+                                                             const float* __restrict__ bias,
+                                                             __bf16* __restrict__ Kf, int Tc, int rows) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r32 = lane & 31, h = lane >> 5;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int R = blockIdx.x * 64 + wm * 32 + r32;     // A row (frame) of this lane
+  bf16x8 af[12];
+  {
+    const bool ok = R < rows;
+    const int b = ok ? R / Tc : 0, f = R - b * Tc;
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk) {
+      const int tap = kk >> 2, kc = kk & 3, ff = f + tap - 1;
+      float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
+      if (ok && ff >= 0 && ff < Tc) {
+        const float* p = hin + ((long long)b * Tc + ff) * HK + kc * 16 + h * 8;
+        u = *reinterpret_cast<const float4*>(p);
+        v = *reinterpret_cast<const float4*>(p + 4);
+      }
+      af[kk] = bf16x8{(__bf16)u.x, (__bf16)u.y, (__bf16)u.z, (__bf16)u.w,
+                      (__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    }
+  }
+  const int n0 = blockIdx.y * 256 + wn * 128;
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < 12; ++kk) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(W + (long long)(n0 + j * 32 + r32) * 192 + kk * 16 + h * 8);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk], bw, acc[j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + j * 32 + r32;
+    const float bn = bias[n];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = blockIdx.x * 64 + wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row < rows) Kf[(long long)row * KPERLAYER + n] = (__bf16)(acc[j][reg] + bn);
+    }
+  }
+}
+
 // eps[b][t] = bias + sum_{k<7,c<32} w[k][c] x[b][t+k-3][c]      (FastDiff_model.py:67-68,100)
 // mode 0: eps_out = eps.  mode 1 (sampler, util.py:222-226):
 //   xa = (xa - ce*eps) / den + sig * z
@@ -462,6 +647,20 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
     const long long Tout = Tin * r;
     const long long bsC = (long long)Tc * CC, bsH = (long long)Tc * HK;
     // --- kernel predictor on c + fc_t(emb)   (modules.py:202-204, 320-343)
+    const bool bf = m->pool_bf != nullptr;
+    const float* hk = nullptr;   // final h  [B][Tc][64]
+    if (bf) {
+      KPArgs ka{};
+      ka.condT = condT; ka.nz = nz + n * CC; ka.nz_ld = nb * CC;
+      ka.Win = lookup_bf16(K.kin_w); ka.bin = K.kin_b;
+      for (int j = 0; j < 6; ++j) { ka.Wr[j] = lookup_bf16(K.kres_w[j]); ka.br[j] = K.kres_b[j]; }
+      ka.Wb = lookup_bf16(K.kb_w); ka.bb = K.kb_b;
+      ka.hout = ws + W.h0; ka.Bf = ws + W.Bf; ka.Tc = Tc;
+      ProfScope ps("fd_kp_hidden", st);
+      hipLaunchKernelGGL(kp_hidden_bf16_kernel, dim3(cdiv(Tc, 64), B), dim3(256), 0, st, ka);
+      PD_LAUNCH_CHECK();
+      hk = ws + W.h0;
+    } else {
     {
       GemmArgs a = make_gemm(B, Tc, HK, K.kin_w, 5 * 96, K.kin_b, ws + W.h0, bsH, HK);
       for (int tap = 0; tap < 5; ++tap) {
@@ -484,12 +683,13 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_RES>(a, st, "fd_kp_res")));
       src = dst;
     }
-    const float* hk = src;   // final h  [B][Tc][64]
+    hk = src;
     {
       GemmArgs a = make_gemm(B, Tc, 2 * CI * NLY, K.kb_w, 3 * HK, K.kb_b, ws + W.Bf,
                              (long long)Tc * 2 * CI * NLY, 2 * CI * NLY);
       for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_BIAS>(a, st, "fd_kp_bias")));
+    }
     }
     // --- upsample (modules.py:205-206)
     {
@@ -501,16 +701,21 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
     }
     // --- 4 LVC layers (modules.py:208-217)
     for (int i = 0; i < NLY; ++i) {
-      {  // this layer's kernels, frame-major
+      if (bf) {  // this layer's kernels, frame-major bf16
+        ProfScope ps("fd_kp_kernel", st);
+        const int rows = B * Tc;
+        hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(cdiv(rows, 64), KPERLAYER / 256), dim3(256), 0, st, hk,
+                           lookup_bf16(K.kk_w) + (size_t)i * KPERLAYER * 3 * HK, K.kk_b + (size_t)i * KPERLAYER,
+                           reinterpret_cast<__bf16*>(ws + W.Kf), Tc, rows);
+        PD_LAUNCH_CHECK();
+      } else {
         GemmArgs a = make_gemm(B, Tc, KPERLAYER, K.kk_w + (size_t)i * KPERLAYER * 3 * HK, 3 * HK,
                                K.kk_b + (size_t)i * KPERLAYER, ws + W.Kf, (long long)Tc * KPERLAYER,
                                KPERLAYER);
         for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
-        a.out_bf16 = m->pool_bf != nullptr;   // bf16 kernels halve the K_l round trip
         PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_KERNEL>(a, st, "fd_kp_kernel")));
       }
       const int dil = (int)std::pow(3, i);
-      const bool bf = m->pool_bf != nullptr;
       if (bf && hop % 64 == 0) {
         // one fused launch: pre-conv + LVC + gate (bf16 MFMA)
         ProfScope ps("fd_lvc_fused", st);
