@@ -405,15 +405,53 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 
 // Location-variable kernels of one LVC layer, frame-major bf16 (modules.py:335-340):
 //   Kf[f][n] = b[n] + W[n] . [h(f-1); h(f); h(f+1)]      n < 6144, K = 192
-// Block: 64 frames x 256 kernel rows, 2x2 waves.  The A operand (64 x 192) is loaded
-// once into registers; each wave streams its 4 weight column tiles from L2.
+// Block: 128 frames (one 32-frame tile per wave, its h fragments held in registers for
+// the whole block) x a run of 64-row weight tiles.  Each weight tile is staged in LDS
+// with coalesced 16-B loads (double-buffered, next tile in flight under the MFMAs).
+// The MFMA computes C[n][frame] (weights as the A operand), so a lane holds 4
+// consecutive kernel values of one frame and stores 8 B at a time.
+constexpr int KPK_ROWS = 128, KPK_NT = 64, KPK_LDW = 200;   // 400-B LDS rows: conflict-free b128 reads
 __global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __restrict__ hin,
                                                              const __bf16* __restrict__ W,
                                                              const float* __restrict__ bias,
-                                                             __bf16* __restrict__ Kf, int Tc, int rows) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r32 = lane & 31, h = lane >> 5;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int R = blockIdx.x * 64 + wm * 32 + r32;     // A row (frame) of this lane
+                                                             __bf16* __restrict__ Kf, int Tc, int rows,
+                                                             int tiles_per_block) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][KPK_NT * KPK_LDW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int R = blockIdx.x * KPK_ROWS + wave * 32 + r32;     // frame (C column) of this lane
+  const int tile0 = blockIdx.y * tiles_per_block;
+  // W tile = 64 rows x 384 B = 1536 16-B pieces, 6 per thread (named registers: an
+  // indexed array here is demoted to scratch by hipcc)
+  uint4 s0, s1, s2, s3, s4, s5;
+  int goff[6], loff[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int c = tid + 256 * i, row = c / 24, col = (c - row * 24) * 8;
+    goff[i] = row * 192 + col;
+    loff[i] = row * KPK_LDW + col;
+  }
+#define KPK_LD(t)                                                        \
+  do {                                                                   \
+    const __bf16* src_ = W + (long long)(t) * KPK_NT * 192;              \
+    s0 = *reinterpret_cast<const uint4*>(src_ + goff[0]);                \
+    s1 = *reinterpret_cast<const uint4*>(src_ + goff[1]);                \
+    s2 = *reinterpret_cast<const uint4*>(src_ + goff[2]);                \
+    s3 = *reinterpret_cast<const uint4*>(src_ + goff[3]);                \
+    s4 = *reinterpret_cast<const uint4*>(src_ + goff[4]);                \
+    s5 = *reinterpret_cast<const uint4*>(src_ + goff[5]);                \
+  } while (0)
+#define KPK_ST(buf)                                                      \
+  do {                                                                   \
+    *reinterpret_cast<uint4*>(&Ws[buf][loff[0]]) = s0;                   \
+    *reinterpret_cast<uint4*>(&Ws[buf][loff[1]]) = s1;                   \
+    *reinterpret_cast<uint4*>(&Ws[buf][loff[2]]) = s2;                   \
+    *reinterpret_cast<uint4*>(&Ws[buf][loff[3]]) = s3;                   \
+    *reinterpret_cast<uint4*>(&Ws[buf][loff[4]]) = s4;                   \
+    *reinterpret_cast<uint4*>(&Ws[buf][loff[5]]) = s5;                   \
+  } while (0)
+#define load_tile(t) KPK_LD(t)
+#define store_tile(b) KPK_ST(b)
+  load_tile(tile0);
   bf16x8 af[12];
   {
     const bool ok = R < rows;
@@ -431,30 +469,46 @@ __global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __rest
                       (__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
     }
   }
-  const int n0 = blockIdx.y * 256 + wn * 128;
-  f32x16 acc[4];
+  store_tile(0);
+  __syncthreads();
+  __bf16* out = Kf + (long long)R * KPERLAYER;
+  for (int it = 0; it < tiles_per_block; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < tiles_per_block) load_tile(tile0 + it + 1);
+    f32x16 acc[2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 #pragma unroll
-  for (int kk = 0; kk < 12; ++kk) {
+    for (int kk = 0; kk < 12; ++kk) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(W + (long long)(n0 + j * 32 + r32) * 192 + kk * 16 + h * 8);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk], bw, acc[j], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&Ws[buf][(j * 32 + r32) * KPK_LDW + kk * 16 + h * 8]);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[kk], acc[j], 0, 0, 0);
+      }
     }
-  }
+    // C[n][frame]: this lane owns frame R, rows n = n0 + 32j + 8g + 4h + (0..3)
+    const int n0 = (tile0 + it) * KPK_NT;
+    if (R < rows) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + j * 32 + r32;
-    const float bn = bias[n];
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = blockIdx.x * 64 + wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (row < rows) Kf[(long long)row * KPERLAYER + n] = (__bf16)(acc[j][reg] + bn);
+        for (int g = 0; g < 4; ++g) {
+          const int n = n0 + j * 32 + 8 * g + 4 * h;
+          const float4 bn = *reinterpret_cast<const float4*>(bias + n);
+          bf16x4 v = {(__bf16)(acc[j][4 * g] + bn.x), (__bf16)(acc[j][4 * g + 1] + bn.y),
+                      (__bf16)(acc[j][4 * g + 2] + bn.z), (__bf16)(acc[j][4 * g + 3] + bn.w)};
+          *reinterpret_cast<bf16x4*>(out + n) = v;
+        }
     }
+    if (it + 1 < tiles_per_block) store_tile(buf ^ 1);
+    __syncthreads();
   }
+#undef load_tile
+#undef store_tile
+#undef KPK_LD
+#undef KPK_ST
 }
 
 // eps[b][t] = bias + sum_{k<7,c<32} w[k][c] x[b][t+k-3][c]      (FastDiff_model.py:67-68,100)
@@ -704,9 +758,13 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       if (bf) {  // this layer's kernels, frame-major bf16
         ProfScope ps("fd_kp_kernel", st);
         const int rows = B * Tc;
-        hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(cdiv(rows, 64), KPERLAYER / 256), dim3(256), 0, st, hk,
+        // ~2 blocks per CU: split the 96 weight tiles over enough groups
+        const int rblocks = cdiv(rows, KPK_ROWS);
+        int groups = 1;
+        while (groups < 32 && rblocks * groups < 512) groups *= 2;   // groups | 96
+        hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(rblocks, groups), dim3(256), 0, st, hk,
                            lookup_bf16(K.kk_w) + (size_t)i * KPERLAYER * 3 * HK, K.kk_b + (size_t)i * KPERLAYER,
-                           reinterpret_cast<__bf16*>(ws + W.Kf), Tc, rows);
+                           reinterpret_cast<__bf16*>(ws + W.Kf), Tc, rows, (KPERLAYER / KPK_NT) / groups);
         PD_LAUNCH_CHECK();
       } else {
         GemmArgs a = make_gemm(B, Tc, KPERLAYER, K.kk_w + (size_t)i * KPERLAYER * 3 * HK, 3 * HK,
