@@ -61,6 +61,34 @@ def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
     }
 
 
+def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
+    """Compulsory HBM bytes of ONE launch of each tagged kernel with the layouts the
+    kernels use (activations fp32 time-major; weights and LVC kernels bf16 in the
+    bf16 path, fp32 otherwise).  Mean over launches where the block size varies."""
+    F = B * T
+    wb = 2 if dtype == "bf16" else 4
+    rows = [F * h for h in hops]
+    per_row_io = 32 * 4
+    kf_frame = 6144 * wb + 256 * 4
+    # fused LVC (hop >= 64): x read+write, audio_down read, this layer's kernels+biases
+    lvc_f = [r * 3 * per_row_io + F * kf_frame for r in rows[1:]]
+    lvc_v = [r * 4 * per_row_io + F * kf_frame for r in rows]          # unfused: x r/w, a, y
+    return {
+        "wn_inproj": F * (M + C) * 4 + C * M * wb,
+        "wn_gate": F * (C + H + C) * 4 + 2 * C * (3 * C + H) * wb,
+        "wn_resskip": F * (C + 2 * C + 2 * C) * 4 + 2 * C * C * wb,
+        "wn_skiphead": F * 2 * C * 4 + C * C * wb,
+        "wn_outproj_posterior": F * (C + 3 * M) * 4 + M * C * wb,
+        "fd_first_conv": F * 256 * (1 + 32) * 4,
+        "fd_kp_kernel": F * (64 * 4 + 6144 * wb) + 6144 * 192 * wb,
+        "fd_kp_hidden": F * (80 + 64 + 256) * 4 + (64 * 480 + 6 * 64 * 192 + 256 * 192) * wb,
+        "fd_lvc_fused": sum(lvc_f) / 2.0,
+        "fd_lvc": sum(lvc_v) / 3.0,
+        "fd_upsample": sum(r * (1 + 1.0 / h) * per_row_io for r, h in zip(rows, (8, 8, 4))) / 3.0,
+        "fd_final_update": F * 256 * (32 + 3) * 4,
+    }
+
+
 def step_flops(B, T):
     """Whole-step algorithmic FLOPs: 2 x 26.43 + 4 x 56.98 MFLOP per frame."""
     f = flops_per_launch(B, T)
@@ -166,20 +194,32 @@ def main():
     audio_s = frames * HOP / SAMPLE_RATE
     ms_step = dt / args.steps * 1e3
     fl = flops_per_launch(B, T)
+    by = bytes_per_launch(B, T, args.dtype)
+    peak_tf = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
+    ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)          # FLOP/B where MFMA and HBM bounds meet
     roofline, kernels = None, {}
     if kern:
         for tag, (cnt, ms) in sorted(kern.items(), key=lambda kv: -kv[1][1]):
-            tf = fl.get(tag, 0.0) * cnt / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+            sec = ms * 1e-3
             kernels[tag] = {"launches": cnt, "ms_total": round(ms, 3), "avg_us": round(ms / cnt * 1e3, 2),
-                            "tflops": round(tf, 2)}
+                            "tflops": round(fl.get(tag, 0.0) * cnt / sec / 1e12, 2) if ms > 0 else 0.0,
+                            "gbs": round(by.get(tag, 0.0) * cnt / sec / 1e9, 1) if ms > 0 else 0.0}
         dom = max(kern.items(), key=lambda kv: kv[1][1])[0]
         cnt, ms = kern[dom]
-        ach = fl[dom] * cnt / (ms * 1e-3) / 1e12
-        peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
-        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
-                    "flop_per_launch": fl[dom], "avg_launch_us": round(ms / cnt * 1e3, 2),
-                    "share_of_step": round(ms / (dt * 1e3), 3)}
+        sec = ms * 1e-3
+        intensity = fl[dom] / by[dom] if by.get(dom) else float("inf")
+        if intensity < ridge:      # HBM-bound at its compulsory bytes
+            ach = by[dom] * cnt / sec / 1e9
+            roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4)}
+        else:
+            ach = fl[dom] * cnt / sec / 1e12
+            roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
+                        "frac": round(ach / peak_tf, 4)}
+        roofline.update({"traffic": None, "kernel": dom, "flop_per_launch": fl[dom],
+                         "bytes_per_launch": by.get(dom), "intensity_flop_per_byte": round(intensity, 1),
+                         "ridge_flop_per_byte": round(ridge, 1), "avg_launch_us": round(ms / cnt * 1e3, 2),
+                         "launches": cnt, "share_of_step": round(ms / (dt * 1e3), 3)})
     out = {
         "metric": METRIC,
         "value": round(frames / dt, 1),
