@@ -272,6 +272,169 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
   }
 }
 
+// ------------------------------------------------------------------ whole LVC block (bf16)
+// All 4 LVC layers of one TimeAware_LVCBlock (modules.py:208-217) in ONE launch:
+//   for l < 4:  x = x + a + gate(LVC_l(lrelu(conv_{3^l}(lrelu(x + a)) + b_l)))
+// Block = 256 output samples of one utterance.  x and a (audio_down) are read once
+// (with the 44-sample halo of the 1/3/9/27-dilated stack) into LDS as fp32 and the
+// state never leaves LDS until the last layer; layer l is evaluated on its own valid
+// range (halo e_l = 42, 38, 28, 0), so each later layer still sees exact inputs.
+// A 32-row LVC tile that straddles a frame boundary is multiplied by both frames'
+// kernels and each row keeps its own frame's result.
+struct LvcBlockArgs {
+  float* xout;              // [B][Lh][32]
+  const float* xin;         // [B][Lh][32] upsample output
+  const float* a;           // [B][Lh][32] audio_down
+  const __bf16* Kf[NLY];    // [B*Tc][6144] per layer (frame-major)
+  const float* Bf;          // [B*Tc][256]: layer l at +64 l
+  const __bf16* Wc[NLY];    // [32][96] pre-conv weights (bf16 mirror)
+  const float* bc[NLY];
+  int Tc, hop;
+};
+constexpr int LB_TS = 256, LB_HALO = 44, LB_ROWS = LB_TS + 2 * LB_HALO, LB_UY = 360, LB_LD = 40;
+
+__global__ __launch_bounds__(512) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
+  __shared__ __attribute__((aligned(16))) float X[LB_ROWS * CI];
+  __shared__ __attribute__((aligned(16))) float Aa[LB_ROWS * CI];
+  __shared__ __attribute__((aligned(16))) __bf16 U[LB_UY * LB_LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Yb[LB_UY * LB_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int b = blockIdx.y, Tc = P.Tc, hop = P.hop;
+  const long long Lh = (long long)Tc * hop;
+  const long long t0 = (long long)blockIdx.x * LB_TS;
+  const long long tb = t0 - LB_HALO;                 // time of local row 0
+  const long long base = (long long)b * Lh;
+
+  for (int i = tid; i < LB_ROWS * 8; i += 512) {
+    const int r = i >> 3, q = (i & 7) * 4;
+    const long long t = tb + r;
+    float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
+    if (t >= 0 && t < Lh) {
+      xv = *reinterpret_cast<const float4*>(P.xin + (base + t) * CI + q);
+      av = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + q);
+    }
+    *reinterpret_cast<float4*>(&X[r * CI + q]) = xv;
+    *reinterpret_cast<float4*>(&Aa[r * CI + q]) = av;
+  }
+  __syncthreads();
+
+#pragma unroll 1
+  for (int l = 0; l < NLY; ++l) {
+    const int d = (l == 0) ? 1 : (l == 1) ? 3 : (l == 2) ? 9 : 27;
+    const int e = (l == 0) ? 42 : (l == 1) ? 38 : (l == 2) ? 28 : 0;   // halo still needed after layer l
+    const int lo = LB_HALO - e, hi = LB_HALO + LB_TS + e;              // output rows [lo, hi)
+    const int nyt = (hi - lo + 2 + 31) / 32;                      // y rows lo-1 .. hi
+    const int ulo = lo - 1 - d;                                   // local row of U[0]
+    // (1) u = lrelu(x + a), zero outside the utterance
+    const int nu = nyt * 32 + 2 * d;
+    for (int i = tid; i < nu * 8; i += 512) {
+      const int j = i >> 3, q = (i & 7) * 4, r = ulo + j;
+      const long long t = tb + r;
+      bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+      if (r >= 0 && r < LB_ROWS && t >= 0 && t < Lh) {
+        const float4 xv = *reinterpret_cast<const float4*>(&X[r * CI + q]);
+        const float4 av = *reinterpret_cast<const float4*>(&Aa[r * CI + q]);
+        float u0 = xv.x + av.x, u1 = xv.y + av.y, u2 = xv.z + av.z, u3 = xv.w + av.w;
+        u0 = u0 >= 0.f ? u0 : 0.2f * u0; u1 = u1 >= 0.f ? u1 : 0.2f * u1;
+        u2 = u2 >= 0.f ? u2 : 0.2f * u2; u3 = u3 >= 0.f ? u3 : 0.2f * u3;
+        v = bf16x4{(__bf16)u0, (__bf16)u1, (__bf16)u2, (__bf16)u3};
+      }
+      *reinterpret_cast<bf16x4*>(&U[j * LB_LD + q]) = v;
+    }
+    __syncthreads();
+    // (2) y = lrelu(W_c . [u(r-d); u(r); u(r+d)] + b), zero outside the utterance
+    {
+      bf16x8 wf[6];
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk)
+        wf[kk] = *reinterpret_cast<const bf16x8*>(P.Wc[l] + r32 * 96 + kk * 16 + h * 8);
+      const float bias = P.bc[l][r32];
+      for (int mt = wave; mt < nyt; mt += 8) {
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const int tap = kk >> 1, ci0 = (kk & 1) * 16;
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(&U[(mt * 32 + r32 + tap * d) * LB_LD + ci0 + h * 8]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wf[kk], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int yj = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          const long long t = tb + lo - 1 + yj;
+          float y = acc[reg] + bias;
+          y = y >= 0.f ? y : 0.2f * y;
+          if (t < 0 || t >= Lh) y = 0.f;
+          Yb[yj * LB_LD + r32] = (__bf16)y;
+        }
+      }
+    }
+    __syncthreads();
+    // (3) o = Bf + K_frame . [y(t-1); y(t); y(t+1)] ; x += a + sigmoid(o_g) tanh(o_f)
+    {
+      const int nlt = (hi - lo + 31) / 32;
+      for (int mt = wave; mt < nlt; mt += 8) {
+        const long long ts = tb + lo + mt * 32;          // time of the tile's first row
+        const long long tlast = ts + 31;
+        int fa = (int)((ts < 0 ? 0 : ts) / hop), fb = (int)((tlast >= Lh ? Lh - 1 : tlast) / hop);
+        if (fa > Tc - 1) fa = Tc - 1;
+        if (fb < fa) fb = fa;
+        bf16x8 yf[6];
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const int tap = kk >> 1, ci0 = (kk & 1) * 16;
+          yf[kk] = *reinterpret_cast<const bf16x8*>(&Yb[(mt * 32 + r32 + tap) * LB_LD + ci0 + h * 8]);
+        }
+        f32x16 g0, f0, g1, f1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { g0[r] = 0.f; f0[r] = 0.f; g1[r] = 0.f; f1[r] = 0.f; }
+        const __bf16* ka = P.Kf[l] + ((long long)b * Tc + fa) * KPERLAYER;
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const bf16x8 kg = *reinterpret_cast<const bf16x8*>(ka + r32 * 96 + kk * 16 + h * 8);
+          const bf16x8 kl = *reinterpret_cast<const bf16x8*>(ka + (32 + r32) * 96 + kk * 16 + h * 8);
+          g0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kg, g0, 0, 0, 0);
+          f0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kl, f0, 0, 0, 0);
+        }
+        if (fb != fa) {
+          const __bf16* kb2 = P.Kf[l] + ((long long)b * Tc + fb) * KPERLAYER;
+#pragma unroll
+          for (int kk = 0; kk < 6; ++kk) {
+            const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kb2 + r32 * 96 + kk * 16 + h * 8);
+            const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kb2 + (32 + r32) * 96 + kk * 16 + h * 8);
+            g1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kg, g1, 0, 0, 0);
+            f1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kl, f1, 0, 0, 0);
+          }
+        }
+        const float* bfa = P.Bf + ((long long)b * Tc + fa) * (2 * CI * NLY) + l * 2 * CI;
+        const float* bfb = P.Bf + ((long long)b * Tc + fb) * (2 * CI * NLY) + l * 2 * CI;
+        const float bga = bfa[r32], bla = bfa[32 + r32], bgb = bfb[r32], blb = bfb[32 + r32];
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int rr = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          const int row = lo + mt * 32 + rr;
+          const long long t = ts + rr;
+          if (row < hi && t >= 0 && t < Lh) {
+            const bool second = (int)(t / hop) != fa;
+            const float og = second ? g1[reg] + bgb : g0[reg] + bga;
+            const float of = second ? f1[reg] + blb : f0[reg] + bla;
+            X[row * CI + r32] += Aa[row * CI + r32] + sigmoidf_(og) * tanhf(of);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < LB_TS * 8; i += 512) {
+    const int r = i >> 3, q = (i & 7) * 4;
+    const long long t = t0 + r;
+    if (t < Lh)
+      *reinterpret_cast<float4*>(P.xout + (base + t) * CI + q) =
+          *reinterpret_cast<const float4*>(&X[(LB_HALO + r) * CI + q]);
+  }
+}
+
 // ------------------------------------------------------------------ kernel predictor (bf16)
 struct KPArgs {
   const float* condT;       // [B][Tc][80] mel, time-major
@@ -612,7 +775,7 @@ FdWs fd_layout(const fd_model* m, int B, int Tc, int S) {
   w.ra = take((size_t)B * Tc * HK);
   w.rb = take((size_t)B * Tc * HK);
   w.Bf = take((size_t)B * Tc * 2 * CI * NLY);
-  w.Kf = take((size_t)B * Tc * KPERLAYER);
+  w.Kf = take((size_t)B * Tc * KPERLAYER * 2);   // fp32: one layer; bf16: all 4 layers
   w.condT = take((size_t)B * Tc * CC);
   w.total = off * sizeof(float);
   return w;
@@ -754,11 +917,38 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       PD_LAUNCH_CHECK();
     }
     // --- 4 LVC layers (modules.py:208-217)
+    if (bf && hop >= 64) {
+      // every layer's kernels first (frame-major bf16), then the whole block in one launch
+      __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf);
+      const int rows = B * Tc;
+      const int rblocks = cdiv(rows, KPK_ROWS);
+      int groups = 1;
+      while (groups < 32 && rblocks * groups < 512) groups *= 2;   // groups | 96
+      LvcBlockArgs la{};
+      for (int i = 0; i < NLY; ++i) {
+        ProfScope ps("fd_kp_kernel", st);
+        hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(rblocks, groups), dim3(256), 0, st, hk,
+                           lookup_bf16(K.kk_w) + (size_t)i * KPERLAYER * 3 * HK, K.kk_b + (size_t)i * KPERLAYER,
+                           Kb + (size_t)i * rows * KPERLAYER, Tc, rows, (KPERLAYER / KPK_NT) / groups);
+        PD_LAUNCH_CHECK();
+        la.Kf[i] = Kb + (size_t)i * rows * KPERLAYER;
+        la.Wc[i] = lookup_bf16(K.cv_w[i]);
+        la.bc[i] = K.cv_b[i];
+      }
+      la.xin = xn; la.xout = ws + W.y; la.a = ad; la.Bf = ws + W.Bf; la.Tc = Tc; la.hop = hop;
+      {
+        ProfScope ps("fd_lvc_block", st);
+        hipLaunchKernelGGL(lvc_block_bf16_kernel, dim3(cdiv(Tout, LB_TS), B), dim3(512), 0, st, la);
+        PD_LAUNCH_CHECK();
+      }
+      x = ws + W.y;
+      Tin = Tout;
+      continue;
+    }
     for (int i = 0; i < NLY; ++i) {
       if (bf) {  // this layer's kernels, frame-major bf16
         ProfScope ps("fd_kp_kernel", st);
         const int rows = B * Tc;
-        // ~2 blocks per CU: split the 96 weight tiles over enough groups
         const int rblocks = cdiv(rows, KPK_ROWS);
         int groups = 1;
         while (groups < 32 && rblocks * groups < 512) groups *= 2;   // groups | 96
@@ -774,18 +964,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_KERNEL>(a, st, "fd_kp_kernel")));
       }
       const int dil = (int)std::pow(3, i);
-      if (bf && hop % 64 == 0) {
-        // one fused launch: pre-conv + LVC + gate (bf16 MFMA)
-        ProfScope ps("fd_lvc_fused", st);
-        const __bf16* Kb = reinterpret_cast<const __bf16*>(ws + W.Kf);
-        const __bf16* Wc = lookup_bf16(K.cv_w[i]);
-        if (hop % 128 == 0)
-          hipLaunchKernelGGL(lvc_fused_bf16_kernel<128>, dim3(B * Tc * (hop / 128)), dim3(256), 0, st, xn, ad, Kb,
-                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
-        else
-          hipLaunchKernelGGL(lvc_fused_bf16_kernel<64>, dim3(B * Tc * (hop / 64)), dim3(128), 0, st, xn, ad, Kb,
-                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
-      } else {
+      {
         {  // y = lrelu(conv_dil3^i(lrelu(x + a)) + b)
           GemmArgs a = make_gemm(B, (int)Tout, CI, K.cv_w[i], 96, K.cv_b[i], ws + W.y, Tout * CI, CI);
           for (int tap = 0; tap < 3; ++tap) {
