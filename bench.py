@@ -57,6 +57,8 @@ def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_lvc": sum(2 * r * 64 * 96 for r in rows) / 3.0,
         # fused pre-conv + LVC, launched for the hop >= 64 blocks only (bf16 path)
         "fd_lvc_fused": sum(2 * r * 32 * 96 + 2 * r * 64 * 96 for r in rows[1:]) / 2.0,
+        # whole LVC block (4 layers of pre-conv + LVC), hop >= 64 blocks (bf16 path)
+        "fd_lvc_block": sum(4 * (2 * r * 32 * 96 + 2 * r * 64 * 96) for r in rows[1:]) / 2.0,
         "fd_final_update": 2 * F * 256 * 32 * 7,
     }
 
@@ -83,6 +85,8 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_kp_kernel": F * (64 * 4 + 6144 * wb) + 6144 * 192 * wb,
         "fd_kp_hidden": F * (80 + 64 + 256) * 4 + (64 * 480 + 6 * 64 * 192 + 256 * 192) * wb,
         "fd_lvc_fused": sum(lvc_f) / 2.0,
+        # x in + a in + x out once per block, plus all 4 layers' kernels and biases
+        "fd_lvc_block": sum(r * 3 * per_row_io + F * 4 * kf_frame for r in rows[1:]) / 2.0,
         "fd_lvc": sum(lvc_v) / 3.0,
         "fd_upsample": sum(r * (1 + 1.0 / h) * per_row_io for r, h in zip(rows, (8, 8, 4))) / 3.0,
         "fd_final_update": F * 256 * (32 + 3) * 4,
@@ -204,7 +208,8 @@ def main():
             kernels[tag] = {"launches": cnt, "ms_total": round(ms, 3), "avg_us": round(ms / cnt * 1e3, 2),
                             "tflops": round(fl.get(tag, 0.0) * cnt / sec / 1e12, 2) if ms > 0 else 0.0,
                             "gbs": round(by.get(tag, 0.0) * cnt / sec / 1e9, 1) if ms > 0 else 0.0}
-        dom = max(kern.items(), key=lambda kv: kv[1][1])[0]
+        known = {k: v for k, v in kern.items() if k in fl and k in by}
+        dom = max(known.items(), key=lambda kv: kv[1][1])[0]
         cnt, ms = kern[dom]
         sec = ms * 1e-3
         intensity = fl[dom] / by[dom] if by.get(dom) else float("inf")
