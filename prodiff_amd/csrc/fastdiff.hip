@@ -30,6 +30,7 @@ struct fd_model {
   int ratios[4];
   int hops[4];
   int dtype;
+  int lvc_ts = 128;            // whole-block LVC tile (128/256); 0 = one fused launch per layer
   float* pool = nullptr;
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
   // step MLP
@@ -291,11 +292,23 @@ struct LvcBlockArgs {
   const float* bc[NLY];
   int Tc, hop;
 };
-constexpr int LB_TS = 256, LB_HALO = 44, LB_ROWS = LB_TS + 2 * LB_HALO, LB_UY = 360, LB_LD = 40;
+constexpr int LB_HALO = 44, LB_LD = 40;
+// TS = output samples per block.  TS=128 with 256 threads keeps LDS at ~78 KB, so two
+// blocks share a CU (one streams its tile in while the other computes).
+template <int TS> struct LbCfg {
+  static constexpr int ROWS = TS + 2 * LB_HALO;
+  static constexpr int UY = (TS + 84 + 2 + 31) / 32 * 32 + 8;    // y/u tile rows (+ tap reach)
+  static constexpr int URows = (UY - 8) + 2 * 3 > (TS + 2 + 31) / 32 * 32 + 54 ? (UY - 8) + 6 + 2
+                                                                               : (TS + 2 + 31) / 32 * 32 + 56;
+  static constexpr int NT = TS == 256 ? 512 : 256;
+};
 
-__global__ __launch_bounds__(512) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
+template <int TS>
+__global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
+  constexpr int LB_TS = TS, LB_ROWS = LbCfg<TS>::ROWS, NT = LbCfg<TS>::NT, NW = NT / 64;
+  constexpr int LB_UY = LbCfg<TS>::URows;
   __shared__ __attribute__((aligned(16))) float X[LB_ROWS * CI];
-  __shared__ __attribute__((aligned(16))) float Aa[LB_ROWS * CI];
+  __shared__ __attribute__((aligned(16))) __bf16 Aa[LB_ROWS * CI];      // audio_down, bf16
   __shared__ __attribute__((aligned(16))) __bf16 U[LB_UY * LB_LD];
   __shared__ __attribute__((aligned(16))) __bf16 Yb[LB_UY * LB_LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(512) void lvc_block_bf16_kernel(const LvcBlockArgs 
   const long long tb = t0 - LB_HALO;                 // time of local row 0
   const long long base = (long long)b * Lh;
 
-  for (int i = tid; i < LB_ROWS * 8; i += 512) {
+  for (int i = tid; i < LB_ROWS * 8; i += NT) {
     const int r = i >> 3, q = (i & 7) * 4;
     const long long t = tb + r;
     float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
@@ -314,7 +327,7 @@ __global__ __launch_bounds__(512) void lvc_block_bf16_kernel(const LvcBlockArgs 
       av = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + q);
     }
     *reinterpret_cast<float4*>(&X[r * CI + q]) = xv;
-    *reinterpret_cast<float4*>(&Aa[r * CI + q]) = av;
+    *reinterpret_cast<bf16x4*>(&Aa[r * CI + q]) = bf16x4{(__bf16)av.x, (__bf16)av.y, (__bf16)av.z, (__bf16)av.w};
   }
   __syncthreads();
 
@@ -327,13 +340,14 @@ __global__ __launch_bounds__(512) void lvc_block_bf16_kernel(const LvcBlockArgs 
     const int ulo = lo - 1 - d;                                   // local row of U[0]
     // (1) u = lrelu(x + a), zero outside the utterance
     const int nu = nyt * 32 + 2 * d;
-    for (int i = tid; i < nu * 8; i += 512) {
+    for (int i = tid; i < nu * 8; i += NT) {
       const int j = i >> 3, q = (i & 7) * 4, r = ulo + j;
       const long long t = tb + r;
       bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
       if (r >= 0 && r < LB_ROWS && t >= 0 && t < Lh) {
         const float4 xv = *reinterpret_cast<const float4*>(&X[r * CI + q]);
-        const float4 av = *reinterpret_cast<const float4*>(&Aa[r * CI + q]);
+        const bf16x4 ab = *reinterpret_cast<const bf16x4*>(&Aa[r * CI + q]);
+        const float4 av = make_float4((float)ab[0], (float)ab[1], (float)ab[2], (float)ab[3]);
         float u0 = xv.x + av.x, u1 = xv.y + av.y, u2 = xv.z + av.z, u3 = xv.w + av.w;
         u0 = u0 >= 0.f ? u0 : 0.2f * u0; u1 = u1 >= 0.f ? u1 : 0.2f * u1;
         u2 = u2 >= 0.f ? u2 : 0.2f * u2; u3 = u3 >= 0.f ? u3 : 0.2f * u3;
@@ -349,7 +363,7 @@ __global__ __launch_bounds__(512) void lvc_block_bf16_kernel(const LvcBlockArgs 
       for (int kk = 0; kk < 6; ++kk)
         wf[kk] = *reinterpret_cast<const bf16x8*>(P.Wc[l] + r32 * 96 + kk * 16 + h * 8);
       const float bias = P.bc[l][r32];
-      for (int mt = wave; mt < nyt; mt += 8) {
+      for (int mt = wave; mt < nyt; mt += NW) {
         f32x16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -374,7 +388,7 @@ __global__ __launch_bounds__(512) void lvc_block_bf16_kernel(const LvcBlockArgs 
     // (3) o = Bf + K_frame . [y(t-1); y(t); y(t+1)] ; x += a + sigmoid(o_g) tanh(o_f)
     {
       const int nlt = (hi - lo + 31) / 32;
-      for (int mt = wave; mt < nlt; mt += 8) {
+      for (int mt = wave; mt < nlt; mt += NW) {
         const long long ts = tb + lo + mt * 32;          // time of the tile's first row
         const long long tlast = ts + 31;
         int fa = (int)((ts < 0 ? 0 : ts) / hop), fb = (int)((tlast >= Lh ? Lh - 1 : tlast) / hop);
@@ -419,14 +433,14 @@ __global__ __launch_bounds__(512) void lvc_block_bf16_kernel(const LvcBlockArgs 
             const bool second = (int)(t / hop) != fa;
             const float og = second ? g1[reg] + bgb : g0[reg] + bga;
             const float of = second ? f1[reg] + blb : f0[reg] + bla;
-            X[row * CI + r32] += Aa[row * CI + r32] + sigmoidf_(og) * tanhf(of);
+            X[row * CI + r32] += (float)Aa[row * CI + r32] + sigmoidf_(og) * tanhf(of);
           }
         }
       }
     }
     __syncthreads();
   }
-  for (int i = tid; i < LB_TS * 8; i += 512) {
+  for (int i = tid; i < LB_TS * 8; i += NT) {
     const int r = i >> 3, q = (i & 7) * 4;
     const long long t = t0 + r;
     if (t < Lh)
@@ -917,7 +931,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       PD_LAUNCH_CHECK();
     }
     // --- 4 LVC layers (modules.py:208-217)
-    if (bf && hop >= 64) {
+    if (bf && hop >= 64 && m->lvc_ts > 0) {
       // every layer's kernels first (frame-major bf16), then the whole block in one launch
       __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf);
       const int rows = B * Tc;
@@ -938,7 +952,10 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       la.xin = xn; la.xout = ws + W.y; la.a = ad; la.Bf = ws + W.Bf; la.Tc = Tc; la.hop = hop;
       {
         ProfScope ps("fd_lvc_block", st);
-        hipLaunchKernelGGL(lvc_block_bf16_kernel, dim3(cdiv(Tout, LB_TS), B), dim3(512), 0, st, la);
+        if (m->lvc_ts == 256)
+          hipLaunchKernelGGL(lvc_block_bf16_kernel<256>, dim3(cdiv(Tout, 256), B), dim3(512), 0, st, la);
+        else
+          hipLaunchKernelGGL(lvc_block_bf16_kernel<128>, dim3(cdiv(Tout, 128), B), dim3(256), 0, st, la);
         PD_LAUNCH_CHECK();
       }
       x = ws + W.y;
@@ -964,7 +981,18 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_KERNEL>(a, st, "fd_kp_kernel")));
       }
       const int dil = (int)std::pow(3, i);
-      {
+      if (bf && hop % 64 == 0) {
+        // one fused launch per layer: pre-conv + LVC + gate (bf16 MFMA)
+        ProfScope ps("fd_lvc_fused", st);
+        const __bf16* Kb = reinterpret_cast<const __bf16*>(ws + W.Kf);
+        const __bf16* Wc = lookup_bf16(K.cv_w[i]);
+        if (hop % 128 == 0)
+          hipLaunchKernelGGL(lvc_fused_bf16_kernel<128>, dim3(B * Tc * (hop / 128)), dim3(256), 0, st, xn, ad, Kb,
+                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
+        else
+          hipLaunchKernelGGL(lvc_fused_bf16_kernel<64>, dim3(B * Tc * (hop / 64)), dim3(128), 0, st, xn, ad, Kb,
+                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
+      } else {
         {  // y = lrelu(conv_dil3^i(lrelu(x + a)) + b)
           GemmArgs a = make_gemm(B, (int)Tout, CI, K.cv_w[i], 96, K.cv_b[i], ws + W.y, Tout * CI, CI);
           for (int tap = 0; tap < 3; ++tap) {
@@ -1012,6 +1040,7 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   fd_model* m = new fd_model();
   m->nblocks = dims->num_blocks;
   m->dtype = dtype;
+  if (const char* e = getenv("PRODIFF_LVC_TS")) m->lvc_ts = atoi(e);   // A/B switch (bench/tests)
   int hop = 1;
   for (int n = 0; n < m->nblocks; ++n) {
     m->ratios[n] = dims->upsample_ratios[n];
