@@ -23,6 +23,20 @@ constexpr int HK = 64;   // kpnet hidden
 constexpr int NLY = 4;   // lvc layers per block
 constexpr int KPERLAYER = 2 * CI * CI * 3;   // 6144 kernel values per frame per layer
 constexpr int EMB_IN = 128, EMB_MID = 512, EMB_OUT = 512;
+
+// Frame-major LVC kernel layout is MFMA-fragment order: value (o, q) of a frame's
+// 64x96 kernel (o = output channel, q = tap*32 + ci) lives at
+//   ((o/32 * 6 + q/16) * 64 + ((q%16)/8) * 32 + o%32) * 8 + q%8,
+// i.e. [gate|filter tile][k-step][lane][8], so each B-fragment load of the LVC
+// MFMA is one contiguous 1 KB per wave.
+__host__ __device__ inline int kf_packed(int o, int q) {
+  return (((o >> 5) * 6 + (q >> 4)) * 64 + ((q & 15) >> 3) * 32 + (o & 31)) * 8 + (q & 7);
+}
+__host__ __device__ inline void kf_unpack(int p, int& o, int& q) {
+  const int j = p & 7, l = (p >> 3) & 63, kkn = p >> 9;
+  o = (kkn / 6) * 32 + (l & 31);
+  q = (kkn % 6) * 16 + (l >> 5) * 8 + j;
+}
 }  // namespace
 
 struct fd_model {
@@ -137,8 +151,9 @@ __global__ __launch_bounds__(256) void lvc_kernel(float* __restrict__ x, const f
   const long long L = (long long)Tc * hop;
   const KT* kf = Kf + (long long)g * kf_ld;
   for (int i = tid; i < 64 * 96; i += 256) {
-    int o = i / 96, qq = i - o * 96;
-    ks[o * 97 + qq] = (float)kf[i];
+    int oo, q2;
+    kf_unpack(i, oo, q2);   // fragment-major -> [o][q] rows for the VALU loop
+    ks[oo * 97 + q2] = (float)kf[i];
   }
   if (tid < 64) bs[tid] = Bf[(long long)g * bf_ld + tid];
   const int c = tid & 31, sg = tid >> 5;
@@ -258,8 +273,8 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
     for (int kk = 0; kk < 6; ++kk) {
       const int tap = kk >> 1, ci0 = (kk & 1) * 16;
       const bf16x8 yf = *reinterpret_cast<const bf16x8*>(Y + (mt * 32 + r32 + tap) * LD + ci0 + h * 8);
-      const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kf + r32 * 96 + kk * 16 + h * 8);
-      const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kf + (32 + r32) * 96 + kk * 16 + h * 8);
+      const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kf + (kk * 64 + lane) * 8);
+      const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kf + ((6 + kk) * 64 + lane) * 8);
       ag = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf, kg, ag, 0, 0, 0);
       afl = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf, kl, afl, 0, 0, 0);
     }
@@ -406,8 +421,8 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
         const __bf16* ka = P.Kf[l] + ((long long)b * Tc + fa) * KPERLAYER;
 #pragma unroll
         for (int kk = 0; kk < 6; ++kk) {
-          const bf16x8 kg = *reinterpret_cast<const bf16x8*>(ka + r32 * 96 + kk * 16 + h * 8);
-          const bf16x8 kl = *reinterpret_cast<const bf16x8*>(ka + (32 + r32) * 96 + kk * 16 + h * 8);
+          const bf16x8 kg = *reinterpret_cast<const bf16x8*>(ka + (kk * 64 + lane) * 8);
+          const bf16x8 kl = *reinterpret_cast<const bf16x8*>(ka + ((6 + kk) * 64 + lane) * 8);
           g0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kg, g0, 0, 0, 0);
           f0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kl, f0, 0, 0, 0);
         }
@@ -415,8 +430,8 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
           const __bf16* kb2 = P.Kf[l] + ((long long)b * Tc + fb) * KPERLAYER;
 #pragma unroll
           for (int kk = 0; kk < 6; ++kk) {
-            const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kb2 + r32 * 96 + kk * 16 + h * 8);
-            const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kb2 + (32 + r32) * 96 + kk * 16 + h * 8);
+            const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kb2 + (kk * 64 + lane) * 8);
+            const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kb2 + ((6 + kk) * 64 + lane) * 8);
             g1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kg, g1, 0, 0, 0);
             f1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kl, f1, 0, 0, 0);
           }
@@ -737,7 +752,7 @@ __global__ void pack_kernel_conv_kernel(float* dst, float* dst_b, const float* s
   int h = (int)(r % HK);
   int ch = (int)(r / HK);
   int tap = ch % 3, o = (ch / 3) % 64, ci = (ch / 192) % 32, layer = ch / (192 * 32);
-  long long row = (long long)layer * KPERLAYER + o * 96 + tap * 32 + ci;
+  long long row = (long long)layer * KPERLAYER + kf_packed(o, tap * 32 + ci);
   dst[row * (3 * HK) + kt * HK + h] = src[i];
   if (kt == 0 && h == 0) dst_b[row] = src_b[ch];
 }
