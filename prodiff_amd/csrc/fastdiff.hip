@@ -404,9 +404,11 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
     {
       const int nlt = (hi - lo + 31) / 32;
       for (int mt = wave; mt < nlt; mt += NW) {
-        const long long ts = tb + lo + mt * 32;          // time of the tile's first row
-        const long long tlast = ts + 31;
-        int fa = (int)((ts < 0 ? 0 : ts) / hop), fb = (int)((tlast >= Lh ? Lh - 1 : tlast) / hop);
+        // utterance-local times fit in 32 bits; no 64-bit division anywhere per element
+        const int ts = (int)(tb + lo + mt * 32);           // time of the tile's first row
+        const int tlast = ts + 31;
+        const int Lhi = (int)Lh;
+        int fa = (ts < 0 ? 0 : ts) / hop, fb = (tlast >= Lhi ? Lhi - 1 : tlast) / hop;
         if (fa > Tc - 1) fa = Tc - 1;
         if (fb < fa) fb = fa;
         bf16x8 yf[6];
@@ -443,9 +445,9 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
         for (int reg = 0; reg < 16; ++reg) {
           const int rr = (reg & 3) + 8 * (reg >> 2) + 4 * h;
           const int row = lo + mt * 32 + rr;
-          const long long t = ts + rr;
-          if (row < hi && t >= 0 && t < Lh) {
-            const bool second = (int)(t / hop) != fa;
+          const int t = ts + rr;
+          if (row < hi && t >= 0 && t < Lhi) {
+            const bool second = t >= (fa + 1) * hop;        // row belongs to frame fb
             const float og = second ? g1[reg] + bgb : g0[reg] + bga;
             const float of = second ? f1[reg] + blb : f0[reg] + bla;
             X[row * CI + r32] += (float)Aa[row * CI + r32] + sigmoidf_(og) * tanhf(of);
