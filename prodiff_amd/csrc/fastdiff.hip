@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void lvc_kernel(float* __restrict__ x, const f
         }
       }
       long long idx = ((long long)b * L + (long long)l * hop + s0 + s) * CI + c;
-      x[idx] = x[idx] + a[idx] + sigmoidf_(og) * tanhf(of);
+      x[idx] = x[idx] + a[idx] + sigmoidf_(og) * tanhf_(of);
     }
   }
 }
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
     for (int reg = 0; reg < 16; ++reg) {
       const int s = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
       const long long idx = (base + t0 + s) * CI + r32;
-      x[idx] = x[idx] + a[idx] + sigmoidf_(ag[reg] + bg) * tanhf(afl[reg] + bl);
+      x[idx] = x[idx] + a[idx] + sigmoidf_(ag[reg] + bg) * tanhf_(afl[reg] + bl);
     }
   }
 }
@@ -328,14 +328,14 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
   __shared__ __attribute__((aligned(16))) __bf16 Yb[LB_UY * LB_LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, Tc = P.Tc, hop = P.hop;
-  const long long Lh = (long long)Tc * hop;
-  const long long t0 = (long long)blockIdx.x * LB_TS;
-  const long long tb = t0 - LB_HALO;                 // time of local row 0
+  const int Lh = Tc * hop;                           // utterance-local times fit in 32 bits
+  const int t0 = blockIdx.x * LB_TS;
+  const int tb = t0 - LB_HALO;                       // time of local row 0
   const long long base = (long long)b * Lh;
 
   for (int i = tid; i < LB_ROWS * 8; i += NT) {
     const int r = i >> 3, q = (i & 7) * 4;
-    const long long t = tb + r;
+    const int t = tb + r;
     float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
     if (t >= 0 && t < Lh) {
       xv = *reinterpret_cast<const float4*>(P.xin + (base + t) * CI + q);
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
     const int nu = nyt * 32 + 2 * d;
     for (int i = tid; i < nu * 8; i += NT) {
       const int j = i >> 3, q = (i & 7) * 4, r = ulo + j;
-      const long long t = tb + r;
+      const int t = tb + r;
       bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
       if (r >= 0 && r < LB_ROWS && t >= 0 && t < Lh) {
         const float4 xv = *reinterpret_cast<const float4*>(&X[r * CI + q]);
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const int yj = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-          const long long t = tb + lo - 1 + yj;
+          const int t = tb + lo - 1 + yj;
           float y = acc[reg] + bias;
           y = y >= 0.f ? y : 0.2f * y;
           if (t < 0 || t >= Lh) y = 0.f;
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
         // utterance-local times fit in 32 bits; no 64-bit division anywhere per element
         const int ts = (int)(tb + lo + mt * 32);           // time of the tile's first row
         const int tlast = ts + 31;
-        const int Lhi = (int)Lh;
+        const int Lhi = Lh;
         int fa = (ts < 0 ? 0 : ts) / hop, fb = (tlast >= Lhi ? Lhi - 1 : tlast) / hop;
         if (fa > Tc - 1) fa = Tc - 1;
         if (fb < fa) fb = fa;
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
             const bool second = t >= (fa + 1) * hop;        // row belongs to frame fb
             const float og = second ? g1[reg] + bgb : g0[reg] + bga;
             const float of = second ? f1[reg] + blb : f0[reg] + bla;
-            X[row * CI + r32] += (float)Aa[row * CI + r32] + sigmoidf_(og) * tanhf(of);
+            X[row * CI + r32] += (float)Aa[row * CI + r32] + sigmoidf_(og) * tanhf_(of);
           }
         }
       }
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
   }
   for (int i = tid; i < LB_TS * 8; i += NT) {
     const int r = i >> 3, q = (i & 7) * 4;
-    const long long t = t0 + r;
+    const int t = t0 + r;
     if (t < Lh)
       *reinterpret_cast<float4*>(P.xout + (base + t) * CI + q) =
           *reinterpret_cast<const float4*>(&X[(LB_HALO + r) * CI + q]);

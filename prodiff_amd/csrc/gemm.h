@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
         const int n = nb + r32;
         float v0 = acc[i][0][reg] + a.bias[n];
         float v1 = acc[i][1][reg] + a.bias[a.half + n];
-        a.out[(long long)b * a.out_bs + (long long)t * a.out_ld + n] = sigmoidf_(v0) * tanhf(v1);
+        a.out[(long long)b * a.out_bs + (long long)t * a.out_ld + n] = sigmoidf_(v0) * tanhf_(v1);
       } else if constexpr (EPI == EPI_RESSKIP) {
         const int n = nb + r32;
         float v0 = acc[i][0][reg] + a.bias[n];
