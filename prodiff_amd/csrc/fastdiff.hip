@@ -44,7 +44,7 @@ struct fd_model {
   int ratios[4];
   int hops[4];
   int dtype;
-  int lvc_ts = 128;            // whole-block LVC tile (128/256); 0 = one fused launch per layer
+  int lvc_ts = 0;              // whole-block LVC tile (128/256); 0 = one fused launch per layer (default: faster today)
   float* pool = nullptr;
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
   // step MLP
