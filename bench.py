@@ -44,6 +44,7 @@ def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
         "wn_inproj": 2 * F * M * C,
         "wn_gate": 2 * F * 2 * C * (3 * C + H),
         "wn_resskip": 2 * F * 2 * C * C,
+        "wn_layer": 2 * F * 2 * C * (3 * C + H) + 2 * F * 2 * C * C,     # fused gate + res/skip (bf16)
         "wn_skiphead": 2 * F * C * C,
         "wn_outproj_posterior": 2 * F * M * C,
         "fd_first_conv": 2 * F * 256 * 32 * 7,
@@ -79,6 +80,7 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         "wn_inproj": F * (M + C) * 4 + C * M * wb,
         "wn_gate": F * (C + H + C) * 4 + 2 * C * (3 * C + H) * wb,
         "wn_resskip": F * (C + 2 * C + 2 * C) * 4 + 2 * C * C * wb,
+        "wn_layer": F * (C + H + C + 2 * C) * 4 + 2 * C * (4 * C + H) * wb,
         "wn_skiphead": F * 2 * C * 4 + C * C * wb,
         "wn_outproj_posterior": F * (C + 3 * M) * 4 + M * C * wb,
         "fd_first_conv": F * 256 * (1 + 32) * 4,

@@ -26,12 +26,133 @@ struct pd_wavenet {
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
   size_t pool_n = 0;
   float *Win, *b_in, *W1, *b1, *W2, *b2, *Wd, *bd, *Wl1, *bl1, *Wl2, *bl2, *Ws, *bs, *Wo, *bo;
+  // bf16 path, C == 256: residual-layer weights in MFMA-fragment order (wn_layer_bf16_kernel)
+  __bf16* frag = nullptr;
+  __bf16* W1f = nullptr;   // [L][2C/32 tiles][K/16 steps][64 lanes][8]
+  __bf16* W2f = nullptr;
 };
 
 namespace {
 
+constexpr int WNF_C = 256;   // channels the fused layer kernel is built for (base_config.yaml:211)
+
+// dst[((nt*KS + ks)*64 + lane)*8 + j] = bf16(src[(nt*32 + lane%32) * ld + ks*16 + (lane/32)*8 + j])
+__global__ void pack_frag_kernel(__bf16* dst, const float* src, int N, int K, int ld) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)N * K) return;
+  const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
+  const long long rest = i >> 9;
+  const int KS = K / 16, ks = (int)(rest % KS), nt = (int)(rest / KS);
+  const int n = nt * 32 + (lane & 31), k = ks * 16 + (lane >> 5) * 8 + j;
+  dst[i] = (__bf16)src[(long long)n * ld + k];
+}
+
+// One WaveNet residual layer, bf16 MFMA, fully fused (wavenet.py:60-72):
+//   z = W1 . [x(t-d)+dp; x(t)+dp; x(t+d)+dp; cond(t)] + b1      (K = 3C + H)
+//   g = sigmoid(z[:C]) * tanh(z[C:])
+//   o = W2 . g + b2 ;  x = (x + o[:C]) / sqrt2 ;  skip (+)= o[C:]
+// Block = 32 rows (frames, may straddle utterances), 8 waves; wave w owns gate/filter
+// columns [32w, 32w+32) / [C+32w, ...) of GEMM1 and residual/skip columns of GEMM2,
+// so both epilogues pair their halves in registers.  The K=1024 input row lives in
+// LDS (bf16); weights stream from L2 in fragment order (1 KB per wave-load).
+struct WnLayerArgs {
+  const float* xin;       // [B][T][C] layer input (other blocks read its halo rows,
+  float* xout;            //            so the update goes to a second buffer)
+  float* skip;            // [B][T][C]
+  const float* cond;      // [B][T][H]
+  const float* dp;        // this layer's diffusion projection, dp[b*dp_ld + c]
+  int dp_ld;
+  const __bf16* W1f;      // [2C/32][K1/16][64][8]
+  const float* b1;        // [2C]
+  const __bf16* W2f;      // [2C/32][C/16][64][8]
+  const float* b2;        // [2C]
+  int B, T, H, dil, first;
+};
+
+template <int KMAX>
+__global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P) {
+  constexpr int C = WNF_C;
+  constexpr int LDA = KMAX + 8, LDG = C + 8;     // 16-B-offset rows: conflict-free b128 fragment reads
+  __shared__ __attribute__((aligned(16))) __bf16 As[32 * LDA];
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[32 * LDG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int H = P.H, K1 = 3 * C + H, rows = P.B * P.T, R0 = blockIdx.x * 32;
+  // stage [x(t-d)+dp; x(t)+dp; x(t+d)+dp; cond] as bf16 (zero outside each row's utterance)
+  const int ng = K1 / 4;
+  for (int i = tid; i < 32 * ng; i += 512) {
+    const int r = i / ng, g = (i - r * ng) * 4, R = R0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (R < rows) {
+      const int b = R / P.T, t = R - b * P.T;
+      if (g < 3 * C) {
+        const int tap = g / C, c = g - tap * C, tt = t + (tap - 1) * P.dil;
+        if (tt >= 0 && tt < P.T) {
+          v = *reinterpret_cast<const float4*>(P.xin + ((long long)b * P.T + tt) * C + c);
+          const float4 d = *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + c);
+          v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
+        }
+      } else {
+        v = *reinterpret_cast<const float4*>(P.cond + ((long long)b * P.T + t) * H + (g - 3 * C));
+      }
+    }
+    *reinterpret_cast<bf16x4*>(&As[r * LDA + g]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+  }
+  __syncthreads();
+
+  // GEMM1: gate tile nt = wave, filter tile nt = 8 + wave
+  const int KS1 = K1 / 16;
+  const bf16x8* wg = reinterpret_cast<const bf16x8*>(P.W1f) + (long long)wave * KS1 * 64 + lane;
+  const bf16x8* wf = reinterpret_cast<const bf16x8*>(P.W1f) + (long long)(8 + wave) * KS1 * 64 + lane;
+  f32x16 ag, af;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { ag[r] = 0.f; af[r] = 0.f; }
+#pragma unroll 8
+  for (int ks = 0; ks < KS1; ++ks) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[r32 * LDA + ks * 16 + h * 8]);
+    const bf16x8 bgt = wg[ks * 64], bft = wf[ks * 64];
+    ag = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bgt, ag, 0, 0, 0);
+    af = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bft, af, 0, 0, 0);
+  }
+  {
+    const int n = wave * 32 + r32;
+    const float bgv = P.b1[n], bfv = P.b1[C + n];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int r = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      Gs[r * LDG + n] = (__bf16)(sigmoidf_(ag[reg] + bgv) * tanhf_(af[reg] + bfv));
+    }
+  }
+  __syncthreads();
+
+  // GEMM2: residual tile nt = wave, skip tile nt = 8 + wave
+  constexpr int KS2 = C / 16;
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)wave * KS2 * 64 + lane;
+  const bf16x8* wsk = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)(8 + wave) * KS2 * 64 + lane;
+  f32x16 ar, as_;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { ar[r] = 0.f; as_[r] = 0.f; }
+#pragma unroll
+  for (int ks = 0; ks < KS2; ++ks) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Gs[r32 * LDG + ks * 16 + h * 8]);
+    ar = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, wr[ks * 64], ar, 0, 0, 0);
+    as_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, wsk[ks * 64], as_, 0, 0, 0);
+  }
+  const int n = wave * 32 + r32;
+  const float brv = P.b2[n], bsv = P.b2[C + n];
+  const float rs2 = 0.70710678118654752440f;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int R = R0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    if (R < rows) {
+      const long long o = (long long)R * C + n;      // rows are b*T + t: contiguous [B][T][C]
+      P.xout[o] = (P.xin[o] + ar[reg] + brv) * rs2;
+      P.skip[o] = (P.first ? 0.f : P.skip[o]) + as_[reg] + bsv;
+    }
+  }
+}
+
 struct WsLayout {
-  size_t x, g, skip, hs, xin, condT, outT, steps, emb, h1, d, dproj, total;
+  size_t x, x2, g, skip, hs, xin, condT, outT, steps, emb, h1, d, dproj, total;
 };
 
 WsLayout ws_layout(const pd_wavenet* h, int B, int T, int S) {
@@ -44,6 +165,7 @@ WsLayout ws_layout(const pd_wavenet* h, int B, int T, int S) {
   };
   const size_t BT = (size_t)B * T;
   w.x = take(BT * h->C);
+  w.x2 = take(BT * h->C);
   w.g = take(BT * h->C);
   w.skip = take(BT * h->C);
   w.hs = take(BT * h->C);
@@ -85,6 +207,21 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     a.act = ACT_RELU;
     PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_WN_INPROJ>(a, st, "wn_inproj")));
   }
+  if (h->W1f) {
+    // bf16, C == 256: one fused launch per residual layer, x ping-pongs x <-> x2
+    float* xb[2] = {x, ws + Lw.x2};
+    for (int l = 0; l < Ly; ++l) {
+      WnLayerArgs P{};
+      P.xin = xb[l & 1]; P.xout = xb[(l + 1) & 1]; P.skip = skip; P.cond = cond;
+      P.dp = dproj + (size_t)l * C; P.dp_ld = Ly * C;
+      P.W1f = h->W1f + (size_t)l * 2 * C * (3 * C + H); P.b1 = h->bl1 + (size_t)l * 2 * C;
+      P.W2f = h->W2f + (size_t)l * 2 * C * C; P.b2 = h->bl2 + (size_t)l * 2 * C;
+      P.B = B; P.T = T; P.H = H; P.dil = 1 << (l % h->cyc); P.first = (l == 0);
+      ProfScope ps("wn_layer", st);
+      hipLaunchKernelGGL(wn_layer_bf16_kernel<1024>, dim3(cdiv((long long)B * T, 32)), dim3(512), 0, st, P);
+      PD_LAUNCH_CHECK();
+    }
+  } else
   for (int l = 0; l < Ly; ++l) {
     const int dil = 1 << (l % h->cyc);
     {  // z = dilconv(x + dproj) + condproj ; g = sigmoid(z[:C]) * tanh(z[C:])   (wavenet.py:60-67)
@@ -202,6 +339,22 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
       PD_HIP(hipMalloc(&h->pool_bf, off * sizeof(__bf16)));
       PD_TRY(convert_f32_bf16(h->pool, h->pool_bf, (long long)off, st));
       register_bf16_pool(h->pool, off, h->pool_bf);
+      if (C == WNF_C && H % 32 == 0 && 3 * C + H <= 1024) {
+        const int K1 = 3 * C + H;
+        const size_t per = (size_t)2 * C * K1 + (size_t)2 * C * C;
+        PD_HIP(hipMalloc(&h->frag, (size_t)L * per * sizeof(__bf16)));
+        h->W1f = h->frag;
+        h->W2f = h->frag + (size_t)L * 2 * C * K1;
+        for (int l = 0; l < L; ++l) {
+          const long long n1 = (long long)2 * C * K1, n2 = (long long)2 * C * C;
+          hipLaunchKernelGGL(pack_frag_kernel, dim3(cdiv(n1, 256)), dim3(256), 0, st, h->W1f + l * n1,
+                             h->Wl1 + (size_t)l * 2 * C * h->ldw1, 2 * C, K1, h->ldw1);
+          PD_LAUNCH_CHECK();
+          hipLaunchKernelGGL(pack_frag_kernel, dim3(cdiv(n2, 256)), dim3(256), 0, st, h->W2f + l * n2,
+                             h->Wl2 + (size_t)l * 2 * C * C, 2 * C, C, C);
+          PD_LAUNCH_CHECK();
+        }
+      }
     }
     return PD_OK;
   };
@@ -209,6 +362,7 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
   if (rc != PD_OK) {
     (void)hipFree(h->pool);
     if (h->pool_bf) (void)hipFree(h->pool_bf);
+    if (h->frag) (void)hipFree(h->frag);
     delete h;
     return rc;
   }
@@ -222,6 +376,7 @@ void pd_wavenet_destroy(pd_wavenet* h) {
     unregister_bf16_pool(h->pool);
     (void)hipFree(h->pool_bf);
   }
+  if (h->frag) (void)hipFree(h->frag);
   (void)hipFree(h->pool);
   delete h;
 }
