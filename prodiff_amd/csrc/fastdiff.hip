@@ -605,12 +605,14 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 // The MFMA computes C[n][frame] (weights as the A operand), so a lane holds 4
 // consecutive kernel values of one frame and stores 8 B at a time.
 constexpr int KPK_ROWS = 128, KPK_NT = 64, KPK_LDW = 200;   // 400-B LDS rows: conflict-free b128 reads
+constexpr int KPK_LDO = 72;                                  // output transpose rows: 64 + 8 pad
 __global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __restrict__ hin,
                                                              const __bf16* __restrict__ W,
                                                              const float* __restrict__ bias,
                                                              __bf16* __restrict__ Kf, int Tc, int rows,
                                                              int tiles_per_block) {
   __shared__ __attribute__((aligned(16))) __bf16 Ws[2][KPK_NT * KPK_LDW];
+  __shared__ __attribute__((aligned(16))) __bf16 Ot[4][32 * KPK_LDO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int R = blockIdx.x * KPK_ROWS + wave * 32 + r32;     // frame (C column) of this lane
   const int tile0 = blockIdx.y * tiles_per_block;
@@ -665,7 +667,6 @@ __global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __rest
   }
   store_tile(0);
   __syncthreads();
-  __bf16* out = Kf + (long long)R * KPERLAYER;
   for (int it = 0; it < tiles_per_block; ++it) {
     const int buf = it & 1;
     if (it + 1 < tiles_per_block) load_tile(tile0 + it + 1);
@@ -682,19 +683,28 @@ __global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __rest
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[kk], acc[j], 0, 0, 0);
       }
     }
-    // C[n][frame]: this lane owns frame R, rows n = n0 + 32j + 8g + 4h + (0..3)
+    // C[n][frame]: this lane owns frame R, rows n = n0 + 32j + 8g + 4h + (0..3).
+    // Transpose through LDS so each store instruction writes 8 frames x 128 B full lines.
     const int n0 = (tile0 + it) * KPK_NT;
-    if (R < rows) {
+    __bf16* ot = Ot[wave];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int n = n0 + j * 32 + 8 * g + 4 * h;
-          const float4 bn = *reinterpret_cast<const float4*>(bias + n);
-          bf16x4 v = {(__bf16)(acc[j][4 * g] + bn.x), (__bf16)(acc[j][4 * g + 1] + bn.y),
-                      (__bf16)(acc[j][4 * g + 2] + bn.z), (__bf16)(acc[j][4 * g + 3] + bn.w)};
-          *reinterpret_cast<bf16x4*>(out + n) = v;
-        }
+      for (int g = 0; g < 4; ++g) {
+        const int nl = j * 32 + 8 * g + 4 * h;
+        const float4 bn = *reinterpret_cast<const float4*>(bias + n0 + nl);
+        *reinterpret_cast<bf16x4*>(&ot[r32 * KPK_LDO + nl]) =
+            bf16x4{(__bf16)(acc[j][4 * g] + bn.x), (__bf16)(acc[j][4 * g + 1] + bn.y),
+                   (__bf16)(acc[j][4 * g + 2] + bn.z), (__bf16)(acc[j][4 * g + 3] + bn.w)};
+      }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
+      const int Rf = blockIdx.x * KPK_ROWS + wave * 32 + fl;
+      const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KPK_LDO + ch]);
+      if (Rf < rows) *reinterpret_cast<uint4*>(Kf + (long long)Rf * KPERLAYER + n0 + ch) = v;
     }
     if (it + 1 < tiles_per_block) store_tile(buf ^ 1);
     __syncthreads();
