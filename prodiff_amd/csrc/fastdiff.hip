@@ -467,18 +467,21 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
 }
 
 // ------------------------------------------------------------------ kernel predictor (bf16)
+// Batched over grid.z = step * nb + block: the hidden stack depends only on the mel
+// and the step embedding, so a sampler runs it for every step and block in ONE launch.
 struct KPArgs {
   const float* condT;       // [B][Tc][80] mel, time-major
-  const float* nz;          // fc_t(emb) rows for this block: nz[b*nz_ld + c]
-  int nz_ld;
-  const __bf16* Win;        // [64][5*96]   (tap*96 + ci)
-  const float* bin;
-  const __bf16* Wr[6];      // [64][3*64]
-  const float* br[6];
-  const __bf16* Wb;         // [256][3*64]  bias_conv
-  const float* bb;
-  float* hout;              // [B][Tc][64]  h = h0 + R(h0)
-  float* Bf;                // [B][Tc][256] LVC biases
+  const float* nz;          // fc_t(emb): row of (step s, utterance b, block n) at
+  int nz_step, nz_ld;       //   nz + s*nz_step + b*nz_ld + n*80
+  int nb, B;
+  const __bf16* Win[4];     // per block: [64][5*96]   (tap*96 + ci)
+  const float* bin[4];
+  const __bf16* Wr[4][6];   // [64][3*64]
+  const float* br[4][6];
+  const __bf16* Wb[4];      // [256][3*64]  bias_conv
+  const float* bb[4];
+  float* hout;              // [z][B][Tc][64]  h = h0 + R(h0)
+  float* Bf;                // [z][B][Tc][256] LVC biases
   int Tc;
 };
 
@@ -494,7 +497,11 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   __shared__ __attribute__((aligned(16))) __bf16 Hb[3][98 * LDH];   // H0, R0, R1 (+1 zero row each side)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, f0 = blockIdx.x * 64, Tc = A.Tc;
+  const int z = blockIdx.z, step = z / A.nb, nblk = z - step * A.nb;
   const long long rb = (long long)b * Tc;
+  const float* nzrow = A.nz + (long long)step * A.nz_step + (long long)b * A.nz_ld + nblk * CC;
+  float* hout = A.hout + (long long)z * A.B * Tc * HK;
+  float* Bfo = A.Bf + (long long)z * A.B * Tc * (2 * CI * NLY);
 
   // c' = c + fc_t(e) on frames f0-18 .. f0+81 (channels 80..95 zero)
   for (int i = tid; i < 100 * 24; i += 256) {
@@ -502,7 +509,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
     bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
     if (g < CC && f >= 0 && f < Tc) {
       const float4 c = *reinterpret_cast<const float4*>(A.condT + (rb + f) * CC + g);
-      const float4 n = *reinterpret_cast<const float4*>(A.nz + (long long)b * A.nz_ld + g);
+      const float4 n = *reinterpret_cast<const float4*>(nzrow + g);
       v = bf16x4{(__bf16)(c.x + n.x), (__bf16)(c.y + n.y), (__bf16)(c.z + n.z), (__bf16)(c.w + n.w)};
     }
     *reinterpret_cast<bf16x4*>(Cs + p * LDC + g) = v;
@@ -520,7 +527,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const __bf16* wrow = A.Win + (nt * 32 + r32) * 480 + h * 8;
+    const __bf16* wrow = A.Win[nblk] + (nt * 32 + r32) * 480 + h * 8;
 #pragma unroll 6
     for (int kk = 0; kk < 30; ++kk) {
       const int tap = kk / 6, kc = kk - tap * 6;
@@ -529,7 +536,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
     }
     const int n = nt * 32 + r32;
-    const float bias = A.bin[n];
+    const float bias = A.bin[nblk][n];
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int p = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, f = f0 - 16 + p;
@@ -550,7 +557,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const __bf16* wrow = A.Wr[j] + (nt * 32 + r32) * 192 + h * 8;
+      const __bf16* wrow = A.Wr[nblk][j] + (nt * 32 + r32) * 192 + h * 8;
 #pragma unroll
       for (int kk = 0; kk < 12; ++kk) {
         const int tap = kk >> 2, kc = kk & 3;
@@ -559,7 +566,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
       }
       const int n = nt * 32 + r32;
-      const float bias = A.br[j][n];
+      const float bias = A.br[nblk][j][n];
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int p = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, f = f0 - 16 + p;
@@ -568,7 +575,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
         if (j == 5) v += keep[q][reg];           // h = h0 + R(h0)
         if (f < 0 || f >= Tc) v = 0.f;
         Out[(p + 1) * LDH + n] = (__bf16)v;
-        if (j == 5 && p >= 16 && p < 80 && f < Tc) A.hout[(rb + f) * HK + n] = v;
+        if (j == 5 && p >= 16 && p < 80 && f < Tc) hout[(rb + f) * HK + n] = v;
       }
     }
     __syncthreads();
@@ -579,7 +586,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const __bf16* wrow = A.Wb + (nt * 32 + r32) * 192 + h * 8;
+    const __bf16* wrow = A.Wb[nblk] + (nt * 32 + r32) * 192 + h * 8;
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk) {
       const int tap = kk >> 2, kc = kk & 3;
@@ -588,11 +595,11 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
     }
     const int n = nt * 32 + r32;
-    const float bias = A.bb[n];
+    const float bias = A.bb[nblk][n];
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int f = f0 + mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (f < Tc) A.Bf[(rb + f) * (2 * CI * NLY) + n] = acc[reg] + bias;
+      if (f < Tc) Bfo[(rb + f) * (2 * CI * NLY) + n] = acc[reg] + bias;
     }
   }
 }
@@ -724,15 +731,18 @@ __global__ __launch_bounds__(256) void final_conv_kernel(const float* __restrict
                                                          float sig, const float* noise,
                                                          unsigned long long seed, unsigned stream,
                                                          long long L) {
-  __shared__ float xs[262 * 33];
-  __shared__ float wsh[7 * 32];
+  // rows of 36 floats (144 B): 16-B reads, slot 9*row mod 16 -> conflict-free across lanes
+  __shared__ __attribute__((aligned(16))) float xs[262 * 36];
+  __shared__ __attribute__((aligned(16))) float wsh[7 * 32];
   const int b = blockIdx.y, tid = threadIdx.x;
   const long long t0 = (long long)blockIdx.x * 256;
   if (tid < 224) wsh[tid] = w[tid];
-  for (int i = tid; i < 262 * 32; i += 256) {
-    int rr = i >> 5, c = i & 31;
-    long long t = t0 - 3 + rr;
-    xs[rr * 33 + c] = (t >= 0 && t < L) ? x[((long long)b * L + t) * CI + c] : 0.f;
+  for (int i = tid; i < 262 * 8; i += 256) {
+    const int rr = i >> 3, q = (i & 7) * 4;
+    const long long t = t0 - 3 + rr;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t >= 0 && t < L) v = *reinterpret_cast<const float4*>(x + ((long long)b * L + t) * CI + q);
+    *reinterpret_cast<float4*>(&xs[rr * 36 + q]) = v;
   }
   __syncthreads();
   const long long t = t0 + tid;
@@ -740,9 +750,13 @@ __global__ __launch_bounds__(256) void final_conv_kernel(const float* __restrict
   float e = bias[0];
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
-    const float* xr = xs + (tid + k) * 33;
-#pragma unroll 8
-    for (int c = 0; c < 32; ++c) e = fmaf(wsh[k * 32 + c], xr[c], e);
+    const float* xr = xs + (tid + k) * 36;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(xr + 4 * q);
+      const float4 ww = *reinterpret_cast<const float4*>(&wsh[k * 32 + 4 * q]);
+      e = fmaf(ww.x, v.x, fmaf(ww.y, v.y, fmaf(ww.z, v.z, fmaf(ww.w, v.w, e))));
+    }
   }
   const long long idx = (long long)b * L + t;
   if (eps_out) eps_out[idx] = e;
@@ -787,7 +801,7 @@ __global__ void pack_final_kernel(float* dst, const float* src) {
 struct FdWs {
   size_t steps, e128, e512a, e512, nz;  // step MLP (nvec = S*B)
   size_t a0, d[3], dtmp0, dtmp1, xs;
-  size_t X0, X1, y, h0, ra, rb, Bf, Kf, condT, total;
+  size_t X0, X1, y, h0, ra, rb, Bf, Kf, condT, hall, bfall, total;
 };
 
 FdWs fd_layout(const fd_model* m, int B, int Tc, int S) {
@@ -816,6 +830,9 @@ FdWs fd_layout(const fd_model* m, int B, int Tc, int S) {
   w.ra = take((size_t)B * Tc * HK);
   w.rb = take((size_t)B * Tc * HK);
   w.Bf = take((size_t)B * Tc * 2 * CI * NLY);
+  // bf16 path: kernel-predictor hidden outputs of every (step, block), one batched launch
+  w.hall = take((size_t)S * m->nblocks * B * Tc * HK);
+  w.bfall = take((size_t)S * m->nblocks * B * Tc * 2 * CI * NLY);
   w.Kf = take((size_t)B * Tc * KPERLAYER * 2);   // fp32: one layer; bf16: all 4 layers
   w.condT = take((size_t)B * Tc * CC);
   w.total = off * sizeof(float);
@@ -869,10 +886,30 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
   return PD_OK;
 }
 
+// Kernel-predictor hidden stacks (bf16) for `nsteps` steps x every block in one launch.
+// nz: [nsteps*B][nb*80] (the step-MLP output); results in ws.hall / ws.bfall, z = s*nb + n.
+int fd_kp_hidden_all(const fd_model* m, float* ws, const FdWs& W, const float* condT, const float* nz,
+                     int nsteps, int B, int Tc, hipStream_t st) {
+  const int nb = m->nblocks;
+  KPArgs ka{};
+  ka.condT = condT; ka.nz = nz; ka.nz_step = B * nb * CC; ka.nz_ld = nb * CC; ka.nb = nb; ka.B = B;
+  for (int n = 0; n < nb; ++n) {
+    const fd_model::Block& K = m->blk[n];
+    ka.Win[n] = lookup_bf16(K.kin_w); ka.bin[n] = K.kin_b;
+    for (int j = 0; j < 6; ++j) { ka.Wr[n][j] = lookup_bf16(K.kres_w[j]); ka.br[n][j] = K.kres_b[j]; }
+    ka.Wb[n] = lookup_bf16(K.kb_w); ka.bb[n] = K.kb_b;
+  }
+  ka.hout = ws + W.hall; ka.Bf = ws + W.bfall; ka.Tc = Tc;
+  ProfScope ps("fd_kp_hidden", st);
+  hipLaunchKernelGGL(kp_hidden_bf16_kernel, dim3(cdiv(Tc, 64), B, nsteps * nb), dim3(256), 0, st, ka);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
 // One eps-network evaluation.  xa: audio [B][L]; condT: [B][Tc][80];
 // nz: this step's per-block fc_t(emb) rows ([B][nblocks*80]).  Leaves the LVC output in *xout.
 int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const float* condT,
-           const float* nz, int B, int Tc, float** xout, hipStream_t st) {
+           const float* nz, int step, int B, int Tc, float** xout, hipStream_t st) {
   const int nb = m->nblocks;
   const long long L = (long long)Tc * m->hops[nb - 1];
   float* a0 = ws + W.a0;
@@ -907,17 +944,12 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
     // --- kernel predictor on c + fc_t(emb)   (modules.py:202-204, 320-343)
     const bool bf = m->pool_bf != nullptr;
     const float* hk = nullptr;   // final h  [B][Tc][64]
+    float* Bfp = ws + W.Bf;      // LVC biases of this block [B][Tc][256]
     if (bf) {
-      KPArgs ka{};
-      ka.condT = condT; ka.nz = nz + n * CC; ka.nz_ld = nb * CC;
-      ka.Win = lookup_bf16(K.kin_w); ka.bin = K.kin_b;
-      for (int j = 0; j < 6; ++j) { ka.Wr[j] = lookup_bf16(K.kres_w[j]); ka.br[j] = K.kres_b[j]; }
-      ka.Wb = lookup_bf16(K.kb_w); ka.bb = K.kb_b;
-      ka.hout = ws + W.h0; ka.Bf = ws + W.Bf; ka.Tc = Tc;
-      ProfScope ps("fd_kp_hidden", st);
-      hipLaunchKernelGGL(kp_hidden_bf16_kernel, dim3(cdiv(Tc, 64), B), dim3(256), 0, st, ka);
-      PD_LAUNCH_CHECK();
-      hk = ws + W.h0;
+      // computed for every step and block up front (fd_kp_hidden_all)
+      const size_t z = (size_t)step * nb + n;
+      hk = ws + W.hall + z * B * Tc * HK;
+      Bfp = ws + W.bfall + z * B * Tc * 2 * CI * NLY;
     } else {
     {
       GemmArgs a = make_gemm(B, Tc, HK, K.kin_w, 5 * 96, K.kin_b, ws + W.h0, bsH, HK);
@@ -976,7 +1008,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         la.Wc[i] = lookup_bf16(K.cv_w[i]);
         la.bc[i] = K.cv_b[i];
       }
-      la.xin = xn; la.xout = ws + W.y; la.a = ad; la.Bf = ws + W.Bf; la.Tc = Tc; la.hop = hop;
+      la.xin = xn; la.xout = ws + W.y; la.a = ad; la.Bf = Bfp; la.Tc = Tc; la.hop = hop;
       {
         ProfScope ps("fd_lvc_block", st);
         if (m->lvc_ts == 256)
@@ -1015,10 +1047,10 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         const __bf16* Wc = lookup_bf16(K.cv_w[i]);
         if (hop % 128 == 0)
           hipLaunchKernelGGL(lvc_fused_bf16_kernel<128>, dim3(B * Tc * (hop / 128)), dim3(256), 0, st, xn, ad, Kb,
-                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
+                             KPERLAYER, Bfp + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
         else
           hipLaunchKernelGGL(lvc_fused_bf16_kernel<64>, dim3(B * Tc * (hop / 64)), dim3(128), 0, st, xn, ad, Kb,
-                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
+                             KPERLAYER, Bfp + i * 2 * CI, 2 * CI * NLY, Wc, K.cv_b[i], Tc, hop, dil);
       } else {
         {  // y = lrelu(conv_dil3^i(lrelu(x + a)) + b)
           GemmArgs a = make_gemm(B, (int)Tout, CI, K.cv_w[i], 96, K.cv_b[i], ws + W.y, Tout * CI, CI);
@@ -1034,11 +1066,11 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         ProfScope ps("fd_lvc", st);
         if (bf)
           hipLaunchKernelGGL(lvc_kernel<__bf16>, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y,
-                             reinterpret_cast<const __bf16*>(ws + W.Kf), KPERLAYER, ws + W.Bf + i * 2 * CI,
+                             reinterpret_cast<const __bf16*>(ws + W.Kf), KPERLAYER, Bfp + i * 2 * CI,
                              2 * CI * NLY, Tc, hop);
         else
           hipLaunchKernelGGL(lvc_kernel<float>, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y, ws + W.Kf,
-                             KPERLAYER, ws + W.Bf + i * 2 * CI, 2 * CI * NLY, Tc, hop);
+                             KPERLAYER, Bfp + i * 2 * CI, 2 * CI * NLY, Tc, hop);
       }
       PD_LAUNCH_CHECK();
     }
@@ -1219,7 +1251,8 @@ int fd_forward(const fd_model* m, const float* audio, const float* cond, const f
   PD_TRY(fd_step_mlp(m, ws, W, B, st));
   PD_TRY(transpose_ct_to_tc(cond, ws + W.condT, B, CC, Tc, st));
   float* x = nullptr;
-  PD_TRY(fd_net(m, ws, W, audio, ws + W.condT, ws + W.nz, B, Tc, &x, st));
+  if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, ws + W.condT, ws + W.nz, 1, B, Tc, st));
+  PD_TRY(fd_net(m, ws, W, audio, ws + W.condT, ws + W.nz, 0, B, Tc, &x, st));
   hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w, m->final_b,
                      eps, (float*)nullptr, 0.f, 0.f, 0.f, (const float*)nullptr, 0ull, 0u, L);
   PD_LAUNCH_CHECK();
@@ -1247,10 +1280,11 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
   for (int j = 0; j < N; ++j) sv[j] = steps[N - 1 - j];
   PD_TRY(fill_steps(ws + W.steps, sv.data(), N, B, st));
   PD_TRY(fd_step_mlp(m, ws, W, N * B, st));
+  if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, mel, ws + W.nz, N, B, Tc, st));
   for (int j = 0; j < N; ++j) {
     const int n = N - 1 - j;
     float* x = nullptr;
-    PD_TRY(fd_net(m, ws, W, wav, mel, ws + W.nz + (size_t)j * B * m->nblocks * CC, B, Tc, &x, st));
+    PD_TRY(fd_net(m, ws, W, wav, mel, ws + W.nz + (size_t)j * B * m->nblocks * CC, j, B, Tc, &x, st));
     // x = (x - beta/sqrt(1-alpha^2) eps) / sqrt(1-beta) + [n>0] sigma z   (util.py:222-226)
     const float ce = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
     const float den = sqrtf(1.f - beta[n]);
