@@ -49,6 +49,7 @@ def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
         "wn_outproj_posterior": 2 * F * M * C,
         "fd_first_conv": 2 * F * 256 * 32 * 7,
         "fd_dblock": dblock,
+        "fd_dblock_fused": dblock * 3.0,                    # all 3 convs + residual of one DBlock
         "fd_kp_in": 2 * F * 64 * 80 * 5,
         "fd_kp_res": 2 * F * 64 * 64 * 3,
         "fd_kp_bias": 2 * F * 256 * 64 * 3,
@@ -84,6 +85,8 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         "wn_skiphead": F * 2 * C * 4 + C * C * wb,
         "wn_outproj_posterior": F * (C + 3 * M) * 4 + M * C * wb,
         "fd_first_conv": F * 256 * (1 + 32) * 4,
+        # fused DBlock: strided input rows (32 ch) read once + output written once
+        "fd_dblock_fused": sum(r * 2 * per_row_io for r in (F * 64, F * 8, F)) / 3.0,
         "fd_kp_kernel": F * (64 * 4 + 6144 * wb) + 6144 * 192 * wb,
         "fd_kp_hidden": F * (80 + 64 + 256) * 4 + (64 * 480 + 6 * 64 * 192 + 256 * 192) * wb,
         "fd_lvc_fused": sum(lvc_f) / 2.0,

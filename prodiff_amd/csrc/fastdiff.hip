@@ -466,6 +466,96 @@ __global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const Lvc
   }
 }
 
+// ------------------------------------------------------------------ DiffusionDBlock (bf16)
+// modules.py:131-138 in one launch:
+//   xs = x[f i];  h1 = lrelu(conv_d1(lrelu(xs)));  h2 = lrelu(conv_d2(h1));
+//   out = conv_d4(h2) + W_r xs + (b3 + b_r)        (conv.2 and residual_dense share one K=128 GEMM)
+// Block = 128 output rows of one utterance; local row p <-> i = i0 - 7 + p (halo 1+2+4).
+// Every intermediate is zeroed outside [0, Lout): each reference conv's zero padding.
+constexpr int DB_TS = 128, DB_ROWS = 168, DB_LD = 40;
+__global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                          const __bf16* __restrict__ W0, const float* __restrict__ b0,
+                                                          const __bf16* __restrict__ W1, const float* __restrict__ b1,
+                                                          const __bf16* __restrict__ W2, const float* __restrict__ b2,
+                                                          int Lout, int f) {
+  __shared__ __attribute__((aligned(16))) __bf16 U0[DB_ROWS * DB_LD];   // lrelu(x[f i])
+  __shared__ __attribute__((aligned(16))) __bf16 R0[DB_ROWS * DB_LD];   // x[f i] (residual input)
+  __shared__ __attribute__((aligned(16))) __bf16 H1[DB_ROWS * DB_LD];
+  __shared__ __attribute__((aligned(16))) __bf16 H2[DB_ROWS * DB_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int b = blockIdx.y, i0 = blockIdx.x * DB_TS, ib = i0 - 7;
+  const long long Lin = (long long)Lout * f;
+  const float* src = in + (long long)b * Lin * CI;
+  for (int i = tid; i < DB_ROWS * 8; i += 256) {
+    const int p = i >> 3, q = (i & 7) * 4, ii = ib + p;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < DB_TS + 14 && ii >= 0 && ii < Lout) v = *reinterpret_cast<const float4*>(src + (long long)ii * f * CI + q);
+    *reinterpret_cast<bf16x4*>(&R0[p * DB_LD + q]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    v.x = v.x >= 0.f ? v.x : 0.2f * v.x; v.y = v.y >= 0.f ? v.y : 0.2f * v.y;
+    v.z = v.z >= 0.f ? v.z : 0.2f * v.z; v.w = v.w >= 0.f ? v.w : 0.2f * v.w;
+    *reinterpret_cast<bf16x4*>(&U0[p * DB_LD + q]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+  }
+  __syncthreads();
+  // one dilated 32->32 conv stage over 5 row tiles starting at local row `first`
+  auto stage = [&](const __bf16* In, __bf16* Out, const __bf16* Wt, const float* bias, int first, int dil) {
+    bf16x8 wf[6];
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const bf16x8*>(Wt + r32 * 96 + kk * 16 + h * 8);
+    const float bv = bias[r32];
+    for (int mt = wave; mt < 5; mt += 4) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) {
+        const int tap = kk >> 1, ci0 = (kk & 1) * 16;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(&In[(first + mt * 32 + r32 + (tap - 1) * dil) * DB_LD + ci0 + h * 8]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wf[kk], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int p = first + mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, ii = ib + p;
+        float v = acc[reg] + bv;
+        v = v >= 0.f ? v : 0.2f * v;                        // the next conv's input activation
+        if (ii < 0 || ii >= Lout || p >= DB_ROWS) v = 0.f;
+        if (p < DB_ROWS) Out[p * DB_LD + r32] = (__bf16)v;
+      }
+    }
+  };
+  stage(U0, H1, W0, b0, 1, 1);    // h1 on p in [1, 161)
+  __syncthreads();
+  stage(H1, H2, W1, b1, 3, 2);    // h2 on p in [3, 163)
+  __syncthreads();
+  // out on p in [7, 135): conv_d4(h2) ++ residual_dense(x), K = 96 + 32
+  {
+    bf16x8 wf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wf[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
+    const float bv = b2[r32];
+    const int mt = wave;   // 4 tiles, one per wave
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      bf16x8 af;
+      if (kk < 6) {
+        const int tap = kk >> 1, ci0 = (kk & 1) * 16;
+        af = *reinterpret_cast<const bf16x8*>(&H2[(7 + mt * 32 + r32 + (tap - 1) * 4) * DB_LD + ci0 + h * 8]);
+      } else {
+        af = *reinterpret_cast<const bf16x8*>(&R0[(7 + mt * 32 + r32) * DB_LD + (kk - 6) * 16 + h * 8]);
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wf[kk], acc, 0, 0, 0);
+    }
+    float* dst = out + (long long)b * Lout * CI;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int ii = i0 + mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (ii < Lout) dst[(long long)ii * CI + r32] = acc[reg] + bv;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ kernel predictor (bf16)
 // Batched over grid.z = step * nb + block: the hidden stack depends only on the mel
 // and the step embedding, so a sampler runs it for every step and block in ONE launch.
@@ -855,6 +945,13 @@ int fd_step_mlp(const fd_model* m, float* ws, const FdWs& W, int nv, hipStream_t
 int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, float* t1, int B, int Tout,
            int f, hipStream_t st) {
   const long long bsi = (long long)Tout * f * CI, bso = (long long)Tout * CI;
+  if (const __bf16* w0 = lookup_bf16(D.c0_w)) {   // bf16: one fused launch, intermediates in LDS
+    ProfScope ps("fd_dblock_fused", st);
+    hipLaunchKernelGGL(dblock_bf16_kernel, dim3(cdiv(Tout, DB_TS), B), dim3(256), 0, st, in, out, w0, D.c0_b,
+                       lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f);
+    PD_LAUNCH_CHECK();
+    return PD_OK;
+  }
   {
     GemmArgs a = make_gemm(B, Tout, CI, D.c0_w, 96, D.c0_b, t0, bso, CI);
     for (int tap = 0; tap < 3; ++tap) {
