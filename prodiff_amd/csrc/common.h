@@ -81,6 +81,14 @@ __device__ __forceinline__ float tanhf_(float v) {
   return 1.f - 2.f * __builtin_amdgcn_rcpf(exp_fast(2.f * v) + 1.f);
 }
 
+// sigmoid(g) * tanh(f) with 2 exp + 1 rcp:  (E_f - 1) / ((E_f + 1)(1 + E_g)),
+// E_f = e^{2f} (f clamped to +-15, where tanh is 1 in fp32), E_g = e^{-g} (inf -> 0).
+__device__ __forceinline__ float gate_fast(float g, float f) {
+  const float ef = __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(f, -15.f, 15.f) * 2.8853900817779268f);
+  const float eg = __builtin_amdgcn_exp2f(g * -1.4426950408889634f);
+  return (ef - 1.f) * __builtin_amdgcn_rcpf((ef + 1.f) * (1.f + eg));
+}
+
 // ---------------------------------------------------------------------------
 // Counter-based normal/uniform draws (Philox4x32-10), used when the caller does
 // not hand in explicit noise.  key = seed, counter = (index, stream id).

@@ -24,18 +24,25 @@ constexpr int NLY = 4;   // lvc layers per block
 constexpr int KPERLAYER = 2 * CI * CI * 3;   // 6144 kernel values per frame per layer
 constexpr int EMB_IN = 128, EMB_MID = 512, EMB_OUT = 512;
 
-// Frame-major LVC kernel layout is MFMA-fragment order: value (o, q) of a frame's
-// 64x96 kernel (o = output channel, q = tap*32 + ci) lives at
-//   ((o/32 * 6 + q/16) * 64 + ((q%16)/8) * 32 + o%32) * 8 + q%8,
-// i.e. [gate|filter tile][k-step][lane][8], so each B-fragment load of the LVC
-// MFMA is one contiguous 1 KB per wave.
+// Frame-major LVC kernel layout is MFMA-fragment order.  Within each tap the 32 input
+// channels are stored in the permuted order pos = lvc_pos(ci): position 16h + reg holds
+// channel (reg&3) + 8(reg>>2) + 4h, which is exactly the channel set a lane of a 32x32
+// MFMA result holds (rows (reg&3) + 8(reg>>2) + 4h).  So an LVC/pre-conv result computed
+// with channels as rows is the next GEMM's k-operand in place (lvc_block_bf16_kernel).
+// Value (o, q = tap*32 + ci) of a frame's 64x96 kernel (o = output channel) lives at
+//   ((o/32 * 6 + k/16) * 64 + ((k%16)/8) * 32 + o%32) * 8 + k%8,  k = tap*32 + lvc_pos(ci),
+// i.e. [gate|filter tile][k-step][lane][8]: each MFMA fragment load is 1 KB per wave.
+__host__ __device__ inline int lvc_pos(int ci) { return (((ci >> 2) & 1) << 4) | ((ci >> 3) << 2) | (ci & 3); }
+__host__ __device__ inline int lvc_chan(int p) { return (p & 3) | (((p & 15) >> 2) << 3) | ((p >> 4) << 2); }
 __host__ __device__ inline int kf_packed(int o, int q) {
-  return (((o >> 5) * 6 + (q >> 4)) * 64 + ((q & 15) >> 3) * 32 + (o & 31)) * 8 + (q & 7);
+  const int k = (q & ~31) | lvc_pos(q & 31);
+  return (((o >> 5) * 6 + (k >> 4)) * 64 + ((k & 15) >> 3) * 32 + (o & 31)) * 8 + (k & 7);
 }
 __host__ __device__ inline void kf_unpack(int p, int& o, int& q) {
   const int j = p & 7, l = (p >> 3) & 63, kkn = p >> 9;
   o = (kkn / 6) * 32 + (l & 31);
-  q = (kkn % 6) * 16 + (l >> 5) * 8 + j;
+  const int k = (kkn % 6) * 16 + (l >> 5) * 8 + j;
+  q = (k & ~31) | lvc_chan(k & 31);
 }
 }  // namespace
 
@@ -44,7 +51,7 @@ struct fd_model {
   int ratios[4];
   int hops[4];
   int dtype;
-  int lvc_ts = 0;              // whole-block LVC tile (128/256); 0 = one fused launch per layer (default: faster today)
+  int lvc_ts = 128;            // whole-block LVC tile (128/256); 0 = one fused launch per layer (PRODIFF_LVC_TS)
   float* pool = nullptr;
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
   // step MLP
@@ -254,7 +261,7 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
         float y = acc[reg] + bias;
         y = y >= 0.f ? y : 0.2f * y;
         if (t < 0 || t >= Lh) y = 0.f;        // the LVC zero-pads y at utterance edges
-        Y[r * LD + r32] = (__bf16)y;
+        Y[r * LD + lvc_pos(r32)] = (__bf16)y; // kernel k-order (kf_packed)
       }
     }
   }
@@ -283,7 +290,7 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
     for (int reg = 0; reg < 16; ++reg) {
       const int s = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
       const long long idx = (base + t0 + s) * CI + r32;
-      x[idx] = x[idx] + a[idx] + sigmoidf_(ag[reg] + bg) * tanhf_(afl[reg] + bl);
+      x[idx] = x[idx] + a[idx] + gate_fast(ag[reg] + bg, afl[reg] + bl);
     }
   }
 }
@@ -291,179 +298,244 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
 // ------------------------------------------------------------------ whole LVC block (bf16)
 // All 4 LVC layers of one TimeAware_LVCBlock (modules.py:208-217) in ONE launch:
 //   for l < 4:  x = x + a + gate(LVC_l(lrelu(conv_{3^l}(lrelu(x + a)) + b_l)))
-// Block = 256 output samples of one utterance.  x and a (audio_down) are read once
-// (with the 44-sample halo of the 1/3/9/27-dilated stack) into LDS as fp32 and the
-// state never leaves LDS until the last layer; layer l is evaluated on its own valid
-// range (halo e_l = 42, 38, 28, 0), so each later layer still sees exact inputs.
-// A 32-row LVC tile that straddles a frame boundary is multiplied by both frames'
-// kernels and each row keeps its own frame's result.
+// Block = TS output samples of one utterance on a grid of NG 32-row tiles covering
+// [t0 - 64, t0 + TS + 64).  Tiles are 32-aligned in time and hop % 64 == 0, so every
+// tile lies in ONE frame and multiplies one 64x96 kernel.  The state x and audio_down a
+// stay in registers in the MFMA C layout (wave w owns tiles w and w + NW); LDS only
+// holds the bf16 operands u = lrelu(x + a) and y.  Layer l is valid on rows
+// [64 - e_l, 64 + TS + e_l), e = 42, 38, 28, 0 (the remaining dilation reach), and
+// only the tiles overlapping that range are computed; rows outside it are never
+// read by a valid row, so they may hold anything.
 struct LvcBlockArgs {
   float* xout;              // [B][Lh][32]
   const float* xin;         // [B][Lh][32] upsample output
   const float* a;           // [B][Lh][32] audio_down
-  const __bf16* Kf[NLY];    // [B*Tc][6144] per layer (frame-major)
+  const __bf16* Kf[NLY];    // [B*Tc][6144] per layer (frame-major, fragment order)
   const float* Bf;          // [B*Tc][256]: layer l at +64 l
   const __bf16* Wc[NLY];    // [32][96] pre-conv weights (bf16 mirror)
   const float* bc[NLY];
   int Tc, hop;
+#ifdef LB_TRACE
+  unsigned long long* trace;   // tools/lvc_probe.hip: per-phase s_memtime stamps
+#endif
 };
-constexpr int LB_HALO = 44, LB_LD = 40;
-// TS = output samples per block.  TS=128 with 256 threads keeps LDS at ~78 KB, so two
-// blocks share a CU (one streams its tile in while the other computes).
-template <int TS> struct LbCfg {
-  static constexpr int ROWS = TS + 2 * LB_HALO;
-  static constexpr int UY = (TS + 84 + 2 + 31) / 32 * 32 + 8;    // y/u tile rows (+ tap reach)
-  static constexpr int URows = (UY - 8) + 2 * 3 > (TS + 2 + 31) / 32 * 32 + 54 ? (UY - 8) + 6 + 2
-                                                                               : (TS + 2 + 31) / 32 * 32 + 56;
-  static constexpr int NT = TS == 256 ? 512 : 256;
+#ifdef LB_TRACE
+#define LB_STAMP(i)                                                                       \
+  do {                                                                                    \
+    if (lane == 0 && blockIdx.x % 61 == 0)                                                \
+      P.trace[((blockIdx.y * gridDim.x + blockIdx.x) / 61 * NW + wave) * 16 + (i)] =      \
+          __builtin_readcyclecounter();                                                   \
+  } while (0)
+#else
+#define LB_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+constexpr int LB_LD = 40;
+template <int TS> struct LbGeo {
+  static constexpr int NG = TS / 32 + 4;            // tiles in the grid
+  static constexpr int NW = NG / 2;                 // waves; two tiles each
+  static constexpr int NT = NW * 64;
+  static constexpr int UOFF = 28;                   // U index = row + 28 (pre-conv reach 1 + 27)
+  static constexpr int UROWS = NG * 32 + 2 * UOFF;
+  static constexpr int YROWS = (NG + 1) * 32;       // Y index = row + 1
 };
+
+// Packed-fp32 epilogue helpers (v_pk_fma/mul/add_f32 work on two lanes' values at once).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr float LOG2E = 1.4426950408889634f;
+__device__ __forceinline__ f32x2 lrelu2(f32x2 v) {
+  const f32x2 s = v * 0.2f;
+  return f32x2{fmaxf(v.x, s.x), fmaxf(v.y, s.y)};
+}
+// sigmoid(g) tanh(f) from gs = -log2e (g + b_g), fs = 2 log2e (f + b_f): gate_fast, paired
+__device__ __forceinline__ f32x2 gate2s(f32x2 gs, f32x2 fs) {
+  constexpr float C = 15.f * 2.f * LOG2E;
+  const f32x2 ef = {__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(fs.x, -C, C)),
+                    __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(fs.y, -C, C))};
+  const f32x2 eg = {__builtin_amdgcn_exp2f(gs.x), __builtin_amdgcn_exp2f(gs.y)};
+  const f32x2 den = (ef + 1.f) * (eg + 1.f);
+  return (ef - 1.f) * f32x2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+}
 
 template <int TS>
-__global__ __launch_bounds__(LbCfg<TS>::NT) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
-  constexpr int LB_TS = TS, LB_ROWS = LbCfg<TS>::ROWS, NT = LbCfg<TS>::NT, NW = NT / 64;
-  constexpr int LB_UY = LbCfg<TS>::URows;
-  __shared__ __attribute__((aligned(16))) float X[LB_ROWS * CI];
-  __shared__ __attribute__((aligned(16))) __bf16 Aa[LB_ROWS * CI];      // audio_down, bf16
-  __shared__ __attribute__((aligned(16))) __bf16 U[LB_UY * LB_LD];
-  __shared__ __attribute__((aligned(16))) __bf16 Yb[LB_UY * LB_LD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+__global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
+  using G = LbGeo<TS>;
+  constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF;
+  // Rows = time, 40 bf16 per row; position p of a row holds channel lvc_chan(p).
+  __shared__ __attribute__((aligned(16))) __bf16 U[G::UROWS * LB_LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Y[G::YROWS * LB_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, Tc = P.Tc, hop = P.hop;
   const int Lh = Tc * hop;                           // utterance-local times fit in 32 bits
-  const int t0 = blockIdx.x * LB_TS;
-  const int tb = t0 - LB_HALO;                       // time of local row 0
+  const int t0 = blockIdx.x * TS, tg = t0 - 64;      // time of grid row 0
   const long long base = (long long)b * Lh;
-
-  for (int i = tid; i < LB_ROWS * 8; i += NT) {
-    const int r = i >> 3, q = (i & 7) * 4;
-    const int t = tb + r;
-    float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
-    if (t >= 0 && t < Lh) {
-      xv = *reinterpret_cast<const float4*>(P.xin + (base + t) * CI + q);
-      av = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + q);
+  LB_STAMP(0);
+  {
+    const bf16x8 z = {};
+    for (int i = tid; i < G::UROWS * LB_LD / 8; i += G::NT) reinterpret_cast<bf16x8*>(U)[i] = z;
+    for (int i = tid; i < G::YROWS * LB_LD / 8; i += G::NT) reinterpret_cast<bf16x8*>(Y)[i] = z;
+  }
+  // Transposed C layout: lane (n, h) of tile k holds time tg + 32k + n, channels
+  // (reg&3) + 8(reg>>2) + 4h; pair p = regs (2p, 2p+1).  Four float4 loads per tensor
+  // (channels 8i + 4h .. +3).  Rows [20, TS + 108) = times [t0 - 44, t0 + TS + 44).
+  f32x2 xr[2][8], ar[2][8];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = wave + j * NW, row = k * 32 + n, t = tg + row;
+    const bool ok = row >= 20 && row < TS + 108 && t >= 0 && t < Lh;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
+#ifdef LB_EXP_NOXA
+      if (ok) { xv = make_float4(0.1f * i, 0.2f, 0.3f, (float)t * 1e-6f); av = xv; }
+#else
+      if (ok) {
+        xv = *reinterpret_cast<const float4*>(P.xin + (base + t) * CI + 8 * i + 4 * h);
+        av = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + 8 * i + 4 * h);
+      }
+#endif
+      xr[j][2 * i] = f32x2{xv.x, xv.y}; xr[j][2 * i + 1] = f32x2{xv.z, xv.w};
+      ar[j][2 * i] = f32x2{av.x, av.y}; ar[j][2 * i + 1] = f32x2{av.z, av.w};
     }
-    *reinterpret_cast<float4*>(&X[r * CI + q]) = xv;
-    *reinterpret_cast<bf16x4*>(&Aa[r * CI + q]) = bf16x4{(__bf16)av.x, (__bf16)av.y, (__bf16)av.z, (__bf16)av.w};
   }
   __syncthreads();
-
-#pragma unroll 1
+  LB_STAMP(1);
+#pragma unroll
   for (int l = 0; l < NLY; ++l) {
-    const int d = (l == 0) ? 1 : (l == 1) ? 3 : (l == 2) ? 9 : 27;
-    const int e = (l == 0) ? 42 : (l == 1) ? 38 : (l == 2) ? 28 : 0;   // halo still needed after layer l
-    const int lo = LB_HALO - e, hi = LB_HALO + LB_TS + e;              // output rows [lo, hi)
-    const int nyt = (hi - lo + 2 + 31) / 32;                      // y rows lo-1 .. hi
-    const int ulo = lo - 1 - d;                                   // local row of U[0]
-    // (1) u = lrelu(x + a), zero outside the utterance
-    const int nu = nyt * 32 + 2 * d;
-    for (int i = tid; i < nu * 8; i += NT) {
-      const int j = i >> 3, q = (i & 7) * 4, r = ulo + j;
-      const int t = tb + r;
-      bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-      if (r >= 0 && r < LB_ROWS && t >= 0 && t < Lh) {
-        const float4 xv = *reinterpret_cast<const float4*>(&X[r * CI + q]);
-        const bf16x4 ab = *reinterpret_cast<const bf16x4*>(&Aa[r * CI + q]);
-        const float4 av = make_float4((float)ab[0], (float)ab[1], (float)ab[2], (float)ab[3]);
-        float u0 = xv.x + av.x, u1 = xv.y + av.y, u2 = xv.z + av.z, u3 = xv.w + av.w;
-        u0 = u0 >= 0.f ? u0 : 0.2f * u0; u1 = u1 >= 0.f ? u1 : 0.2f * u1;
-        u2 = u2 >= 0.f ? u2 : 0.2f * u2; u3 = u3 >= 0.f ? u3 : 0.2f * u3;
-        v = bf16x4{(__bf16)u0, (__bf16)u1, (__bf16)u2, (__bf16)u3};
+    const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
+    const int e = l == 0 ? 42 : l == 1 ? 38 : l == 2 ? 28 : 0;
+    const int kf = (64 - e) / 32, kl = (64 + TS + e - 1) / 32;   // LVC tiles of this layer
+    const int kpl = kl + 1 < NG - 1 ? kl + 1 : NG - 1;           // last pre-conv tile
+    // (1) u = lrelu(x + a) of the owned tiles the pre-conv reads: 2 x 16 B per lane
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = wave + j * NW;
+      if (k >= kf - 1 && k <= kl + 2) {
+        bf16x8 u0, u1;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const f32x2 v0 = lrelu2(xr[j][p] + ar[j][p]), v1 = lrelu2(xr[j][4 + p] + ar[j][4 + p]);
+          u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
+          u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
+        }
+        __bf16* dst = &U[(k * 32 + n + UOFF) * LB_LD + 16 * h];
+        *reinterpret_cast<bf16x8*>(dst) = u0;
+        *reinterpret_cast<bf16x8*>(dst + 8) = u1;
       }
-      *reinterpret_cast<bf16x4*>(&U[j * LB_LD + q]) = v;
     }
     __syncthreads();
-    // (2) y = lrelu(W_c . [u(r-d); u(r); u(r+d)] + b), zero outside the utterance
+    LB_STAMP(2 + 3 * l);
+    // (2) y^T = lrelu(W_c . [u(t-d); u(t); u(t+d)]^T + b): A = weights (rows = out channel,
+    //     k in kernel order), B = u rows.  Pre-conv tile kp -> Y index [32kp, 32kp+32) = rows - 1.
     {
       bf16x8 wf[6];
 #pragma unroll
-      for (int kk = 0; kk < 6; ++kk)
-        wf[kk] = *reinterpret_cast<const bf16x8*>(P.Wc[l] + r32 * 96 + kk * 16 + h * 8);
-      const float bias = P.bc[l][r32];
-      for (int mt = wave; mt < nyt; mt += NW) {
+      for (int kk = 0; kk < 6; ++kk) {
+        const __bf16* w = P.Wc[l] + n * 96 + (kk >> 1) * 32 + 16 * h + 4 * (kk & 1);
+        const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(w), w1 = *reinterpret_cast<const bf16x4*>(w + 8);
+        wf[kk] = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+      }
+      f32x2 bias[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 bv = *reinterpret_cast<const float4*>(P.bc[l] + 8 * i + 4 * h);
+        bias[2 * i] = f32x2{bv.x, bv.y}; bias[2 * i + 1] = f32x2{bv.z, bv.w};
+      }
+      for (int kp = kf + wave; kp <= kpl; kp += NW) {
         f32x16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
         for (int kk = 0; kk < 6; ++kk) {
-          const int tap = kk >> 1, ci0 = (kk & 1) * 16;
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(&U[(mt * 32 + r32 + tap * d) * LB_LD + ci0 + h * 8]);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wf[kk], acc, 0, 0, 0);
+          const int tap = kk >> 1;
+          const bf16x8 bu = *reinterpret_cast<const bf16x8*>(
+              &U[(kp * 32 + n + UOFF - 1 + (tap - 1) * d) * LB_LD + 16 * (kk & 1) + 8 * h]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc, 0, 0, 0);
         }
+        f32x2 v[8];
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int yj = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-          const int t = tb + lo - 1 + yj;
-          float y = acc[reg] + bias;
-          y = y >= 0.f ? y : 0.2f * y;
-          if (t < 0 || t >= Lh) y = 0.f;
-          Yb[yj * LB_LD + r32] = (__bf16)y;
+        for (int p = 0; p < 8; ++p) v[p] = lrelu2(f32x2{acc[2 * p], acc[2 * p + 1]} + bias[p]);
+        const int tt = tg + kp * 32 - 1;                  // the tile's first time (wave-uniform)
+        if (tt < 0 || tt + 31 >= Lh) {                    // utterance-edge tile: zero-pad
+          const int t = tt + n;
+          const float m = (t >= 0 && t < Lh) ? 1.f : 0.f;
+#pragma unroll
+          for (int p = 0; p < 8; ++p) v[p] = v[p] * m;
         }
+        bf16x8 y0, y1;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          y0[2 * p] = (__bf16)v[p].x; y0[2 * p + 1] = (__bf16)v[p].y;
+          y1[2 * p] = (__bf16)v[4 + p].x; y1[2 * p + 1] = (__bf16)v[4 + p].y;
+        }
+        __bf16* dst = &Y[(kp * 32 + n) * LB_LD + 16 * h];
+        *reinterpret_cast<bf16x8*>(dst) = y0;
+        *reinterpret_cast<bf16x8*>(dst + 8) = y1;
       }
     }
     __syncthreads();
-    // (3) o = Bf + K_frame . [y(t-1); y(t); y(t+1)] ; x += a + sigmoid(o_g) tanh(o_f)
-    {
-      const int nlt = (hi - lo + 31) / 32;
-      for (int mt = wave; mt < nlt; mt += NW) {
-        // utterance-local times fit in 32 bits; no 64-bit division anywhere per element
-        const int ts = (int)(tb + lo + mt * 32);           // time of the tile's first row
-        const int tlast = ts + 31;
-        const int Lhi = Lh;
-        int fa = (ts < 0 ? 0 : ts) / hop, fb = (tlast >= Lhi ? Lhi - 1 : tlast) / hop;
-        if (fa > Tc - 1) fa = Tc - 1;
-        if (fb < fa) fb = fa;
-        bf16x8 yf[6];
+    LB_STAMP(3 + 3 * l);
+    // (3) o^T = K_frame . [y(t-1); y(t); y(t+1)]^T + Bf;  x += a + sigmoid(o_g) tanh(o_f)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = wave + j * NW, ts = tg + k * 32;
+      if (k >= kf && k <= kl && ts >= 0 && ts < Lh) {
+#ifdef LB_EXP_K0
+        const int frame = 0 * (ts / hop) + (b & 0);   // probe ablation: cache-resident kernels
+#else
+        const int frame = ts / hop;
+#endif
+        const __bf16* kq = P.Kf[l] + ((long long)b * Tc + frame) * KPERLAYER;
+        const float* bq = P.Bf + ((long long)b * Tc + frame) * (2 * CI * NLY) + l * 2 * CI;
+        f32x16 g, f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { g[r] = 0.f; f[r] = 0.f; }
 #pragma unroll
         for (int kk = 0; kk < 6; ++kk) {
-          const int tap = kk >> 1, ci0 = (kk & 1) * 16;
-          yf[kk] = *reinterpret_cast<const bf16x8*>(&Yb[(mt * 32 + r32 + tap) * LB_LD + ci0 + h * 8]);
+          const int tap = kk >> 1;
+          const bf16x8 yb = *reinterpret_cast<const bf16x8*>(&Y[(k * 32 + n + tap) * LB_LD + 16 * (kk & 1) + 8 * h]);
+          const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+          const bf16x8 kt = *reinterpret_cast<const bf16x8*>(kq + ((6 + kk) * 64 + lane) * 8);
+          g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kg, yb, g, 0, 0, 0);
+          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, yb, f, 0, 0, 0);
         }
-        f32x16 g0, f0, g1, f1;
+        const f32x2 cg = {-LOG2E, -LOG2E}, cf = {2.f * LOG2E, 2.f * LOG2E};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { g0[r] = 0.f; f0[r] = 0.f; g1[r] = 0.f; f1[r] = 0.f; }
-        const __bf16* ka = P.Kf[l] + ((long long)b * Tc + fa) * KPERLAYER;
-#pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
-          const bf16x8 kg = *reinterpret_cast<const bf16x8*>(ka + (kk * 64 + lane) * 8);
-          const bf16x8 kl = *reinterpret_cast<const bf16x8*>(ka + ((6 + kk) * 64 + lane) * 8);
-          g0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kg, g0, 0, 0, 0);
-          f0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kl, f0, 0, 0, 0);
-        }
-        if (fb != fa) {
-          const __bf16* kb2 = P.Kf[l] + ((long long)b * Tc + fb) * KPERLAYER;
-#pragma unroll
-          for (int kk = 0; kk < 6; ++kk) {
-            const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kb2 + (kk * 64 + lane) * 8);
-            const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kb2 + ((6 + kk) * 64 + lane) * 8);
-            g1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kg, g1, 0, 0, 0);
-            f1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yf[kk], kl, f1, 0, 0, 0);
-          }
-        }
-        const float* bfa = P.Bf + ((long long)b * Tc + fa) * (2 * CI * NLY) + l * 2 * CI;
-        const float* bfb = P.Bf + ((long long)b * Tc + fb) * (2 * CI * NLY) + l * 2 * CI;
-        const float bga = bfa[r32], bla = bfa[32 + r32], bgb = bfb[r32], blb = bfb[32 + r32];
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int rr = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-          const int row = lo + mt * 32 + rr;
-          const int t = ts + rr;
-          if (row < hi && t >= 0 && t < Lhi) {
-            const bool second = t >= (fa + 1) * hop;        // row belongs to frame fb
-            const float og = second ? g1[reg] + bgb : g0[reg] + bga;
-            const float of = second ? f1[reg] + blb : f0[reg] + bla;
-            X[row * CI + r32] += (float)Aa[row * CI + r32] + sigmoidf_(og) * tanhf_(of);
-          }
+        for (int i = 0; i < 4; ++i) {
+          const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
+          const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
+          const f32x2 bg0 = f32x2{bg.x, bg.y} * cg, bg1 = f32x2{bg.z, bg.w} * cg;
+          const f32x2 bl0 = f32x2{bl.x, bl.y} * cf, bl1 = f32x2{bl.z, bl.w} * cf;
+#ifdef LB_EXP_NOGATE
+          const f32x2 o0 = f32x2{g[4 * i], g[4 * i + 1]} + f32x2{f[4 * i], f[4 * i + 1]} + bg0 + bl0;
+          const f32x2 o1 = f32x2{g[4 * i + 2], g[4 * i + 3]} + f32x2{f[4 * i + 2], f[4 * i + 3]} + bg1 + bl1;
+#else
+          const f32x2 o0 = gate2s(__builtin_elementwise_fma(f32x2{g[4 * i], g[4 * i + 1]}, cg, bg0),
+                                  __builtin_elementwise_fma(f32x2{f[4 * i], f[4 * i + 1]}, cf, bl0));
+          const f32x2 o1 = gate2s(__builtin_elementwise_fma(f32x2{g[4 * i + 2], g[4 * i + 3]}, cg, bg1),
+                                  __builtin_elementwise_fma(f32x2{f[4 * i + 2], f[4 * i + 3]}, cf, bl1));
+#endif
+          xr[j][2 * i] += ar[j][2 * i] + o0;
+          xr[j][2 * i + 1] += ar[j][2 * i + 1] + o1;
         }
       }
     }
-    __syncthreads();
+    if (l < NLY - 1) LB_STAMP(4 + 3 * l);
   }
-  for (int i = tid; i < LB_TS * 8; i += NT) {
-    const int r = i >> 3, q = (i & 7) * 4;
-    const int t = t0 + r;
-    if (t < Lh)
-      *reinterpret_cast<float4*>(P.xout + (base + t) * CI + q) =
-          *reinterpret_cast<const float4*>(&X[(LB_HALO + r) * CI + q]);
+  LB_STAMP(14);
+  // centre tiles [2, 2 + TS/32) -> x out
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = wave + j * NW, t = tg + k * 32 + n;
+    if (k >= 2 && k < 2 + TS / 32 && t < Lh) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<float4*>(P.xout + (base + t) * CI + 8 * i + 4 * h) =
+            make_float4(xr[j][2 * i].x, xr[j][2 * i].y, xr[j][2 * i + 1].x, xr[j][2 * i + 1].y);
+    }
   }
+  LB_STAMP(15);
 }
 
 // ------------------------------------------------------------------ DiffusionDBlock (bf16)
@@ -1109,9 +1181,9 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       {
         ProfScope ps("fd_lvc_block", st);
         if (m->lvc_ts == 256)
-          hipLaunchKernelGGL(lvc_block_bf16_kernel<256>, dim3(cdiv(Tout, 256), B), dim3(512), 0, st, la);
+          hipLaunchKernelGGL(lvc_block_bf16_kernel<256>, dim3(cdiv(Tout, 256), B), dim3(LbGeo<256>::NT), 0, st, la);
         else
-          hipLaunchKernelGGL(lvc_block_bf16_kernel<128>, dim3(cdiv(Tout, 128), B), dim3(256), 0, st, la);
+          hipLaunchKernelGGL(lvc_block_bf16_kernel<128>, dim3(cdiv(Tout, 128), B), dim3(LbGeo<128>::NT), 0, st, la);
         PD_LAUNCH_CHECK();
       }
       x = ws + W.y;

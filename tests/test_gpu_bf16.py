@@ -95,3 +95,20 @@ def test_fastdiff_sample_bf16(fd16):
                                         torch.from_numpy(s["fd_n4_beta"]), condition=tt(d["c"]),
                                         x_T=tt(d["x_T"]), noise=tt(d["noise"])).cpu().numpy()
     assert_bf16_close(wav, d["wav"])
+
+
+@pytest.mark.parametrize("ts", [0, 128, 256])
+@pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
+def test_fastdiff_lvc_block_bf16(monkeypatch, ts, B, Tc):
+    """LVC modes (PRODIFF_LVC_TS: 0 = one fused launch per layer, 128/256 = whole block) against the
+    oracle, including utterances shorter than one block and the grid/halo edges."""
+    monkeypatch.setenv("PRODIFF_LVC_TS", str(ts))
+    p = G.fastdiff_params(31)
+    m = FastDiff()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+    m = m.to(DEV).set_compute_dtype("bf16")
+    audio = synth.synth_inputs(7 * B + Tc, (B, 1, Tc * 256))
+    c = synth.synth_inputs(7 * B + Tc + 1, (B, 80, Tc), loc=-5.0, scale=2.0)
+    st = np.full((B, 1), 41.5, np.float32)
+    eps = m((tt(audio), tt(c), tt(st))).cpu().numpy()
+    assert_bf16_close(eps, OF.fastdiff_forward(OF.fold_weight_norm(p), audio, c, st))

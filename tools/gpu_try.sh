@@ -1,12 +1,19 @@
 #!/bin/bash
-# Retry a gpurun call ONLY while the pool reports "no box free" (exit 3: nothing ran,
-# nothing charged).  Any other exit (including failures of the command) ends the loop.
+# Retry a gpurun call ONLY while the pool reports "no box free" (exit 3) or an
+# infrastructure back-off (nothing ran, nothing charged).  Any other exit, including
+# failures of the command itself, ends the loop.
 # usage: tools/gpu_try.sh <timeout-s> <max-tries> '<command>'
 T=$1; N=$2; CMD=$3
+LOG=$(mktemp)
 for i in $(seq 1 $N); do
-  /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD"
-  rc=$?
-  [ $rc -ne 3 ] && exit $rc
-  sleep 90
+  /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD" 2>&1 | tee "$LOG"
+  rc=${PIPESTATUS[0]}
+  if [ $rc -eq 3 ] || { [ $rc -eq 2 ] && grep -q "backing off" "$LOG"; }; then
+    sleep 120
+    continue
+  fi
+  rm -f "$LOG"
+  exit $rc
 done
+rm -f "$LOG"
 exit 3

@@ -1,0 +1,112 @@
+// Standalone probe for lvc_block_bf16_kernel: times the kernel alone on C3-sized
+// synthetic inputs and prints where a block spends its time (s_memtime stamps per
+// phase, LB_TRACE).  Diagnostic only (not a parity check: inputs are random).
+//   build: make -C tools lvc_probe      run: tools/build/lvc_probe [hop] [TS]
+#define LB_TRACE 1
+#include "../prodiff_amd/csrc/fastdiff.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                  \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+static unsigned long long rng = 88172645463325252ull;
+static float frand() {   // xorshift, uniform [-1, 1)
+  rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+  return (float)((rng >> 40) & 0xFFFFFF) / 8388608.f - 1.f;
+}
+template <typename T> static T* upload(size_t n, float scale) {
+  std::vector<T> h(n);
+  for (size_t i = 0; i < n; ++i) h[i] = (T)(scale * frand());
+  T* d;
+  CK(hipMalloc((void**)&d, n * sizeof(T)));
+  CK(hipMemcpy(d, h.data(), n * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+template <int TS> static void run(int hop) {
+  using G = LbGeo<TS>;
+  const int B = 8, Tc = 861;
+  const long long Lh = (long long)Tc * hop, rows = B * Lh;
+  LvcBlockArgs la{};
+  la.xin = upload<float>(rows * CI, 1.f);
+  la.a = upload<float>(rows * CI, 1.f);
+  CK(hipMalloc((void**)&la.xout, rows * CI * sizeof(float)));
+  for (int l = 0; l < NLY; ++l) {
+    la.Kf[l] = upload<__bf16>((size_t)B * Tc * KPERLAYER, 0.1f);
+    la.Wc[l] = upload<__bf16>(CI * 96, 0.2f);
+    la.bc[l] = upload<float>(CI, 0.05f);
+  }
+  la.Bf = upload<float>((size_t)B * Tc * 2 * CI * NLY, 0.1f);
+  la.Tc = Tc; la.hop = hop;
+  const dim3 grid(cdiv(Lh, TS), B);
+  const int nsamp = (grid.x * grid.y) / 61 + 1;
+  CK(hipMalloc((void**)&la.trace, (size_t)nsamp * G::NW * 16 * 8));
+  CK(hipMemset(la.trace, 0, (size_t)nsamp * G::NW * 16 * 8));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(lvc_block_bf16_kernel<TS>, grid, dim3(G::NT), 0, 0, la);
+  const int reps = 20;
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(lvc_block_bf16_kernel<TS>, grid, dim3(G::NT), 0, 0, la);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1000.0 / reps;
+  const double bytes = (double)rows * 3 * 128 + (double)B * Tc * NLY * (KPERLAYER * 2 + 256);
+  printf("TS=%d hop=%d grid=%dx%d  %.1f us/launch  %.2f TB/s (x,a in + x out + kernels)\n", TS, hop, grid.x,
+         grid.y, us, bytes / us * 1e-6);
+  std::vector<unsigned long long> tr((size_t)nsamp * G::NW * 16);
+  CK(hipMemcpy(tr.data(), la.trace, tr.size() * 8, hipMemcpyDeviceToHost));
+  // mean per-phase cycles over sampled waves (last launch's stamps)
+  const char* names[16] = {"start", "zero+load", "L0 stage", "L0 preconv", "L0 lvc", "L1 stage", "L1 preconv",
+                           "L1 lvc", "L2 stage", "L2 preconv", "L2 lvc", "L3 stage", "L3 preconv", "-",
+                           "L3 lvc", "store"};
+  // median per-phase duration over sampled waves whose stamps are monotone
+  std::vector<std::vector<double>> ph(16);
+  std::vector<double> life;
+  for (int s = 0; s < nsamp * G::NW; ++s) {
+    const unsigned long long* t = &tr[(size_t)s * 16];
+    bool ok = t[0] != 0;
+    unsigned long long prev = t[0];
+    for (int i = 1; i < 16 && ok; ++i) {
+      if (i == 13) continue;
+      ok = t[i] >= prev && t[i] - prev < 100000000ull;
+      prev = t[i];
+    }
+    if (!ok) continue;
+    prev = t[0];
+    for (int i = 1; i < 16; ++i) {
+      if (i == 13) continue;
+      ph[i].push_back((double)(t[i] - prev));
+      prev = t[i];
+    }
+    life.push_back((double)(t[15] - t[0]));
+  }
+  auto med = [](std::vector<double> v) {
+    if (v.empty()) return 0.0;
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  const double L = med(life);
+  printf("  %zu sampled waves, median lifetime %.0f cycles\n", life.size(), L);
+  for (int i = 1; i < 16; ++i)
+    if (i != 13) printf("    %-11s %8.0f cyc  %5.1f%%\n", names[i], med(ph[i]), 100.0 * med(ph[i]) / L);
+}
+
+int main(int argc, char** argv) {
+  const int hop = argc > 1 ? atoi(argv[1]) : 256;
+  const int ts = argc > 2 ? atoi(argv[2]) : 128;
+  if (ts == 256) run<256>(hop); else run<128>(hop);
+  return 0;
+}
