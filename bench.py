@@ -62,6 +62,10 @@ def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
         # whole LVC block (4 layers of pre-conv + LVC), hop >= 64 blocks (bf16 path)
         "fd_lvc_block": sum(4 * (2 * r * 32 * 96 + 2 * r * 64 * 96) for r in rows[1:]) / 2.0,
         "fd_final_update": 2 * F * 256 * 32 * 7,
+        # whole LVC block with the upsample fused (hop-64 block, r = 8)
+        "fd_lvc_block_ups": rows[1] * (4 * (2 * 32 * 96 + 2 * 64 * 96) + 2 * 2 * 32 * 32),
+        # hop-256 block with upsample (r = 4), first conv and final conv + update fused
+        "fd_lvc_block_final": rows[2] * (4 * (2 * 32 * 96 + 2 * 64 * 96) + 2 * 2 * 32 * 32 + 2 * 2 * 7 * 32),
     }
 
 
@@ -95,6 +99,10 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_lvc": sum(lvc_v) / 3.0,
         "fd_upsample": sum(r * (1 + 1.0 / h) * per_row_io for r, h in zip(rows, (8, 8, 4))) / 3.0,
         "fd_final_update": F * 256 * (32 + 3) * 4,
+        # x_prev (r = 8 fewer rows) + audio_down in, x out, the 4 layers' kernels + biases
+        "fd_lvc_block_ups": rows[1] / 8 * per_row_io + rows[1] * 2 * per_row_io + F * 4 * kf_frame,
+        # x_prev (r = 4 fewer rows) + audio sample in + new audio sample out, kernels + biases
+        "fd_lvc_block_final": rows[2] / 4 * per_row_io + rows[2] * 2 * 4 + F * 4 * kf_frame,
     }
 
 

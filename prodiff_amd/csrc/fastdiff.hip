@@ -52,6 +52,7 @@ struct fd_model {
   int hops[4];
   int dtype;
   int lvc_ts = 128;            // whole-block LVC tile (128/256); 0 = one fused launch per layer (PRODIFF_LVC_TS)
+  bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (PRODIFF_LVC_FUSE)
   float* pool = nullptr;
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
   // step MLP
@@ -60,6 +61,7 @@ struct fd_model {
   float *final_w, *final_b;          // [7][32], [1]
   struct Block {
     float *up_w, *up_b;              // [2r][32 ci][32 co]
+    float *upf_w;                    // [r][32 co][64]: phase k's [W_k^T | W_{k+r}^T] (fused upsample, bf16 mirror)
     float *fct_w, *fct_b;            // [80][512]
     float *kin_w, *kin_b;            // [64][5*96]
     float *kres_w[6], *kres_b[6];    // [64][3*64]
@@ -303,17 +305,39 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
 // tile lies in ONE frame and multiplies one 64x96 kernel.  The state x and audio_down a
 // stay in registers in the MFMA C layout (wave w owns tiles w and w + NW); LDS only
 // holds the bf16 operands u = lrelu(x + a) and y.  Layer l is valid on rows
-// [64 - e_l, 64 + TS + e_l), e = 42, 38, 28, 0 (the remaining dilation reach), and
-// only the tiles overlapping that range are computed; rows outside it are never
-// read by a valid row, so they may hold anything.
+// [64 - e_l, 64 + TS + e_l), e = 42, 38, 28, 0 (the remaining dilation reach; +3 each
+// when the final conv is fused), and only the tiles overlapping that range are
+// computed; rows outside it are never read by a valid row, so they may hold anything.
+//
+// Optional fusions (template flags), each removing a full-rate HBM round trip:
+//  UPS  the block's ConvTranspose upsample (modules.py:205-206) runs in the prologue
+//       from x_prev (r x fewer rows), as r phase GEMMs on MFMA: output t = r j + k - p
+//       uses taps k and k + r on inputs j and j - 1 (K = 64), staged through LDS.
+//  AUD  audio_down = first_conv(audio) (FastDiff_model.py:90) is recomputed per row
+//       from the 1-channel audio instead of read as a [L][32] tensor.
+//  FIN  the final conv7 32 -> 1 and the sampler update (FastDiff_model.py:100,
+//       util.py:222-226) run in the epilogue: only the new audio sample leaves.
 struct LvcBlockArgs {
-  float* xout;              // [B][Lh][32]
-  const float* xin;         // [B][Lh][32] upsample output
-  const float* a;           // [B][Lh][32] audio_down
+  float* xout;              // [B][Lh][32]                  (!FIN)
+  const float* xin;         // [B][Lh][32] upsampled x (!UPS), or x_prev [B][Lh/r][32] (UPS)
+  const float* a;           // [B][Lh][32] audio_down       (!AUD)
   const __bf16* Kf[NLY];    // [B*Tc][6144] per layer (frame-major, fragment order)
   const float* Bf;          // [B*Tc][256]: layer l at +64 l
   const __bf16* Wc[NLY];    // [32][96] pre-conv weights (bf16 mirror)
   const float* bc[NLY];
+  const __bf16* Wup;        // UPS: [r][32 co][64] = [W_k^T | W_{k+r}^T] per phase k
+  const float* bup;         // UPS: [32]
+  int r, p;                 // UPS: ratio, ConvTranspose padding
+  const float* audio;       // AUD / FIN: [B][Lh] current sample x_t
+  const float* fw;          // AUD: first conv [32][7]
+  const float* fb;          // AUD: [32]
+  const float* wfin;        // FIN: final conv [7][32]
+  const float* bfin;        // FIN: [1]
+  float* audio_out;         // FIN: [B][Lh]  (x_t - ce eps) / den + sig z
+  const float* noise;       // FIN: explicit z [B][Lh] or null (Philox)
+  float ce, den, sig;
+  unsigned long long seed;
+  unsigned stream;
   int Tc, hop;
 #ifdef LB_TRACE
   unsigned long long* trace;   // tools/lvc_probe.hip: per-phase s_memtime stamps
@@ -332,6 +356,7 @@ struct LvcBlockArgs {
   } while (0)
 #endif
 constexpr int LB_LD = 40;
+constexpr int LB_XLD = 36;                          // fp32 staging rows (144 B)
 template <int TS> struct LbGeo {
   static constexpr int NG = TS / 32 + 4;            // tiles in the grid
   static constexpr int NW = NG / 2;                 // waves; two tiles each
@@ -339,6 +364,11 @@ template <int TS> struct LbGeo {
   static constexpr int UOFF = 28;                   // U index = row + 28 (pre-conv reach 1 + 27)
   static constexpr int UROWS = NG * 32 + 2 * UOFF;
   static constexpr int YROWS = (NG + 1) * 32;       // Y index = row + 1
+  static constexpr int UY_BYTES = (UROWS + YROWS) * LB_LD * 2;
+  static constexpr int XS_BYTES = NG * 32 * LB_XLD * 4;          // fp32 x rows (prologue / epilogue)
+  static constexpr int NTJ_MAX = (NG * 32 / 4 + 2 + 31) / 32;    // phase-GEMM column tiles at r >= 4
+  static constexpr int XP_BYTES = (NTJ_MAX * 32 + 1) * LB_LD * 2;
+  static constexpr int SMEM = UY_BYTES > XS_BYTES + XP_BYTES ? UY_BYTES : XS_BYTES + XP_BYTES;
 };
 
 // Packed-fp32 epilogue helpers (v_pk_fma/mul/add_f32 work on two lanes' values at once).
@@ -357,54 +387,145 @@ __device__ __forceinline__ f32x2 gate2s(f32x2 gs, f32x2 fs) {
   const f32x2 den = (ef + 1.f) * (eg + 1.f);
   return (ef - 1.f) * f32x2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
 }
+__device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0 ? a : a - b + 1) / b; }
 
-template <int TS>
+template <int TS, bool UPS, bool AUD, bool FIN>
 __global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
   using G = LbGeo<TS>;
-  constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF;
+  constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF, GR = NG * 32;
+  constexpr int EX = FIN ? 3 : 0;                    // extra valid rows for the fused final conv
   // Rows = time, 40 bf16 per row; position p of a row holds channel lvc_chan(p).
-  __shared__ __attribute__((aligned(16))) __bf16 U[G::UROWS * LB_LD];
-  __shared__ __attribute__((aligned(16))) __bf16 Y[G::YROWS * LB_LD];
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  __shared__ float AS[AUD ? GR + 6 : 1];             // audio at times [tg - 3, tg + GR + 3)
+  __shared__ __attribute__((aligned(16))) float FW[AUD ? 7 * 32 : 4];   // first conv [tap][c]
+  __shared__ __attribute__((aligned(16))) float FWF[FIN ? 7 * 32 : 4];  // final conv [tap][c]
+  __bf16* U = reinterpret_cast<__bf16*>(smem);
+  __bf16* Y = U + G::UROWS * LB_LD;
+  float* XS = reinterpret_cast<float*>(smem);                       // aliases U/Y outside the layers
+  __bf16* XP = reinterpret_cast<__bf16*>(smem + G::XS_BYTES);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, h = lane >> 5;
-  const int b = blockIdx.y, Tc = P.Tc, hop = P.hop;
-  const int Lh = Tc * hop;                           // utterance-local times fit in 32 bits
-  const int t0 = blockIdx.x * TS, tg = t0 - 64;      // time of grid row 0
-  const long long base = (long long)b * Lh;
-  LB_STAMP(0);
+  // XCD-aware block order: the hardware deals consecutive block ids round-robin over
+  // the 8 XCDs; remap so each XCD walks a contiguous run of (utterance, time) tiles and
+  // neighbouring tiles -- which share frames' kernels and halo rows -- share its L2.
+  int bx, b;
   {
-    const bf16x8 z = {};
-    for (int i = tid; i < G::UROWS * LB_LD / 8; i += G::NT) reinterpret_cast<bf16x8*>(U)[i] = z;
-    for (int i = tid; i < G::YROWS * LB_LD / 8; i += G::NT) reinterpret_cast<bf16x8*>(Y)[i] = z;
+    const int total = gridDim.x * gridDim.y, id = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xcd = id & 7, slot = id >> 3, per = total >> 3, rem = total & 7;
+    const int logical = xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
+    b = logical / gridDim.x;
+    bx = logical - b * gridDim.x;
+  }
+  const int Tc = P.Tc, hop = P.hop;
+  const int Lh = Tc * hop;                           // utterance-local times fit in 32 bits
+  const int t0 = bx * TS, tg = t0 - 64;              // time of grid row 0
+  const long long base = (long long)b * Lh;
+  constexpr int RLO = 64 - 44 - EX, RHI = 64 + TS + 44 + EX;   // x rows the valid region reads
+  LB_STAMP(0);
+  if constexpr (AUD) {
+    for (int i = tid; i < GR + 6; i += G::NT) {
+      const int t = tg - 3 + i;
+      AS[i] = (t >= 0 && t < Lh) ? P.audio[base + t] : 0.f;
+    }
+  }
+  if constexpr (AUD) {
+    for (int i = tid; i < 224; i += G::NT) FW[i] = P.fw[(i & 31) * 7 + (i >> 5)];   // fw is [c][tap]
+  }
+  if constexpr (FIN) {
+    for (int i = tid; i < 224; i += G::NT) FWF[i] = P.wfin[i];                     // already [tap][c]
+  }
+  // ---- prologue: x rows (upsampled in-kernel, or loaded) -> registers
+  f32x2 xr[2][8], ar[2][8];
+  if constexpr (UPS) {
+    // (a) XP[j - jb] = bf16 lrelu(x_prev[j]), j in [jb, jb + 32 ntj]: j0 - 1 .. j0 of every column
+    const int r = P.r, pp = P.p, Tin = Lh / r;
+    const int ntj = (GR / r + 2 + 31) / 32;
+    const int jb = floordiv(tg + pp, r) - 2;         // column j0 = jb + 1 + c, c < 32 ntj
+    const float* xp = P.xin + (long long)b * Tin * CI;
+    for (int i = tid; i < (ntj * 32 + 1) * 8; i += G::NT) {
+      const int rr = i >> 3, q = (i & 7) * 4, j = jb + rr;
+      bf16x4 v = {};
+      if (j >= 0 && j < Tin) {
+        const float4 f = *reinterpret_cast<const float4*>(xp + (long long)j * CI + q);
+        const f32x2 u0 = lrelu2(f32x2{f.x, f.y}), u1 = lrelu2(f32x2{f.z, f.w});
+        v = bf16x4{(__bf16)u0.x, (__bf16)u0.y, (__bf16)u1.x, (__bf16)u1.y};
+      }
+      *reinterpret_cast<bf16x4*>(&XP[rr * LB_LD + q]) = v;
+    }
+    __syncthreads();
+    // (b) phase GEMMs: C^T[co][col] = [W_k^T | W_{k+r}^T] . [xp(j0); xp(j0 - 1)], t = r j0 + k - p
+    for (int job = wave; job < r * ntj; job += NW) {
+      const int k = job / ntj, jt = job - k * ntj;
+      const __bf16* wa = P.Wup + ((long long)k * 32 + n) * 64 + 8 * h;
+      f32x16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
+        // k-step kk < 2: input j0 (XP row c + 1), kk >= 2: input j0 - 1 (XP row c)
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(
+            &XP[(jt * 32 + n + (kk < 2 ? 1 : 0)) * LB_LD + 16 * (kk & 1) + 8 * h]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xb, acc, 0, 0, 0);
+      }
+      const int j0 = jb + 1 + jt * 32 + n, row = r * j0 + k - pp - tg;
+      if (row >= RLO && row < RHI) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = *reinterpret_cast<const float4*>(P.bup + 8 * g + 4 * h);
+          *reinterpret_cast<float4*>(&XS[row * LB_XLD + 8 * g + 4 * h]) =
+              make_float4(acc[4 * g] + bv.x, acc[4 * g + 1] + bv.y, acc[4 * g + 2] + bv.z, acc[4 * g + 3] + bv.w);
+        }
+      }
+    }
+    __syncthreads();
+  } else if constexpr (AUD) {
+    __syncthreads();                                  // AS / FW visible
   }
   // Transposed C layout: lane (n, h) of tile k holds time tg + 32k + n, channels
   // (reg&3) + 8(reg>>2) + 4h; pair p = regs (2p, 2p+1).  Four float4 loads per tensor
-  // (channels 8i + 4h .. +3).  Rows [20, TS + 108) = times [t0 - 44, t0 + TS + 44).
-  f32x2 xr[2][8], ar[2][8];
+  // (channels 8i + 4h .. +3).
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int k = wave + j * NW, row = k * 32 + n, t = tg + row;
-    const bool ok = row >= 20 && row < TS + 108 && t >= 0 && t < Lh;
+    const bool ok = row >= RLO && row < RHI && t >= 0 && t < Lh;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
-#ifdef LB_EXP_NOXA
-      if (ok) { xv = make_float4(0.1f * i, 0.2f, 0.3f, (float)t * 1e-6f); av = xv; }
-#else
       if (ok) {
-        xv = *reinterpret_cast<const float4*>(P.xin + (base + t) * CI + 8 * i + 4 * h);
-        av = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + 8 * i + 4 * h);
+        if constexpr (UPS) xv = *reinterpret_cast<const float4*>(&XS[row * LB_XLD + 8 * i + 4 * h]);
+        else xv = *reinterpret_cast<const float4*>(P.xin + (base + t) * CI + 8 * i + 4 * h);
+        if constexpr (AUD) {
+          // a0[t][c] = b[c] + sum_tap w[c][tap] audio[t + tap - 3], first_conv_kernel's order
+          float a4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a4[e] = P.fb[8 * i + 4 * h + e];
+#pragma unroll
+          for (int tap = 0; tap < 7; ++tap) {
+            const float s = AS[row + tap];
+            const float4 w = *reinterpret_cast<const float4*>(&FW[tap * 32 + 8 * i + 4 * h]);
+            a4[0] = fmaf(w.x, s, a4[0]); a4[1] = fmaf(w.y, s, a4[1]);
+            a4[2] = fmaf(w.z, s, a4[2]); a4[3] = fmaf(w.w, s, a4[3]);
+          }
+          av = make_float4(a4[0], a4[1], a4[2], a4[3]);
+        } else {
+          av = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + 8 * i + 4 * h);
+        }
       }
-#endif
       xr[j][2 * i] = f32x2{xv.x, xv.y}; xr[j][2 * i + 1] = f32x2{xv.z, xv.w};
       ar[j][2 * i] = f32x2{av.x, av.y}; ar[j][2 * i + 1] = f32x2{av.z, av.w};
     }
+  }
+  if constexpr (UPS) __syncthreads();                // XS reads done before U/Y (aliased) are zeroed
+  {
+    const bf16x8 z = {};
+    for (int i = tid; i < G::UY_BYTES / 16; i += G::NT) reinterpret_cast<bf16x8*>(smem)[i] = z;
   }
   __syncthreads();
   LB_STAMP(1);
 #pragma unroll
   for (int l = 0; l < NLY; ++l) {
     const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
-    const int e = l == 0 ? 42 : l == 1 ? 38 : l == 2 ? 28 : 0;
+    const int e = (l == 0 ? 42 : l == 1 ? 38 : l == 2 ? 28 : 0) + EX;
     const int kf = (64 - e) / 32, kl = (64 + TS + e - 1) / 32;   // LVC tiles of this layer
     const int kpl = kl + 1 < NG - 1 ? kl + 1 : NG - 1;           // last pre-conv tile
     // (1) u = lrelu(x + a) of the owned tiles the pre-conv reads: 2 x 16 B per lane
@@ -481,11 +602,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const 
     for (int j = 0; j < 2; ++j) {
       const int k = wave + j * NW, ts = tg + k * 32;
       if (k >= kf && k <= kl && ts >= 0 && ts < Lh) {
-#ifdef LB_EXP_K0
-        const int frame = 0 * (ts / hop) + (b & 0);   // probe ablation: cache-resident kernels
-#else
         const int frame = ts / hop;
-#endif
         const __bf16* kq = P.Kf[l] + ((long long)b * Tc + frame) * KPERLAYER;
         const float* bq = P.Bf + ((long long)b * Tc + frame) * (2 * CI * NLY) + l * 2 * CI;
         f32x16 g, f;
@@ -507,15 +624,10 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const 
           const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
           const f32x2 bg0 = f32x2{bg.x, bg.y} * cg, bg1 = f32x2{bg.z, bg.w} * cg;
           const f32x2 bl0 = f32x2{bl.x, bl.y} * cf, bl1 = f32x2{bl.z, bl.w} * cf;
-#ifdef LB_EXP_NOGATE
-          const f32x2 o0 = f32x2{g[4 * i], g[4 * i + 1]} + f32x2{f[4 * i], f[4 * i + 1]} + bg0 + bl0;
-          const f32x2 o1 = f32x2{g[4 * i + 2], g[4 * i + 3]} + f32x2{f[4 * i + 2], f[4 * i + 3]} + bg1 + bl1;
-#else
           const f32x2 o0 = gate2s(__builtin_elementwise_fma(f32x2{g[4 * i], g[4 * i + 1]}, cg, bg0),
                                   __builtin_elementwise_fma(f32x2{f[4 * i], f[4 * i + 1]}, cf, bl0));
           const f32x2 o1 = gate2s(__builtin_elementwise_fma(f32x2{g[4 * i + 2], g[4 * i + 3]}, cg, bg1),
                                   __builtin_elementwise_fma(f32x2{f[4 * i + 2], f[4 * i + 3]}, cf, bl1));
-#endif
           xr[j][2 * i] += ar[j][2 * i] + o0;
           xr[j][2 * i + 1] += ar[j][2 * i + 1] + o1;
         }
@@ -524,15 +636,55 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const 
     if (l < NLY - 1) LB_STAMP(4 + 3 * l);
   }
   LB_STAMP(14);
-  // centre tiles [2, 2 + TS/32) -> x out
+  if constexpr (FIN) {
+    // eps(t) = b + sum_{tap, c} w[tap][c] x(t + tap - 3)[c] on the centre rows; x rows
+    // [61, 67 + TS) go through fp32 LDS (aliasing U/Y: every wave is past its Y reads).
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int k = wave + j * NW, t = tg + k * 32 + n;
-    if (k >= 2 && k < 2 + TS / 32 && t < Lh) {
+    for (int j = 0; j < 2; ++j) {
+      const int k = wave + j * NW, row = k * 32 + n;
+      if (k >= 1 && k <= NG - 2) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<float4*>(P.xout + (base + t) * CI + 8 * i + 4 * h) =
-            make_float4(xr[j][2 * i].x, xr[j][2 * i].y, xr[j][2 * i + 1].x, xr[j][2 * i + 1].y);
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<float4*>(&XS[row * LB_XLD + 8 * i + 4 * h]) =
+              make_float4(xr[j][2 * i].x, xr[j][2 * i].y, xr[j][2 * i + 1].x, xr[j][2 * i + 1].y);
+      }
+    }
+    __syncthreads();
+    // two lanes per output sample (16 channels each), combined by one shuffle
+    for (int s2 = tid; s2 < 2 * TS; s2 += G::NT) {
+      const int s = s2 >> 1, c0 = (s2 & 1) * 16, t = t0 + s;
+      float e = 0.f;
+#pragma unroll
+      for (int tap = 0; tap < 7; ++tap) {
+        const float* xrow = &XS[(64 + s + tap - 3) * LB_XLD + c0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(xrow + 4 * q);
+          const float4 w = *reinterpret_cast<const float4*>(&FWF[tap * 32 + c0 + 4 * q]);
+          e = fmaf(w.x, v.x, fmaf(w.y, v.y, fmaf(w.z, v.z, fmaf(w.w, v.w, e))));
+        }
+      }
+      e += __shfl_xor(e, 1);
+      if ((s2 & 1) == 0 && t < Lh) {
+        e += P.bfin[0];
+        const long long idx = base + t;
+        float v = (P.audio[idx] - P.ce * e) / P.den;
+        if (P.sig != 0.f) v += P.sig * (P.noise ? P.noise[idx] : philox_normal(P.seed, (unsigned long long)idx, P.stream));
+        P.audio_out[idx] = v;
+      }
+    }
+  } else {
+    // centre tiles [2, 2 + TS/32) -> x out
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = wave + j * NW, t = tg + k * 32 + n;
+      if (k >= 2 && k < 2 + TS / 32 && t < Lh) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<float4*>(P.xout + (base + t) * CI + 8 * i + 4 * h) =
+              make_float4(xr[j][2 * i].x, xr[j][2 * i].y, xr[j][2 * i + 1].x, xr[j][2 * i + 1].y);
+      }
     }
   }
   LB_STAMP(15);
@@ -549,7 +701,8 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
                                                           const __bf16* __restrict__ W0, const float* __restrict__ b0,
                                                           const __bf16* __restrict__ W1, const float* __restrict__ b1,
                                                           const __bf16* __restrict__ W2, const float* __restrict__ b2,
-                                                          int Lout, int f) {
+                                                          int Lout, int f, const float* __restrict__ audio,
+                                                          const float* __restrict__ fw, const float* __restrict__ fb) {
   __shared__ __attribute__((aligned(16))) __bf16 U0[DB_ROWS * DB_LD];   // lrelu(x[f i])
   __shared__ __attribute__((aligned(16))) __bf16 R0[DB_ROWS * DB_LD];   // x[f i] (residual input)
   __shared__ __attribute__((aligned(16))) __bf16 H1[DB_ROWS * DB_LD];
@@ -561,7 +714,25 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   for (int i = tid; i < DB_ROWS * 8; i += 256) {
     const int p = i >> 3, q = (i & 7) * 4, ii = ib + p;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p < DB_TS + 14 && ii >= 0 && ii < Lout) v = *reinterpret_cast<const float4*>(src + (long long)ii * f * CI + q);
+    if (p < DB_TS + 14 && ii >= 0 && ii < Lout) {
+      if (audio) {   // input = first_conv(audio) (FastDiff_model.py:90), recomputed: no a0 tensor
+        const long long t = (long long)ii * f;
+        const float* au = audio + (long long)b * Lin;
+        float a7[7], o[4];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) a7[k] = (t + k - 3 >= 0 && t + k - 3 < Lin) ? au[t + k - 3] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float acc = fb[q + e];
+#pragma unroll
+          for (int k = 0; k < 7; ++k) acc = fmaf(fw[(q + e) * 7 + k], a7[k], acc);   // first_conv_kernel's order
+          o[e] = acc;
+        }
+        v = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+        v = *reinterpret_cast<const float4*>(src + (long long)ii * f * CI + q);
+      }
+    }
     *reinterpret_cast<bf16x4*>(&R0[p * DB_LD + q]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
     v.x = v.x >= 0.f ? v.x : 0.2f * v.x; v.y = v.y >= 0.f ? v.y : 0.2f * v.y;
     v.z = v.z >= 0.f ? v.z : 0.2f * v.z; v.w = v.w >= 0.f ? v.w : 0.2f * v.w;
@@ -642,7 +813,7 @@ struct KPArgs {
   const float* br[4][6];
   const __bf16* Wb[4];      // [256][3*64]  bias_conv
   const float* bb[4];
-  float* hout;              // [z][B][Tc][64]  h = h0 + R(h0)
+  __bf16* hout;             // [z][B][Tc][64]  h = h0 + R(h0), bf16 (the kernel GEMM's operand)
   float* Bf;                // [z][B][Tc][256] LVC biases
   int Tc;
 };
@@ -662,7 +833,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   const int z = blockIdx.z, step = z / A.nb, nblk = z - step * A.nb;
   const long long rb = (long long)b * Tc;
   const float* nzrow = A.nz + (long long)step * A.nz_step + (long long)b * A.nz_ld + nblk * CC;
-  float* hout = A.hout + (long long)z * A.B * Tc * HK;
+  __bf16* hout = A.hout + (long long)z * A.B * Tc * HK;
   float* Bfo = A.Bf + (long long)z * A.B * Tc * (2 * CI * NLY);
 
   // c' = c + fc_t(e) on frames f0-18 .. f0+81 (channels 80..95 zero)
@@ -737,7 +908,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
         if (j == 5) v += keep[q][reg];           // h = h0 + R(h0)
         if (f < 0 || f >= Tc) v = 0.f;
         Out[(p + 1) * LDH + n] = (__bf16)v;
-        if (j == 5 && p >= 16 && p < 80 && f < Tc) hout[(rb + f) * HK + n] = v;
+        if (j == 5 && p >= 16 && p < 80 && f < Tc) hout[(rb + f) * HK + n] = (__bf16)v;
       }
     }
     __syncthreads();
@@ -766,25 +937,28 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   }
 }
 
-// Location-variable kernels of one LVC layer, frame-major bf16 (modules.py:335-340):
-//   Kf[f][n] = b[n] + W[n] . [h(f-1); h(f); h(f+1)]      n < 6144, K = 192
-// Block: 128 frames (one 32-frame tile per wave, its h fragments held in registers for
-// the whole block) x a run of 64-row weight tiles.  Each weight tile is staged in LDS
-// with coalesced 16-B loads (double-buffered, next tile in flight under the MFMAs).
-// The MFMA computes C[n][frame] (weights as the A operand), so a lane holds 4
-// consecutive kernel values of one frame and stores 8 B at a time.
-constexpr int KPK_ROWS = 128, KPK_NT = 64, KPK_LDW = 200;   // 400-B LDS rows: conflict-free b128 reads
-constexpr int KPK_LDO = 72;                                  // output transpose rows: 64 + 8 pad
-__global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __restrict__ hin,
-                                                             const __bf16* __restrict__ W,
-                                                             const float* __restrict__ bias,
-                                                             __bf16* __restrict__ Kf, int Tc, int rows,
-                                                             int tiles_per_block) {
-  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][KPK_NT * KPK_LDW];
-  __shared__ __attribute__((aligned(16))) __bf16 Ot[4][32 * KPK_LDO];
+// Location-variable kernels of ALL 4 layers of an LVC block, frame-major bf16
+// (modules.py:335-340):  Kf[l][f][n] = b[l][n] + W[l][n] . [h(f-1); h(f); h(f+1)],
+// n < 6144, K = 192.  One GEMM with 4 x 6144 rows (weights = MFMA A operand, staged in
+// LDS 64 rows at a time, double-buffered, next tile's loads in flight under the MFMAs)
+// and one column per frame.  Block = 256 frames; each wave keeps the bf16 h fragments
+// of its 64 frames (two 32-frame MFMA tiles) in registers for the whole block, so each
+// 16-B LDS weight read feeds two MFMAs.  A lane of C holds 4 consecutive kernel values
+// of one frame; a per-wave LDS transpose turns them into full 128-B line stores.
+// Block (x, y) owns frames [256x, 256x + 256) and weight tiles [y T / G, (y+1) T / G).
+constexpr int KP_FR = 256, KP_NT = 64, KP_LDW = 200;   // 400-B LDS rows: conflict-free b128 reads
+constexpr int KP_LDO = 72;                             // output transpose rows: 64 + 8 pad
+constexpr int KP_TILES = NLY * KPERLAYER / KP_NT;      // 384
+__global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __restrict__ hin,
+                                                                const __bf16* __restrict__ W,
+                                                                const float* __restrict__ bias,
+                                                                __bf16* __restrict__ Kf, int Tc, int rows,
+                                                                int groups) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][KP_NT * KP_LDW];
+  __shared__ __attribute__((aligned(16))) __bf16 Ot[4][32 * KP_LDO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
-  const int R = blockIdx.x * KPK_ROWS + wave * 32 + r32;     // frame (C column) of this lane
-  const int tile0 = blockIdx.y * tiles_per_block;
+  const int fw = blockIdx.x * KP_FR + wave * 64;            // first frame of this wave
+  const int tb = blockIdx.y * KP_TILES / groups, te = (blockIdx.y + 1) * KP_TILES / groups;
   // W tile = 64 rows x 384 B = 1536 16-B pieces, 6 per thread (named registers: an
   // indexed array here is demoted to scratch by hipcc)
   uint4 s0, s1, s2, s3, s4, s5;
@@ -793,11 +967,11 @@ __global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __rest
   for (int i = 0; i < 6; ++i) {
     const int c = tid + 256 * i, row = c / 24, col = (c - row * 24) * 8;
     goff[i] = row * 192 + col;
-    loff[i] = row * KPK_LDW + col;
+    loff[i] = row * KP_LDW + col;
   }
-#define KPK_LD(t)                                                        \
+#define KP_LD(t)                                                         \
   do {                                                                   \
-    const __bf16* src_ = W + (long long)(t) * KPK_NT * 192;              \
+    const __bf16* src_ = W + (long long)(t) * KP_NT * 192;               \
     s0 = *reinterpret_cast<const uint4*>(src_ + goff[0]);                \
     s1 = *reinterpret_cast<const uint4*>(src_ + goff[1]);                \
     s2 = *reinterpret_cast<const uint4*>(src_ + goff[2]);                \
@@ -805,7 +979,7 @@ __global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __rest
     s4 = *reinterpret_cast<const uint4*>(src_ + goff[4]);                \
     s5 = *reinterpret_cast<const uint4*>(src_ + goff[5]);                \
   } while (0)
-#define KPK_ST(buf)                                                      \
+#define KP_ST(buf)                                                       \
   do {                                                                   \
     *reinterpret_cast<uint4*>(&Ws[buf][loff[0]]) = s0;                   \
     *reinterpret_cast<uint4*>(&Ws[buf][loff[1]]) = s1;                   \
@@ -814,74 +988,89 @@ __global__ __launch_bounds__(256) void kp_kernel_bf16_kernel(const float* __rest
     *reinterpret_cast<uint4*>(&Ws[buf][loff[4]]) = s4;                   \
     *reinterpret_cast<uint4*>(&Ws[buf][loff[5]]) = s5;                   \
   } while (0)
-#define load_tile(t) KPK_LD(t)
-#define store_tile(b) KPK_ST(b)
-  load_tile(tile0);
-  bf16x8 af[12];
-  {
+  KP_LD(tb);
+  // B fragments: k = tap*64 + ch (tap-major), lane half h holds 8 consecutive channels
+  bf16x8 af[2][12];
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft) {
+    const int R = fw + ft * 32 + r32;
     const bool ok = R < rows;
     const int b = ok ? R / Tc : 0, f = R - b * Tc;
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk) {
       const int tap = kk >> 2, kc = kk & 3, ff = f + tap - 1;
-      float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
-      if (ok && ff >= 0 && ff < Tc) {
-        const float* p = hin + ((long long)b * Tc + ff) * HK + kc * 16 + h * 8;
-        u = *reinterpret_cast<const float4*>(p);
-        v = *reinterpret_cast<const float4*>(p + 4);
-      }
-      af[kk] = bf16x8{(__bf16)u.x, (__bf16)u.y, (__bf16)u.z, (__bf16)u.w,
-                      (__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+      bf16x8 v = {};
+      if (ok && ff >= 0 && ff < Tc) v = *reinterpret_cast<const bf16x8*>(hin + ((long long)b * Tc + ff) * HK + kc * 16 + h * 8);
+      af[ft][kk] = v;
     }
   }
-  store_tile(0);
+  KP_ST(0);
   __syncthreads();
-  for (int it = 0; it < tiles_per_block; ++it) {
-    const int buf = it & 1;
-    if (it + 1 < tiles_per_block) load_tile(tile0 + it + 1);
-    f32x16 acc[2];
+  __bf16* ot = Ot[wave];
+  for (int t = tb; t < te; ++t) {
+    const int buf = (t - tb) & 1;
+    if (t + 1 < te) KP_LD(t + 1);
+    f32x16 acc[2][2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][ft][r] = 0.f;
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&Ws[buf][(j * 32 + r32) * KPK_LDW + kk * 16 + h * 8]);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[kk], acc[j], 0, 0, 0);
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&Ws[buf][(j * 32 + r32) * KP_LDW + kk * 16 + h * 8]);
+        acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[0][kk], acc[j][0], 0, 0, 0);
+        acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[1][kk], acc[j][1], 0, 0, 0);
       }
     }
-    // C[n][frame]: this lane owns frame R, rows n = n0 + 32j + 8g + 4h + (0..3).
-    // Transpose through LDS so each store instruction writes 8 frames x 128 B full lines.
-    const int n0 = (tile0 + it) * KPK_NT;
-    __bf16* ot = Ot[wave];
+    // C[n][frame]: lane owns frame (r32) of tile ft, rows n = 32j + 8g + 4h + (0..3)
+    const int layer = t / (KPERLAYER / KP_NT), n0 = (t - layer * (KPERLAYER / KP_NT)) * KP_NT;
+    __bf16* kout = Kf + (long long)layer * rows * KPERLAYER + n0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int ft = 0; ft < 2; ++ft) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int nl = j * 32 + 8 * g + 4 * h;
-        const float4 bn = *reinterpret_cast<const float4*>(bias + n0 + nl);
-        *reinterpret_cast<bf16x4*>(&ot[r32 * KPK_LDO + nl]) =
-            bf16x4{(__bf16)(acc[j][4 * g] + bn.x), (__bf16)(acc[j][4 * g + 1] + bn.y),
-                   (__bf16)(acc[j][4 * g + 2] + bn.z), (__bf16)(acc[j][4 * g + 3] + bn.w)};
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int nl = j * 32 + 8 * g + 4 * h;
+          const float4 bn = *reinterpret_cast<const float4*>(bias + (long long)t * KP_NT + nl);
+          *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + nl]) =
+              bf16x4{(__bf16)(acc[j][ft][4 * g] + bn.x), (__bf16)(acc[j][ft][4 * g + 1] + bn.y),
+                     (__bf16)(acc[j][ft][4 * g + 2] + bn.z), (__bf16)(acc[j][ft][4 * g + 3] + bn.w)};
+        }
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
+        const int Rf = fw + ft * 32 + fl;
+        const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
+        if (Rf < rows) *reinterpret_cast<uint4*>(kout + (long long)Rf * KPERLAYER + ch) = v;
       }
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
-      const int Rf = blockIdx.x * KPK_ROWS + wave * 32 + fl;
-      const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KPK_LDO + ch]);
-      if (Rf < rows) *reinterpret_cast<uint4*>(Kf + (long long)Rf * KPERLAYER + n0 + ch) = v;
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // transpose reads done before the next tile's writes
+      __builtin_amdgcn_wave_barrier();
     }
-    if (it + 1 < tiles_per_block) store_tile(buf ^ 1);
+    if (t + 1 < te) KP_ST(buf ^ 1);
     __syncthreads();
   }
-#undef load_tile
-#undef store_tile
-#undef KPK_LD
-#undef KPK_ST
+#undef KP_LD
+#undef KP_ST
+}
+
+// All 4 layers' kernels of one LVC block into Kb ([4][B*Tc][6144], bf16).
+int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B, int Tc, hipStream_t st) {
+  const int rows = B * Tc;
+  const int fblocks = cdiv(rows, KP_FR);
+  int groups = 512 / fblocks;                 // 2 blocks per CU x 256 CUs, one wave of blocks
+  groups = groups < 1 ? 1 : groups > KP_TILES ? KP_TILES : groups;
+  ProfScope ps("fd_kp_kernel", st);
+  hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(fblocks, groups), dim3(256), 0, st, hk, lookup_bf16(K.kk_w),
+                     K.kk_b, Kb, Tc, rows, groups);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
 }
 
 // eps[b][t] = bias + sum_{k<7,c<32} w[k][c] x[b][t+k-3][c]      (FastDiff_model.py:67-68,100)
@@ -953,6 +1142,16 @@ __global__ void pack_upsample_kernel(float* dst, const float* src, int K) {
   dst[(k * CI + ci) * CI + co] = src[i];
 }
 
+// fused-upsample phase weights: dst[(k*32 + co)*64 + q] = q < 32 ? W[k][q][co] : W[k+r][q-32][co]
+// from the [2r][ci][co] packing above
+__global__ void pack_upsample_phase_kernel(float* dst, const float* wp, int r) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= CI * CI * 2 * r) return;
+  const int q = i & 63, co = (i >> 6) & 31, k = i >> 11;
+  const int kk = q < 32 ? k : k + r, ci = q & 31;
+  dst[i] = wp[(kk * CI + ci) * CI + co];
+}
+
 // final conv weight [1][32][7] -> [7][32]
 __global__ void pack_final_kernel(float* dst, const float* src) {
   int i = threadIdx.x;
@@ -962,7 +1161,7 @@ __global__ void pack_final_kernel(float* dst, const float* src) {
 // ------------------------------------------------------------------ workspace
 struct FdWs {
   size_t steps, e128, e512a, e512, nz;  // step MLP (nvec = S*B)
-  size_t a0, d[3], dtmp0, dtmp1, xs;
+  size_t a0, d[3], dtmp0, dtmp1, xs, wav2;
   size_t X0, X1, y, h0, ra, rb, Bf, Kf, condT, hall, bfall, total;
 };
 
@@ -978,6 +1177,7 @@ FdWs fd_layout(const fd_model* m, int B, int Tc, int S) {
   w.e512 = take(nv * EMB_OUT);
   w.nz = take(nv * m->nblocks * CC);
   w.a0 = take((size_t)B * L * CI);
+  w.wav2 = take((size_t)B * L);   // sampler ping-pong buffer (fused final update)
   size_t Ld = L;
   for (int n = 0; n < m->nblocks; ++n) {
     Ld /= m->ratios[m->nblocks - 1 - n];
@@ -1015,12 +1215,13 @@ int fd_step_mlp(const fd_model* m, float* ws, const FdWs& W, int nv, hipStream_t
 
 // DiffusionDBlock (modules.py:131-138): out = conv_d4(lr(conv_d2(lr(conv_d1(lr(x[f i])))))) + Wr x[f i]
 int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, float* t1, int B, int Tout,
-           int f, hipStream_t st) {
+           int f, hipStream_t st, const fd_model* m = nullptr, const float* audio = nullptr) {
   const long long bsi = (long long)Tout * f * CI, bso = (long long)Tout * CI;
   if (const __bf16* w0 = lookup_bf16(D.c0_w)) {   // bf16: one fused launch, intermediates in LDS
     ProfScope ps("fd_dblock_fused", st);
     hipLaunchKernelGGL(dblock_bf16_kernel, dim3(cdiv(Tout, DB_TS), B), dim3(256), 0, st, in, out, w0, D.c0_b,
-                       lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f);
+                       lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, audio,
+                       audio ? m->first_w : nullptr, audio ? m->first_b : nullptr);
     PD_LAUNCH_CHECK();
     return PD_OK;
   }
@@ -1068,26 +1269,73 @@ int fd_kp_hidden_all(const fd_model* m, float* ws, const FdWs& W, const float* c
     for (int j = 0; j < 6; ++j) { ka.Wr[n][j] = lookup_bf16(K.kres_w[j]); ka.br[n][j] = K.kres_b[j]; }
     ka.Wb[n] = lookup_bf16(K.kb_w); ka.bb[n] = K.kb_b;
   }
-  ka.hout = ws + W.hall; ka.Bf = ws + W.bfall; ka.Tc = Tc;
+  ka.hout = reinterpret_cast<__bf16*>(ws + W.hall); ka.Bf = ws + W.bfall; ka.Tc = Tc;
   ProfScope ps("fd_kp_hidden", st);
   hipLaunchKernelGGL(kp_hidden_bf16_kernel, dim3(cdiv(Tc, 64), B, nsteps * nb), dim3(256), 0, st, ka);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
 
-// One eps-network evaluation.  xa: audio [B][L]; condT: [B][Tc][80];
-// nz: this step's per-block fc_t(emb) rows ([B][nblocks*80]).  Leaves the LVC output in *xout.
-int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const float* condT,
-           const float* nz, int step, int B, int Tc, float** xout, hipStream_t st) {
-  const int nb = m->nblocks;
-  const long long L = (long long)Tc * m->hops[nb - 1];
-  float* a0 = ws + W.a0;
-  {
-  ProfScope ps("fd_first_conv", st);
-  hipLaunchKernelGGL(first_conv_kernel, dim3(cdiv(L, 32), B), dim3(256), 0, st, xa, m->first_w,
-                     m->first_b, a0, (int)L);
+// Does the last LVC block run as the fused kernel (upsample + first conv + final update)?
+bool fd_final_fused(const fd_model* m) {
+  const int n = m->nblocks - 1;
+  return m->pool_bf && m->lvc_ts > 0 && m->hops[n] % 64 == 0 && m->lvc_fuse && m->ratios[n] >= 4;
+}
+
+// The sampler update fused into the last LVC block (FIN): audio_out = (xa - ce eps)/den + sig z.
+struct FdFinal {
+  float* audio_out;
+  const float* noise;
+  float ce, den, sig;
+  unsigned long long seed;
+  unsigned stream;
+};
+
+template <int TS, bool UPS, bool AUD, bool FIN>
+void launch_lvc_block_t(const LvcBlockArgs& la, long long Tout, int B, hipStream_t st) {
+  hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, UPS, AUD, FIN>), dim3(cdiv(Tout, TS), B), dim3(LbGeo<TS>::NT), 0,
+                     st, la);
+}
+template <int TS>
+int launch_lvc_block_ts(const LvcBlockArgs& la, bool ups, bool aud, bool fin, long long Tout, int B,
+                        hipStream_t st) {
+  if (!ups) {
+    if (aud || fin) { set_error("lvc_block: audio/final fusion needs the fused upsample"); return PD_ERR_ARG; }
+    launch_lvc_block_t<TS, false, false, false>(la, Tout, B, st);
+  } else if (!aud && !fin) {
+    launch_lvc_block_t<TS, true, false, false>(la, Tout, B, st);
+  } else if (aud && !fin) {
+    launch_lvc_block_t<TS, true, true, false>(la, Tout, B, st);
+  } else if (aud && fin) {
+    launch_lvc_block_t<TS, true, true, true>(la, Tout, B, st);
+  } else {
+    set_error("lvc_block: final fusion needs the audio fusion"); return PD_ERR_ARG;
   }
   PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// One eps-network evaluation.  xa: audio [B][L]; condT: [B][Tc][80];
+// nz: this step's per-block fc_t(emb) rows ([B][nblocks*80]).  Leaves the LVC output in
+// *xout, or -- when `fin` is given and the last block is the fused LVC kernel -- applies
+// the sampler update itself and sets *xout = nullptr.
+int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const float* condT,
+           const float* nz, int step, int B, int Tc, float** xout, hipStream_t st,
+           const FdFinal* fin = nullptr) {
+  const int nb = m->nblocks;
+  const long long L = (long long)Tc * m->hops[nb - 1];
+  const bool bf = m->pool_bf != nullptr;
+  // whole-block LVC kernel with its prologue/epilogue fusions (bf16, hop % 64 == 0)
+  auto fused_block = [&](int n) { return bf && m->lvc_ts > 0 && m->hops[n] % 64 == 0; };
+  auto fused_ups = [&](int n) { return fused_block(n) && m->lvc_fuse && m->ratios[n] >= 4; };
+  const bool aud = fd_final_fused(m);              // a0 = first_conv(audio) recomputed by its consumers
+  float* a0 = ws + W.a0;
+  if (!aud) {
+    ProfScope ps("fd_first_conv", st);
+    hipLaunchKernelGGL(first_conv_kernel, dim3(cdiv(L, 32), B), dim3(256), 0, st, xa, m->first_w,
+                       m->first_b, a0, (int)L);
+    PD_LAUNCH_CHECK();
+  }
   // downsample chain: a0 -> d[0] -> ... -> d[nb-1]   (FastDiff_model.py:89-93)
   const float* cur = a0;
   long long Lc = L;
@@ -1096,7 +1344,8 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
     downs[n] = cur;
     const int f = m->ratios[nb - 1 - n];
     Lc /= f;
-    PD_TRY(dblock(m->dn[n], cur, ws + W.d[n], ws + W.dtmp0, ws + W.dtmp1, B, (int)Lc, f, st));
+    PD_TRY(dblock(m->dn[n], cur, ws + W.d[n], ws + W.dtmp0, ws + W.dtmp1, B, (int)Lc, f, st, m,
+                  n == 0 && aud ? xa : nullptr));
     cur = ws + W.d[n];
   }
   // LVC blocks (FastDiff_model.py:95-97)
@@ -1111,13 +1360,13 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
     const long long Tout = Tin * r;
     const long long bsC = (long long)Tc * CC, bsH = (long long)Tc * HK;
     // --- kernel predictor on c + fc_t(emb)   (modules.py:202-204, 320-343)
-    const bool bf = m->pool_bf != nullptr;
-    const float* hk = nullptr;   // final h  [B][Tc][64]
+    const float* hk = nullptr;   // final h  [B][Tc][64] (fp32 path)
+    const __bf16* hkb = nullptr; // final h, bf16 path
     float* Bfp = ws + W.Bf;      // LVC biases of this block [B][Tc][256]
     if (bf) {
       // computed for every step and block up front (fd_kp_hidden_all)
       const size_t z = (size_t)step * nb + n;
-      hk = ws + W.hall + z * B * Tc * HK;
+      hkb = reinterpret_cast<const __bf16*>(ws + W.hall) + z * B * Tc * HK;
       Bfp = ws + W.bfall + z * B * Tc * 2 * CI * NLY;
     } else {
     {
@@ -1150,6 +1399,46 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_BIAS>(a, st, "fd_kp_bias")));
     }
     }
+    if (fused_block(n)) {
+      // every layer's kernels first (frame-major bf16), then the whole block in one launch
+      const bool ups = fused_ups(n), last = n == nb - 1;
+      const bool fuse_fin = ups && last && fin != nullptr;
+      if (!ups) {   // separate upsample (modules.py:205-206)
+        ProfScope ps("fd_upsample", st);
+        hipLaunchKernelGGL(upsample_kernel, dim3(cdiv(Tin, 32), r, B), dim3(256), 0, st, x, K.up_w, K.up_b,
+                           xn, (int)Tin, r, r / 2 + r % 2);
+        PD_LAUNCH_CHECK();
+      }
+      __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf);
+      const int rows = B * Tc;
+      PD_TRY(kp_kernels_all(K, hkb, Kb, B, Tc, st));
+      LvcBlockArgs la{};
+      for (int i = 0; i < NLY; ++i) {
+        la.Kf[i] = Kb + (size_t)i * rows * KPERLAYER;
+        la.Wc[i] = lookup_bf16(K.cv_w[i]);
+        la.bc[i] = K.cv_b[i];
+      }
+      la.xin = ups ? x : xn;
+      la.xout = ws + W.y;
+      la.a = (last && aud) ? nullptr : ad;
+      la.Bf = Bfp; la.Tc = Tc; la.hop = hop;
+      la.Wup = lookup_bf16(K.upf_w); la.bup = K.up_b; la.r = r; la.p = r / 2 + r % 2;
+      la.audio = xa; la.fw = m->first_w; la.fb = m->first_b;
+      la.wfin = m->final_w; la.bfin = m->final_b;
+      if (fuse_fin) {
+        la.audio_out = fin->audio_out; la.noise = fin->noise; la.ce = fin->ce; la.den = fin->den;
+        la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream;
+      }
+      {
+        ProfScope ps(fuse_fin ? "fd_lvc_block_final" : ups ? "fd_lvc_block_ups" : "fd_lvc_block", st);
+        if (m->lvc_ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, Tout, B, st));
+        else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, Tout, B, st));
+      }
+      if (fuse_fin) { *xout = nullptr; return PD_OK; }
+      x = ws + W.y;
+      Tin = Tout;
+      continue;
+    }
     // --- upsample (modules.py:205-206)
     {
       const int p = r / 2 + r % 2;
@@ -1159,49 +1448,10 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       PD_LAUNCH_CHECK();
     }
     // --- 4 LVC layers (modules.py:208-217)
-    if (bf && hop >= 64 && m->lvc_ts > 0) {
-      // every layer's kernels first (frame-major bf16), then the whole block in one launch
-      __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf);
-      const int rows = B * Tc;
-      const int rblocks = cdiv(rows, KPK_ROWS);
-      int groups = 1;
-      while (groups < 32 && rblocks * groups < 512) groups *= 2;   // groups | 96
-      LvcBlockArgs la{};
-      for (int i = 0; i < NLY; ++i) {
-        ProfScope ps("fd_kp_kernel", st);
-        hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(rblocks, groups), dim3(256), 0, st, hk,
-                           lookup_bf16(K.kk_w) + (size_t)i * KPERLAYER * 3 * HK, K.kk_b + (size_t)i * KPERLAYER,
-                           Kb + (size_t)i * rows * KPERLAYER, Tc, rows, (KPERLAYER / KPK_NT) / groups);
-        PD_LAUNCH_CHECK();
-        la.Kf[i] = Kb + (size_t)i * rows * KPERLAYER;
-        la.Wc[i] = lookup_bf16(K.cv_w[i]);
-        la.bc[i] = K.cv_b[i];
-      }
-      la.xin = xn; la.xout = ws + W.y; la.a = ad; la.Bf = Bfp; la.Tc = Tc; la.hop = hop;
-      {
-        ProfScope ps("fd_lvc_block", st);
-        if (m->lvc_ts == 256)
-          hipLaunchKernelGGL(lvc_block_bf16_kernel<256>, dim3(cdiv(Tout, 256), B), dim3(LbGeo<256>::NT), 0, st, la);
-        else
-          hipLaunchKernelGGL(lvc_block_bf16_kernel<128>, dim3(cdiv(Tout, 128), B), dim3(LbGeo<128>::NT), 0, st, la);
-        PD_LAUNCH_CHECK();
-      }
-      x = ws + W.y;
-      Tin = Tout;
-      continue;
-    }
+    if (bf) PD_TRY(kp_kernels_all(K, hkb, reinterpret_cast<__bf16*>(ws + W.Kf), B, Tc, st));   // all 4 layers
     for (int i = 0; i < NLY; ++i) {
-      if (bf) {  // this layer's kernels, frame-major bf16
-        ProfScope ps("fd_kp_kernel", st);
-        const int rows = B * Tc;
-        const int rblocks = cdiv(rows, KPK_ROWS);
-        int groups = 1;
-        while (groups < 32 && rblocks * groups < 512) groups *= 2;   // groups | 96
-        hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(rblocks, groups), dim3(256), 0, st, hk,
-                           lookup_bf16(K.kk_w) + (size_t)i * KPERLAYER * 3 * HK, K.kk_b + (size_t)i * KPERLAYER,
-                           reinterpret_cast<__bf16*>(ws + W.Kf), Tc, rows, (KPERLAYER / KPK_NT) / groups);
-        PD_LAUNCH_CHECK();
-      } else {
+      const __bf16* Kbl = reinterpret_cast<const __bf16*>(ws + W.Kf) + (size_t)i * B * Tc * KPERLAYER;
+      if (!bf) {
         GemmArgs a = make_gemm(B, Tc, KPERLAYER, K.kk_w + (size_t)i * KPERLAYER * 3 * HK, 3 * HK,
                                K.kk_b + (size_t)i * KPERLAYER, ws + W.Kf, (long long)Tc * KPERLAYER,
                                KPERLAYER);
@@ -1212,7 +1462,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       if (bf && hop % 64 == 0) {
         // one fused launch per layer: pre-conv + LVC + gate (bf16 MFMA)
         ProfScope ps("fd_lvc_fused", st);
-        const __bf16* Kb = reinterpret_cast<const __bf16*>(ws + W.Kf);
+        const __bf16* Kb = Kbl;
         const __bf16* Wc = lookup_bf16(K.cv_w[i]);
         if (hop % 128 == 0)
           hipLaunchKernelGGL(lvc_fused_bf16_kernel<128>, dim3(B * Tc * (hop / 128)), dim3(256), 0, st, xn, ad, Kb,
@@ -1235,7 +1485,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         ProfScope ps("fd_lvc", st);
         if (bf)
           hipLaunchKernelGGL(lvc_kernel<__bf16>, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y,
-                             reinterpret_cast<const __bf16*>(ws + W.Kf), KPERLAYER, Bfp + i * 2 * CI,
+                             Kbl, KPERLAYER, Bfp + i * 2 * CI,
                              2 * CI * NLY, Tc, hop);
         else
           hipLaunchKernelGGL(lvc_kernel<float>, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y, ws + W.Kf,
@@ -1269,6 +1519,7 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   m->nblocks = dims->num_blocks;
   m->dtype = dtype;
   if (const char* e = getenv("PRODIFF_LVC_TS")) m->lvc_ts = atoi(e);   // A/B switch (bench/tests)
+  if (const char* e = getenv("PRODIFF_LVC_FUSE")) m->lvc_fuse = atoi(e) != 0;
   int hop = 1;
   for (int n = 0; n < m->nblocks; ++n) {
     m->ratios[n] = dims->upsample_ratios[n];
@@ -1285,6 +1536,7 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   for (int n = 0; n < m->nblocks; ++n) {
     auto& K = m->blk[n];
     plan.push_back({&K.up_w, (size_t)2 * m->ratios[n] * CI * CI}); plan.push_back({&K.up_b, CI});
+    plan.push_back({&K.upf_w, (size_t)2 * m->ratios[n] * CI * CI});
     plan.push_back({&K.fct_w, (size_t)CC * EMB_OUT}); plan.push_back({&K.fct_b, CC});
     plan.push_back({&K.kin_w, (size_t)HK * 5 * 96}); plan.push_back({&K.kin_b, HK});
     for (int j = 0; j < 6; ++j) { plan.push_back({&K.kres_w[j], (size_t)HK * 3 * HK}); plan.push_back({&K.kres_b[j], HK}); }
@@ -1327,6 +1579,9 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
       {
         const float* w = nxt();
         hipLaunchKernelGGL(pack_upsample_kernel, dim3(cdiv(CI * CI * 2 * r, 256)), dim3(256), 0, st, K.up_w, w, 2 * r);
+        PD_LAUNCH_CHECK();
+        hipLaunchKernelGGL(pack_upsample_phase_kernel, dim3(cdiv(CI * CI * 2 * r, 256)), dim3(256), 0, st, K.upf_w,
+                           K.up_w, r);
         PD_LAUNCH_CHECK();
         PD_TRY(cp(K.up_b, nxt(), CI));
       }
@@ -1438,11 +1693,17 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
   hipStream_t st = (hipStream_t)stream;
   float* ws = (float*)workspace;
   const long long L = (long long)Tc * m->hops[m->nblocks - 1];
+  // With the update fused into the last LVC block, step j reads one audio buffer and
+  // writes the other (its neighbours' halos still read the old samples): start in the
+  // buffer that makes the last step land in `wav`.
+  const bool fused = fd_final_fused(m);
+  float* cur = (!fused || N % 2 == 0) ? wav : ws + W.wav2;
+  float* other = cur == wav ? ws + W.wav2 : wav;
   // x_T ~ N(0,1)  (util.py:208)
   if (x_T) {
-    PD_HIP(hipMemcpyAsync(wav, x_T, sizeof(float) * B * L, hipMemcpyDeviceToDevice, st));
+    PD_HIP(hipMemcpyAsync(cur, x_T, sizeof(float) * B * L, hipMemcpyDeviceToDevice, st));
   } else {
-    PD_TRY(fill_normal(wav, B * L, seed, 0xFFFF0001u, st));
+    PD_TRY(fill_normal(cur, B * L, seed, 0xFFFF0001u, st));
   }
   // every step's embedding at once: pass j uses n = N-1-j
   std::vector<float> sv(N);
@@ -1453,19 +1714,26 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
   for (int j = 0; j < N; ++j) {
     const int n = N - 1 - j;
     float* x = nullptr;
-    PD_TRY(fd_net(m, ws, W, wav, mel, ws + W.nz + (size_t)j * B * m->nblocks * CC, j, B, Tc, &x, st));
     // x = (x - beta/sqrt(1-alpha^2) eps) / sqrt(1-beta) + [n>0] sigma z   (util.py:222-226)
     const float ce = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
     const float den = sqrtf(1.f - beta[n]);
     const float sg = n > 0 ? sigma[n] : 0.f;
+    const FdFinal fin{other, noise ? noise + (size_t)j * B * L : (const float*)nullptr, ce, den, sg, seed,
+                      0x10000u + j};
+    PD_TRY(fd_net(m, ws, W, cur, mel, ws + W.nz + (size_t)j * B * m->nblocks * CC, j, B, Tc, &x, st,
+                  fused ? &fin : nullptr));
+    if (x == nullptr) {   // updated inside the last LVC block
+      std::swap(cur, other);
+      continue;
+    }
     {
     ProfScope ps("fd_final_update", st);
     hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w,
-                       m->final_b, (float*)nullptr, wav, ce, den, sg,
-                       noise ? noise + (size_t)j * B * L : (const float*)nullptr, seed, 0x10000u + j, L);
+                       m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + j, L);
     }
     PD_LAUNCH_CHECK();
   }
+  if (cur != wav) PD_HIP(hipMemcpyAsync(wav, cur, sizeof(float) * B * L, hipMemcpyDeviceToDevice, st));
   return PD_OK;
 }
 

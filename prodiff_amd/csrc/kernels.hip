@@ -41,6 +41,10 @@ int validate_gemm(const GemmArgs& a) {
 }
 
 // ---------------------------------------------------------------- matvec
+// out[v][n] = act(W[n] . in[v] + bias[n]).  One wave per output n and MV_NV vectors at
+// once (grid.y covers the vector groups), so each W row is read once per group and
+// the MV_NV dot products run side by side instead of one after another.
+constexpr int MV_NV = 8;
 __global__ __launch_bounds__(256) void matvec_kernel(const float* __restrict__ W,
                                                      const float* __restrict__ bias,
                                                      const float* __restrict__ in, int in_ld,
@@ -48,23 +52,38 @@ __global__ __launch_bounds__(256) void matvec_kernel(const float* __restrict__ W
                                                      int K, int nvec, int act) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int v0 = blockIdx.y * MV_NV;
   if (n >= N) return;
+  const int nv = nvec - v0 < MV_NV ? nvec - v0 : MV_NV;
   const float* w = W + (long long)n * K;
-  for (int v = 0; v < nvec; ++v) {
-    const float* x = in + (long long)v * in_ld;
-    float s = 0.f;
-    for (int k = lane; k < K; k += 64) s = fmaf(w[k], x[k], s);
+  float s[MV_NV];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (lane == 0) out[(long long)v * out_ld + n] = act_apply(s + (bias ? bias[n] : 0.f), act, 0.f);
+  for (int j = 0; j < MV_NV; ++j) s[j] = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float wk = w[k];
+#pragma unroll
+    for (int j = 0; j < MV_NV; ++j)
+      if (j < nv) s[j] = fmaf(wk, in[(long long)(v0 + j) * in_ld + k], s[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < MV_NV; ++j) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s[j] += __shfl_xor(s[j], o);
+  }
+  if (lane < nv) {
+    float r = s[0];
+#pragma unroll
+    for (int j = 1; j < MV_NV; ++j) r = lane == j ? s[j] : r;
+    out[(long long)(v0 + lane) * out_ld + n] = act_apply(r + (bias ? bias[n] : 0.f), act, 0.f);
   }
 }
 
 int matvec(const float* W, const float* bias, const float* in, int in_ld, float* out, int out_ld,
            int N, int K, int nvec, int act, hipStream_t st) {
   if (nvec <= 0) return PD_OK;
-  hipLaunchKernelGGL(matvec_kernel, dim3(cdiv(N, 4)), dim3(256), 0, st, W, bias, in, in_ld, out,
-                     out_ld, N, K, nvec, act);
+  ProfScope ps("step_mlp", st);
+  hipLaunchKernelGGL(matvec_kernel, dim3(cdiv(N, 4), cdiv(nvec, MV_NV)), dim3(256), 0, st, W, bias, in, in_ld,
+                     out, out_ld, N, K, nvec, act);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }

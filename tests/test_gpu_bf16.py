@@ -112,3 +112,27 @@ def test_fastdiff_lvc_block_bf16(monkeypatch, ts, B, Tc):
     st = np.full((B, 1), 41.5, np.float32)
     eps = m((tt(audio), tt(c), tt(st))).cpu().numpy()
     assert_bf16_close(eps, OF.fastdiff_forward(OF.fold_weight_norm(p), audio, c, st))
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("ts", [128, 256])
+@pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
+def test_fastdiff_sample_bf16_oracle(monkeypatch, fuse, ts, B, Tc):
+    """The 4-step sampler with the upsample / first conv / final update fused into the LVC
+    block kernel (PRODIFF_LVC_FUSE=1: audio ping-pong between steps) and unfused, against
+    the oracle sampler with the same explicit draws; ragged lengths put utterance edges
+    inside blocks and halos."""
+    monkeypatch.setenv("PRODIFF_LVC_TS", str(ts))
+    monkeypatch.setenv("PRODIFF_LVC_FUSE", str(fuse))
+    from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
+    p = G.fastdiff_params(31)
+    m = FastDiff()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+    m = m.to(DEV).set_compute_dtype("bf16")
+    b, a, s, st = fastdiff_infer_params(fastdiff_reverse_schedule(4), fastdiff_train_alpha())
+    mel = synth.synth_inputs(40 + B, (B, Tc, 80), loc=-5.0, scale=2.0)
+    xT = synth.synth_inputs(41 + B, (B, 1, Tc * 256))
+    nz = synth.synth_inputs(42 + B, (3, B, 1, Tc * 256))
+    wav = m.sample(tt(mel), b, a, s, st, x_T=tt(xT), noise=tt(nz)).cpu().numpy()
+    ref = OF.fastdiff_sample(OF.fold_weight_norm(p), np.transpose(mel, (0, 2, 1)), xT, nz, b, a, s, st)
+    assert_bf16_close(wav.reshape(ref.shape), ref)

@@ -54,10 +54,10 @@ template <int TS> static void run(int hop) {
   CK(hipMemset(la.trace, 0, (size_t)nsamp * G::NW * 16 * 8));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(lvc_block_bf16_kernel<TS>, grid, dim3(G::NT), 0, 0, la);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, false, false, false>), grid, dim3(G::NT), 0, 0, la);
   const int reps = 20;
   CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(lvc_block_bf16_kernel<TS>, grid, dim3(G::NT), 0, 0, la);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, false, false, false>), grid, dim3(G::NT), 0, 0, la);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
