@@ -64,6 +64,8 @@ def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_final_update": 2 * F * 256 * 32 * 7,
         # whole LVC block with the upsample fused (hop-64 block, r = 8)
         "fd_lvc_block_ups": rows[1] * (4 * (2 * 32 * 96 + 2 * 64 * 96) + 2 * 2 * 32 * 32),
+        # hop-8 block (several frames per 32-row tile), upsample fused (r = 8)
+        "fd_lvc_block_sub": rows[0] * (4 * (2 * 32 * 96 + 2 * 64 * 96) + 2 * 2 * 32 * 32),
         # hop-256 block with upsample (r = 4), first conv and final conv + update fused
         "fd_lvc_block_final": rows[2] * (4 * (2 * 32 * 96 + 2 * 64 * 96) + 2 * 2 * 32 * 32 + 2 * 2 * 7 * 32),
     }
@@ -101,6 +103,7 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_final_update": F * 256 * (32 + 3) * 4,
         # x_prev (r = 8 fewer rows) + audio_down in, x out, the 4 layers' kernels + biases
         "fd_lvc_block_ups": rows[1] / 8 * per_row_io + rows[1] * 2 * per_row_io + F * 4 * kf_frame,
+        "fd_lvc_block_sub": rows[0] / 8 * per_row_io + rows[0] * 2 * per_row_io + F * 4 * kf_frame,
         # x_prev (r = 4 fewer rows) + audio sample in + new audio sample out, kernels + biases
         "fd_lvc_block_final": rows[2] / 4 * per_row_io + rows[2] * 2 * 4 + F * 4 * kf_frame,
     }

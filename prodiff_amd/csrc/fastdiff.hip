@@ -53,6 +53,8 @@ struct fd_model {
   int dtype;
   int lvc_ts = 128;            // whole-block LVC tile (128/256); 0 = one fused launch per layer (PRODIFF_LVC_TS)
   bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (PRODIFF_LVC_FUSE)
+  bool lvc_pf = false;         // next-layer kernel fragments prefetched into registers (PRODIFF_LVC_PF)
+  bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (PRODIFF_LVC_SUB)
   float* pool = nullptr;
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
   // step MLP
@@ -301,8 +303,9 @@ __global__ __launch_bounds__(TS * 2) void lvc_fused_bf16_kernel(
 // All 4 LVC layers of one TimeAware_LVCBlock (modules.py:208-217) in ONE launch:
 //   for l < 4:  x = x + a + gate(LVC_l(lrelu(conv_{3^l}(lrelu(x + a)) + b_l)))
 // Block = TS output samples of one utterance on a grid of NG 32-row tiles covering
-// [t0 - 64, t0 + TS + 64).  Tiles are 32-aligned in time and hop % 64 == 0, so every
-// tile lies in ONE frame and multiplies one 64x96 kernel.  The state x and audio_down a
+// [t0 - 64, t0 + TS + 64).  Tiles are 32-aligned in time; with hop % 32 == 0 every
+// tile lies in ONE frame and multiplies one 64x96 kernel (SUB: hop | 32, several frames
+// per tile, one masked MFMA chain each).  The state x and audio_down a
 // stay in registers in the MFMA C layout (wave w owns tiles w and w + NW); LDS only
 // holds the bf16 operands u = lrelu(x + a) and y.  Layer l is valid on rows
 // [64 - e_l, 64 + TS + e_l), e = 42, 38, 28, 0 (the remaining dilation reach; +3 each
@@ -389,8 +392,9 @@ __device__ __forceinline__ f32x2 gate2s(f32x2 gs, f32x2 fs) {
 }
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0 ? a : a - b + 1) / b; }
 
-template <int TS, bool UPS, bool AUD, bool FIN>
-__global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
+template <int TS, bool UPS, bool AUD, bool FIN, bool PF = false, bool SUB = false>
+__global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
+  static_assert(!(PF && SUB), "prefetch assumes one frame per tile");
   using G = LbGeo<TS>;
   constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF, GR = NG * 32;
   constexpr int EX = FIN ? 3 : 0;                    // extra valid rows for the fused final conv
@@ -520,6 +524,21 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const 
     const bf16x8 z = {};
     for (int i = tid; i < G::UY_BYTES / 16; i += G::NT) reinterpret_cast<bf16x8*>(smem)[i] = z;
   }
+  // PF: each tile's 64x96 kernel fragments for layer l are loaded into registers while
+  // layer l - 1 finishes (issued right after the tile's previous MFMAs), so their HBM
+  // latency hides behind the gate epilogue, the staging and the pre-conv.
+  bf16x8 kn[2][12];
+  auto kload = [&](int l, int j) {
+    const int e = (l == 0 ? 42 : l == 1 ? 38 : l == 2 ? 28 : 0) + EX;
+    const int kf = (64 - e) / 32, kl = (64 + TS + e - 1) / 32;
+    const int k = wave + j * NW, ts = tg + k * 32;
+    if (k >= kf && k <= kl && ts >= 0 && ts < Lh) {
+      const __bf16* kq = P.Kf[l] + ((long long)b * Tc + ts / hop) * KPERLAYER;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) kn[j][kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+    }
+  };
+  if constexpr (PF) { kload(0, 0); kload(0, 1); }
   __syncthreads();
   LB_STAMP(1);
 #pragma unroll
@@ -602,20 +621,54 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const 
     for (int j = 0; j < 2; ++j) {
       const int k = wave + j * NW, ts = tg + k * 32;
       if (k >= kf && k <= kl && ts >= 0 && ts < Lh) {
-        const int frame = ts / hop;
-        const __bf16* kq = P.Kf[l] + ((long long)b * Tc + frame) * KPERLAYER;
-        const float* bq = P.Bf + ((long long)b * Tc + frame) * (2 * CI * NLY) + l * 2 * CI;
         f32x16 g, f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) { g[r] = 0.f; f[r] = 0.f; }
+        const float* bq;
+        if constexpr (SUB) {
+          // hop < 32: the tile spans 32/hop frames.  Column n belongs to frame (ts + n)/hop;
+          // one MFMA chain per frame with the other frames' columns zeroed in B, so every
+          // column accumulates exactly its own frame's kernel.
+          bf16x8 yb[6];
+#pragma unroll
+          for (int kk = 0; kk < 6; ++kk)
+            yb[kk] = *reinterpret_cast<const bf16x8*>(&Y[(k * 32 + n + (kk >> 1)) * LB_LD + 16 * (kk & 1) + 8 * h]);
+          const int f0 = ts / hop, fn = (ts + n) / hop;
+          for (int fr = f0; fr < f0 + 32 / hop && fr < Tc; ++fr) {
+            const __bf16* kq = P.Kf[l] + ((long long)b * Tc + fr) * KPERLAYER;
+            const bool mine = fn == fr;
+#pragma unroll
+            for (int kk = 0; kk < 6; ++kk) {
+              const bf16x8 z = {};
+              const bf16x8 ym = mine ? yb[kk] : z;
+              const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+              const bf16x8 kt = *reinterpret_cast<const bf16x8*>(kq + ((6 + kk) * 64 + lane) * 8);
+              g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kg, ym, g, 0, 0, 0);
+              f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, ym, f, 0, 0, 0);
+            }
+          }
+          bq = P.Bf + ((long long)b * Tc + (fn < Tc ? fn : Tc - 1)) * (2 * CI * NLY) + l * 2 * CI;
+        } else {
+        const int frame = ts / hop;
+        const __bf16* kq = P.Kf[l] + ((long long)b * Tc + frame) * KPERLAYER;
+        bq = P.Bf + ((long long)b * Tc + frame) * (2 * CI * NLY) + l * 2 * CI;
 #pragma unroll
         for (int kk = 0; kk < 6; ++kk) {
           const int tap = kk >> 1;
           const bf16x8 yb = *reinterpret_cast<const bf16x8*>(&Y[(k * 32 + n + tap) * LB_LD + 16 * (kk & 1) + 8 * h]);
-          const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
-          const bf16x8 kt = *reinterpret_cast<const bf16x8*>(kq + ((6 + kk) * 64 + lane) * 8);
+          bf16x8 kg, kt;
+          if constexpr (PF) {
+            kg = kn[j][kk]; kt = kn[j][6 + kk];
+          } else {
+            kg = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+            kt = *reinterpret_cast<const bf16x8*>(kq + ((6 + kk) * 64 + lane) * 8);
+          }
           g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kg, yb, g, 0, 0, 0);
           f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, yb, f, 0, 0, 0);
+        }
+        if constexpr (PF) {
+          if (l + 1 < NLY) kload(l + 1, j);
+        }
         }
         const f32x2 cg = {-LOG2E, -LOG2E}, cf = {2.f * LOG2E, 2.f * LOG2E};
 #pragma unroll
@@ -628,8 +681,11 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, 3) void lvc_block_bf16_kernel(const 
                                   __builtin_elementwise_fma(f32x2{f[4 * i], f[4 * i + 1]}, cf, bl0));
           const f32x2 o1 = gate2s(__builtin_elementwise_fma(f32x2{g[4 * i + 2], g[4 * i + 3]}, cg, bg1),
                                   __builtin_elementwise_fma(f32x2{f[4 * i + 2], f[4 * i + 3]}, cf, bl1));
-          xr[j][2 * i] += ar[j][2 * i] + o0;
-          xr[j][2 * i + 1] += ar[j][2 * i + 1] + o1;
+          // hop < 32: a tile can straddle the utterance end; rows past it stay zero
+          // (they are the next layer's conv padding)
+          const float live = (!SUB || ts + n < Lh) ? 1.f : 0.f;
+          xr[j][2 * i] += ar[j][2 * i] + o0 * live;
+          xr[j][2 * i + 1] += ar[j][2 * i + 1] + o1 * live;
         }
       }
     }
@@ -1279,7 +1335,7 @@ int fd_kp_hidden_all(const fd_model* m, float* ws, const FdWs& W, const float* c
 // Does the last LVC block run as the fused kernel (upsample + first conv + final update)?
 bool fd_final_fused(const fd_model* m) {
   const int n = m->nblocks - 1;
-  return m->pool_bf && m->lvc_ts > 0 && m->hops[n] % 64 == 0 && m->lvc_fuse && m->ratios[n] >= 4;
+  return m->pool_bf && m->lvc_ts > 0 && m->hops[n] % 32 == 0 && m->lvc_fuse && m->ratios[n] >= 4;
 }
 
 // The sampler update fused into the last LVC block (FIN): audio_out = (xa - ce eps)/den + sig z.
@@ -1291,23 +1347,29 @@ struct FdFinal {
   unsigned stream;
 };
 
-template <int TS, bool UPS, bool AUD, bool FIN>
+template <int TS, bool UPS, bool AUD, bool FIN, bool PF, bool SUB = false>
 void launch_lvc_block_t(const LvcBlockArgs& la, long long Tout, int B, hipStream_t st) {
-  hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, UPS, AUD, FIN>), dim3(cdiv(Tout, TS), B), dim3(LbGeo<TS>::NT), 0,
-                     st, la);
+  hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, UPS, AUD, FIN, PF, SUB>), dim3(cdiv(Tout, TS), B),
+                     dim3(LbGeo<TS>::NT), 0, st, la);
 }
 template <int TS>
-int launch_lvc_block_ts(const LvcBlockArgs& la, bool ups, bool aud, bool fin, long long Tout, int B,
+int launch_lvc_block_ts(const LvcBlockArgs& la, bool ups, bool aud, bool fin, bool pf, long long Tout, int B,
                         hipStream_t st) {
-  if (!ups) {
+  if (la.hop < 32) {   // several frames per 32-row tile (the hop-8 block)
+    if (aud || fin) { set_error("lvc_block: audio/final fusion needs hop >= 32"); return PD_ERR_ARG; }
+    if (ups) launch_lvc_block_t<TS, true, false, false, false, true>(la, Tout, B, st);
+    else launch_lvc_block_t<TS, false, false, false, false, true>(la, Tout, B, st);
+  } else if (!ups) {
     if (aud || fin) { set_error("lvc_block: audio/final fusion needs the fused upsample"); return PD_ERR_ARG; }
-    launch_lvc_block_t<TS, false, false, false>(la, Tout, B, st);
+    launch_lvc_block_t<TS, false, false, false, false>(la, Tout, B, st);
   } else if (!aud && !fin) {
-    launch_lvc_block_t<TS, true, false, false>(la, Tout, B, st);
+    if (pf) launch_lvc_block_t<TS, true, false, false, true>(la, Tout, B, st);
+    else launch_lvc_block_t<TS, true, false, false, false>(la, Tout, B, st);
   } else if (aud && !fin) {
-    launch_lvc_block_t<TS, true, true, false>(la, Tout, B, st);
+    launch_lvc_block_t<TS, true, true, false, false>(la, Tout, B, st);
   } else if (aud && fin) {
-    launch_lvc_block_t<TS, true, true, true>(la, Tout, B, st);
+    if (pf) launch_lvc_block_t<TS, true, true, true, true>(la, Tout, B, st);
+    else launch_lvc_block_t<TS, true, true, true, false>(la, Tout, B, st);
   } else {
     set_error("lvc_block: final fusion needs the audio fusion"); return PD_ERR_ARG;
   }
@@ -1325,8 +1387,11 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
   const int nb = m->nblocks;
   const long long L = (long long)Tc * m->hops[nb - 1];
   const bool bf = m->pool_bf != nullptr;
-  // whole-block LVC kernel with its prologue/epilogue fusions (bf16, hop % 64 == 0)
-  auto fused_block = [&](int n) { return bf && m->lvc_ts > 0 && m->hops[n] % 64 == 0; };
+  // whole-block LVC kernel with its prologue/epilogue fusions (bf16)
+  // (hop % 32 == 0: one frame per 32-row tile; hop | 32: several, masked per frame)
+  auto fused_block = [&](int n) {
+    return bf && m->lvc_ts > 0 && (m->hops[n] % 32 == 0 || (32 % m->hops[n] == 0 && m->lvc_sub));
+  };
   auto fused_ups = [&](int n) { return fused_block(n) && m->lvc_fuse && m->ratios[n] >= 4; };
   const bool aud = fd_final_fused(m);              // a0 = first_conv(audio) recomputed by its consumers
   float* a0 = ws + W.a0;
@@ -1418,8 +1483,10 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         la.Wc[i] = lookup_bf16(K.cv_w[i]);
         la.bc[i] = K.cv_b[i];
       }
+      // never write the buffer this launch reads: with the upsample fused, x_prev is the
+      // previous block's output (the other ping-pong buffer, or the DBlock output)
       la.xin = ups ? x : xn;
-      la.xout = ws + W.y;
+      la.xout = ups ? xn : ws + W.y;
       la.a = (last && aud) ? nullptr : ad;
       la.Bf = Bfp; la.Tc = Tc; la.hop = hop;
       la.Wup = lookup_bf16(K.upf_w); la.bup = K.up_b; la.r = r; la.p = r / 2 + r % 2;
@@ -1430,12 +1497,13 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream;
       }
       {
-        ProfScope ps(fuse_fin ? "fd_lvc_block_final" : ups ? "fd_lvc_block_ups" : "fd_lvc_block", st);
-        if (m->lvc_ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, Tout, B, st));
-        else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, Tout, B, st));
+        ProfScope ps(fuse_fin ? "fd_lvc_block_final" : hop < 32 ? "fd_lvc_block_sub" : ups ? "fd_lvc_block_ups"
+                                                                                   : "fd_lvc_block", st);
+        if (m->lvc_ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, m->lvc_pf, Tout, B, st));
+        else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, m->lvc_pf, Tout, B, st));
       }
       if (fuse_fin) { *xout = nullptr; return PD_OK; }
-      x = ws + W.y;
+      x = la.xout;
       Tin = Tout;
       continue;
     }
@@ -1520,6 +1588,8 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   m->dtype = dtype;
   if (const char* e = getenv("PRODIFF_LVC_TS")) m->lvc_ts = atoi(e);   // A/B switch (bench/tests)
   if (const char* e = getenv("PRODIFF_LVC_FUSE")) m->lvc_fuse = atoi(e) != 0;
+  if (const char* e = getenv("PRODIFF_LVC_PF")) m->lvc_pf = atoi(e) != 0;
+  if (const char* e = getenv("PRODIFF_LVC_SUB")) m->lvc_sub = atoi(e) != 0;
   int hop = 1;
   for (int n = 0; n < m->nblocks; ++n) {
     m->ratios[n] = dims->upsample_ratios[n];

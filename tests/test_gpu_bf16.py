@@ -119,11 +119,13 @@ def test_fastdiff_lvc_block_bf16(monkeypatch, ts, B, Tc):
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
 def test_fastdiff_sample_bf16_oracle(monkeypatch, fuse, ts, B, Tc):
     """The 4-step sampler with the upsample / first conv / final update fused into the LVC
-    block kernel (PRODIFF_LVC_FUSE=1: audio ping-pong between steps) and unfused, against
+    block kernel (PRODIFF_LVC_FUSE=1: audio ping-pong between steps; the hop-8 block on the
+    masked multi-frame whole-block kernel) and unfused, against
     the oracle sampler with the same explicit draws; ragged lengths put utterance edges
     inside blocks and halos."""
     monkeypatch.setenv("PRODIFF_LVC_TS", str(ts))
     monkeypatch.setenv("PRODIFF_LVC_FUSE", str(fuse))
+    monkeypatch.setenv("PRODIFF_LVC_SUB", str(fuse))      # hop-8 block on the whole-block kernel too
     from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
     p = G.fastdiff_params(31)
     m = FastDiff()
