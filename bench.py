@@ -109,6 +109,41 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
     }
 
 
+# bench tag -> kernel symbol (TS = 128 defaults) for the PMC traffic lookup
+TAG_KERNEL = {
+    "fd_lvc_block_final": "lvc_block_bf16_kernel<128, true, true, true, false, false>",
+    "fd_lvc_block_ups": "lvc_block_bf16_kernel<128, true, false, false, false, false>",
+    "fd_lvc_block_sub": "lvc_block_bf16_kernel<128, true, false, false, false, true>",
+    "fd_kp_kernel": "kp_kernel_bf16_kernel",
+    "wn_layer": "wn_layer_bf16_kernel",
+}
+
+
+def pmc_traffic(tag, path=None):
+    """HBM bytes per launch of `tag`'s kernel from the newest committed PMC summary
+    (profiles/rNN_vMM_traffic.json, written by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench command).  None if absent."""
+    import glob
+    import re
+    if path is None:
+        def ver(f):
+            m = re.search(r"r(\d+)_v(\d+)_traffic\.json$", f)
+            return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_v*_traffic.json")), key=ver)
+        if not files:
+            return None, None
+        path = files[-1]
+    sym = TAG_KERNEL.get(tag)
+    if sym is None or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        kern = json.load(f)["kernels"]
+    for name, v in kern.items():
+        if sym in name:
+            return float(v["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def step_flops(B, T):
     """Whole-step algorithmic FLOPs: 2 x 26.43 + 4 x 56.98 MFLOP per frame."""
     f = flops_per_launch(B, T)
@@ -162,6 +197,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="compute dtype (C3 is specified in bf16; fp32 is the exact parity path)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--traffic", default=None, help="PMC traffic summary (default: newest profiles/r*_v*_traffic.json)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,7 +273,8 @@ def main():
             ach = fl[dom] * cnt / sec / 1e12
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
                         "frac": round(ach / peak_tf, 4)}
-        roofline.update({"traffic": None, "kernel": dom, "flop_per_launch": fl[dom],
+        traffic, tsrc = pmc_traffic(dom, args.traffic)
+        roofline.update({"traffic": round(traffic) if traffic else None, "traffic_source": tsrc, "kernel": dom, "flop_per_launch": fl[dom],
                          "bytes_per_launch": by.get(dom), "intensity_flop_per_byte": round(intensity, 1),
                          "ridge_flop_per_byte": round(ridge, 1), "avg_launch_us": round(ms / cnt * 1e3, 2),
                          "launches": cnt, "share_of_step": round(ms / (dt * 1e3), 3)})

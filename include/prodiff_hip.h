@@ -104,6 +104,37 @@ int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1
                       const float* noise, unsigned long long seed, float* mel, int B, int T,
                       void* workspace, size_t ws_bytes, void* stream);
 
+/* ============================================================= rectified flow
+ * RectifiedFlow / PitchRectifiedFlow inference (modules/diffusion/reflow.py:5-144) with
+ * the WaveNet velocity field -- the SVS teacher's diff_type "reflow"
+ * (modules/svs/prodiff_teacher.py:67-82) and the pitch predictor's sampler
+ * (modules/variance_predictor/pitch_predictor.py:40-55):
+ *   x ~ N(0,1); dt = 1/max(1,S); for i < S: x = step(x, t = i*dt)      (reflow.py:86-101)
+ *   v(x, t) = WaveNet(x, time_scale*t, cond); step = euler / rk2 / rk4 / rk5 (reflow.py:48-84).
+ * Euler's update is fused into the velocity output projection. */
+#define PD_REFLOW_EULER 0
+#define PD_REFLOW_RK2 1
+#define PD_REFLOW_RK4 2
+#define PD_REFLOW_RK5 3
+
+/* 0 if the arguments are invalid (S * stages > 128, unknown algorithm). */
+size_t pd_reflow_workspace_size(const pd_wavenet* h, int B, int T, int S, int algo);
+
+/*   cond [B,T,H] time-major (the condition before the transpose at reflow.py:33)
+ *   x_T  [B,T,M] time-major draw, or NULL -> Philox N(0,1) from `seed`
+ *   x    [B,T,M] output: the reference's x.transpose(2,3).squeeze(1) before denorm_spec. */
+int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, float time_scale,
+                     const float* x_T, unsigned long long seed, float* x, int B, int T,
+                     void* workspace, size_t ws_bytes, void* stream);
+
+/* denorm_spec (reflow.py:106-107): y = (x+1)/2 * (spec_max - spec_min) + spec_min with
+ * spec_min/spec_max device arrays of length nspec (1, broadcast, or M);  x [rows,M].
+ * mean_clamp = 0: out [rows,M] = y.  mean_clamp = 1 (PitchRectifiedFlow, :138-144):
+ * out [rows] = clamp(mean over the M bins of y, clamp_min, clamp_max). */
+int pd_reflow_denorm(const float* x, const float* spec_min, const float* spec_max, int nspec, int M,
+                     int rows, int mean_clamp, float clamp_min, float clamp_max, float* out,
+                     void* stream);
+
 /* ==================================================================== FastDiff
  * eps-network -- replaces modules/FastDiff/module/FastDiff_model.py:10-102 (FastDiff)
  * and the sampler util.py:158-232 (sampling_given_noise_schedule, ddim=False).

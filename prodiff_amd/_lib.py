@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("PRODIFF_HIP_LIB", os.path.join(_HERE, "libprodiff_hip
 
 PD_DTYPE_F32 = 0
 PD_DTYPE_BF16 = 1
+PD_REFLOW = {"euler": 0, "rk2": 1, "rk4": 2, "rk5": 3}
 
 
 class HipError(RuntimeError):
@@ -46,6 +47,11 @@ _SIGS = {
     "pd_prodiff_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                     C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP,
                                     C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
+    "pd_reflow_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "pd_reflow_sample": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_float, _VP, C.c_ulonglong, _VP, C.c_int,
+                                   C.c_int, _VP, C.c_size_t, _VP]),
+    "pd_reflow_denorm": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                   _VP, _VP]),
     "fd_create": (C.c_int, [C.POINTER(fd_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
     "fd_destroy": (None, [_VP]),
     "fd_hop": (C.c_int, [_VP]),

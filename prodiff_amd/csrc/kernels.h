@@ -16,8 +16,25 @@ int sinusoidal_embed(const float* steps, float* out, int nvec, int dim, hipStrea
 
 // steps[j*B + b] = first - j  (ProDiff reverse indices), j < S.
 int fill_reverse_steps(float* steps, int S, int B, int first, hipStream_t st);
-// steps[j*B + b] = vals[j] for host-provided values (FastDiff fractional steps).
+// steps[j*B + b] = vals[j] for host-provided values (FastDiff fractional steps, the
+// rectified-flow stage times), S <= PD_MAX_STEP_VALS (passed as a kernel argument).
+constexpr int PD_MAX_STEP_VALS = 128;
 int fill_steps(float* steps, const float* host_vals, int S, int B, hipStream_t st);
+
+// out[i] = x[i] + sum_j c[j] * k[j][i], j < n <= 6  (explicit Runge-Kutta stage inputs and
+// the final update of the rectified-flow sampler, reflow.py:48-84).  out may alias x.
+struct AxpyTerms {
+  const float* k[6];
+  float c[6];
+  int n;
+};
+int axpy_multi(float* out, const float* x, const AxpyTerms& t, long long n, hipStream_t st);
+
+// denorm_spec of the rectified flow (reflow.py:106-107, 138-144):
+//   y[r][m] = (x[r][m] + 1) / 2 * (smax[m'] - smin[m']) + smin[m'],  m' = nspec == 1 ? 0 : m
+//   mean_clamp: out[r] = clamp(mean_m y[r][m], cmin, cmax); else out[r][m] = y[r][m].
+int reflow_denorm(const float* x, const float* smin, const float* smax, int nspec, int M, long long rows,
+                  int mean_clamp, float cmin, float cmax, float* out, hipStream_t st);
 
 // [B][C][T] (channel-major, PyTorch Conv1d layout) <-> [B][T][C] (time-major)
 int transpose_ct_to_tc(const float* in, float* out, int B, int C, int T, hipStream_t st);

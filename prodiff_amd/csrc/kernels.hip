@@ -123,17 +123,66 @@ int fill_reverse_steps(float* steps, int S, int B, int first, hipStream_t st) {
   return PD_OK;
 }
 
-struct StepVals { float v[16]; };
+struct StepVals { float v[PD_MAX_STEP_VALS]; };
 __global__ void steps_kernel(float* steps, StepVals vals, int S, int B) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < S * B) steps[i] = vals.v[i / B];
 }
 
 int fill_steps(float* steps, const float* host_vals, int S, int B, hipStream_t st) {
-  if (S > 16) { set_error("fill_steps: at most 16 steps"); return PD_ERR_ARG; }
+  if (S > PD_MAX_STEP_VALS) { set_error("fill_steps: too many step values"); return PD_ERR_ARG; }
   StepVals sv{};
   for (int j = 0; j < S; ++j) sv.v[j] = host_vals[j];
   hipLaunchKernelGGL(steps_kernel, dim3(cdiv(S * B, 256)), dim3(256), 0, st, steps, sv, S, B);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// ---------------------------------------------------------------- rectified flow helpers
+// out[i] = x[i] + sum_j c[j] k[j][i]  (RK stage inputs / final update, reflow.py:48-84)
+__global__ void axpy_multi_kernel(float* out, const float* x, AxpyTerms t, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = x[i];
+  for (int j = 0; j < t.n; ++j) v = fmaf(t.c[j], t.k[j][i], v);
+  out[i] = v;
+}
+
+int axpy_multi(float* out, const float* x, const AxpyTerms& t, long long n, hipStream_t st) {
+  if (t.n < 0 || t.n > 6) { set_error("axpy_multi: 0..6 terms"); return PD_ERR_ARG; }
+  if (n <= 0) return PD_OK;
+  hipLaunchKernelGGL(axpy_multi_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, out, x, t, n);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// denorm_spec: (x + 1) / 2 * (max - min) + min  (reflow.py:106-107); mean_clamp: the
+// PitchRectifiedFlow form, mean over the bins then clamp (reflow.py:138-144)
+__global__ void reflow_denorm_kernel(const float* __restrict__ x, const float* __restrict__ smin,
+                                     const float* __restrict__ smax, int nspec, int M, long long rows,
+                                     int mean_clamp, float cmin, float cmax, float* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (mean_clamp) {
+    if (i >= rows) return;
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) {
+      const int k = nspec == 1 ? 0 : m;
+      s += (x[i * M + m] + 1.f) / 2.f * (smax[k] - smin[k]) + smin[k];
+    }
+    out[i] = fminf(fmaxf(s / (float)M, cmin), cmax);
+  } else {
+    if (i >= rows * M) return;
+    const int k = nspec == 1 ? 0 : (int)(i % M);
+    out[i] = (x[i] + 1.f) / 2.f * (smax[k] - smin[k]) + smin[k];
+  }
+}
+
+int reflow_denorm(const float* x, const float* smin, const float* smax, int nspec, int M, long long rows,
+                  int mean_clamp, float cmin, float cmax, float* out, hipStream_t st) {
+  const long long n = mean_clamp ? rows : rows * M;
+  if (n <= 0) return PD_OK;
+  hipLaunchKernelGGL(reflow_denorm_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, x, smin, smax, nspec, M, rows,
+                     mean_clamp, cmin, cmax, out);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }

@@ -69,47 +69,78 @@ struct WnLayerArgs {
   int B, T, H, dil, first;
 };
 
-template <int KMAX>
+template <int K1>
 __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P) {
   constexpr int C = WNF_C;
-  constexpr int LDA = KMAX + 8, LDG = C + 8;     // 16-B-offset rows: conflict-free b128 fragment reads
+  constexpr int LDA = K1 + 8, LDG = C + 8;       // 16-B-offset rows: conflict-free b128 fragment reads
   __shared__ __attribute__((aligned(16))) __bf16 As[32 * LDA];
   __shared__ __attribute__((aligned(16))) __bf16 Gs[32 * LDG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
-  const int H = P.H, K1 = 3 * C + H, rows = P.B * P.T, R0 = blockIdx.x * 32;
-  // stage [x(t-d)+dp; x(t)+dp; x(t+d)+dp; cond] as bf16 (zero outside each row's utterance)
-  const int ng = K1 / 4;
-  for (int i = tid; i < 32 * ng; i += 512) {
-    const int r = i / ng, g = (i - r * ng) * 4, R = R0 + r;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (R < rows) {
-      const int b = R / P.T, t = R - b * P.T;
-      if (g < 3 * C) {
-        const int tap = g / C, c = g - tap * C, tt = t + (tap - 1) * P.dil;
-        if (tt >= 0 && tt < P.T) {
-          v = *reinterpret_cast<const float4*>(P.xin + ((long long)b * P.T + tt) * C + c);
-          const float4 d = *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + c);
-          v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
-        }
-      } else {
-        v = *reinterpret_cast<const float4*>(P.cond + ((long long)b * P.T + t) * H + (g - 3 * C));
-      }
-    }
-    *reinterpret_cast<bf16x4*>(&As[r * LDA + g]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-  }
-  __syncthreads();
-
-  // GEMM1: gate tile nt = wave, filter tile nt = 8 + wave
-  const int KS1 = K1 / 16;
+  const int H = K1 - 3 * C, rows = P.B * P.T, R0 = blockIdx.x * 32;
+  // GEMM1: gate tile nt = wave, filter tile nt = 8 + wave.  Weight fragments stream from
+  // L2 through a register ring WD k-steps deep (the loop is fully unrolled, so every
+  // wait is a partial vmcnt): the L2 latency hides behind WD steps of MFMAs.  The ring
+  // is primed before the staging so its first loads fly with the activation loads.
+  constexpr int KS1 = K1 / 16, WD = 12;
   const bf16x8* wg = reinterpret_cast<const bf16x8*>(P.W1f) + (long long)wave * KS1 * 64 + lane;
   const bf16x8* wf = reinterpret_cast<const bf16x8*>(P.W1f) + (long long)(8 + wave) * KS1 * 64 + lane;
+  constexpr int KS2 = C / 16, WD2 = 8;
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)wave * KS2 * 64 + lane;
+  const bf16x8* wsk = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)(8 + wave) * KS2 * 64 + lane;
+  bf16x8 rg[WD], rf[WD];
+  constexpr int WD0 = 6;   // primed before the staging (the rest after it: register budget)
+#pragma unroll
+  for (int i = 0; i < WD0; ++i) { rg[i] = wg[i * 64]; rf[i] = wf[i * 64]; }
+  // stage [x(t-d)+dp; x(t)+dp; x(t+d)+dp; cond] as bf16 (zero outside each row's utterance).
+  // Thread tid always owns column group g = 4 (tid % 256) (so its tap/channel is fixed)
+  // and rows tid/256 + 2 it; all 16 loads are issued before any is used (clamped
+  // addresses, masked afterwards) instead of one branch-guarded round trip each.
+  constexpr int NGR = K1 / 4, IT = 32 * NGR / 512;
+  static_assert(NGR == 256 && IT == 16, "staging map assumes K1 = 1024");
+  const int g = (tid & (NGR - 1)) * 4, r0 = tid / NGR;
+  const bool isx = g < 3 * C;
+  const int tap = g / C, c = isx ? g - tap * C : g - 3 * C, sh = (tap - 1) * P.dil;
+  float4 sv[IT], dv[IT];
+  float ok[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int R = R0 + r0 + 2 * it;
+    const int Rc = R < rows ? R : rows - 1;
+    const int b = Rc / P.T, t = Rc - b * P.T, tt = isx ? t + sh : t;
+    const bool v = R < rows && tt >= 0 && tt < P.T;
+    const int ttc = tt < 0 ? 0 : tt >= P.T ? P.T - 1 : tt;
+    ok[it] = v ? 1.f : 0.f;
+    const float* src = isx ? P.xin + ((long long)b * P.T + ttc) * C + c : P.cond + ((long long)b * P.T + ttc) * H + c;
+    sv[it] = *reinterpret_cast<const float4*>(src);
+    dv[it] = isx ? *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const float m = ok[it];
+    const float4 v = sv[it], d = dv[it];
+    *reinterpret_cast<bf16x4*>(&As[(r0 + 2 * it) * LDA + g]) =
+        bf16x4{(__bf16)((v.x + d.x) * m), (__bf16)((v.y + d.y) * m), (__bf16)((v.z + d.z) * m),
+               (__bf16)((v.w + d.w) * m)};
+  }
+#pragma unroll
+  for (int i = WD0; i < WD; ++i) { rg[i] = wg[i * 64]; rf[i] = wf[i * 64]; }
+  __syncthreads();
   f32x16 ag, af;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { ag[r] = 0.f; af[r] = 0.f; }
-#pragma unroll 8
+  bf16x8 r2a[WD2], r2b[WD2];
+#pragma unroll
   for (int ks = 0; ks < KS1; ++ks) {
     const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[r32 * LDA + ks * 16 + h * 8]);
-    const bf16x8 bgt = wg[ks * 64], bft = wf[ks * 64];
+    const bf16x8 bgt = rg[ks % WD], bft = rf[ks % WD];
+    if (ks + WD < KS1) {
+      rg[ks % WD] = wg[(ks + WD) * 64];
+      rf[ks % WD] = wf[(ks + WD) * 64];
+    } else if (ks + WD - KS1 < WD2) {   // the tail of GEMM1 starts GEMM2's ring
+      r2a[ks + WD - KS1] = wr[(ks + WD - KS1) * 64];
+      r2b[ks + WD - KS1] = wsk[(ks + WD - KS1) * 64];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch where it is (the scheduler sinks loads to their use)
     ag = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bgt, ag, 0, 0, 0);
     af = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bft, af, 0, 0, 0);
   }
@@ -119,25 +150,37 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int r = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      Gs[r * LDG + n] = (__bf16)(sigmoidf_(ag[reg] + bgv) * tanhf_(af[reg] + bfv));
+      Gs[r * LDG + n] = (__bf16)gate_fast(ag[reg] + bgv, af[reg] + bfv);
     }
   }
   __syncthreads();
 
-  // GEMM2: residual tile nt = wave, skip tile nt = 8 + wave
-  constexpr int KS2 = C / 16;
-  const bf16x8* wr = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)wave * KS2 * 64 + lane;
-  const bf16x8* wsk = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)(8 + wave) * KS2 * 64 + lane;
+  // GEMM2: residual tile nt = wave, skip tile nt = 8 + wave.  The epilogue's x / skip
+  // reads are issued first so they land under the MFMAs.
+  const int n = wave * 32 + r32;
+  float xo[16], so[16];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int R = R0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    const long long o = (long long)(R < rows ? R : rows - 1) * C + n;
+    xo[reg] = P.xin[o];
+    so[reg] = P.first ? 0.f : P.skip[o];
+  }
   f32x16 ar, as_;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { ar[r] = 0.f; as_[r] = 0.f; }
 #pragma unroll
   for (int ks = 0; ks < KS2; ++ks) {
     const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Gs[r32 * LDG + ks * 16 + h * 8]);
-    ar = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, wr[ks * 64], ar, 0, 0, 0);
-    as_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, wsk[ks * 64], as_, 0, 0, 0);
+    const bf16x8 b0 = r2a[ks % WD2], b1 = r2b[ks % WD2];
+    if (ks + WD2 < KS2) {
+      r2a[ks % WD2] = wr[(ks + WD2) * 64];
+      r2b[ks % WD2] = wsk[(ks + WD2) * 64];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    ar = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0, ar, 0, 0, 0);
+    as_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b1, as_, 0, 0, 0);
   }
-  const int n = wave * 32 + r32;
   const float brv = P.b2[n], bsv = P.b2[C + n];
   const float rs2 = 0.70710678118654752440f;
 #pragma unroll
@@ -145,8 +188,8 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
     const int R = R0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
     if (R < rows) {
       const long long o = (long long)R * C + n;      // rows are b*T + t: contiguous [B][T][C]
-      P.xout[o] = (P.xin[o] + ar[reg] + brv) * rs2;
-      P.skip[o] = (P.first ? 0.f : P.skip[o]) + as_[reg] + bsv;
+      P.xout[o] = (xo[reg] + ar[reg] + brv) * rs2;
+      P.skip[o] = so[reg] + as_[reg] + bsv;
     }
   }
 }
@@ -339,7 +382,7 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
       PD_HIP(hipMalloc(&h->pool_bf, off * sizeof(__bf16)));
       PD_TRY(convert_f32_bf16(h->pool, h->pool_bf, (long long)off, st));
       register_bf16_pool(h->pool, off, h->pool_bf);
-      if (C == WNF_C && H % 32 == 0 && 3 * C + H <= 1024) {
+      if (C == WNF_C && 3 * C + H == 1024) {   // H == 256: the fused kernel is built for K1 = 1024
         const int K1 = 3 * C + H;
         const size_t per = (size_t)2 * C * K1 + (size_t)2 * C * C;
         PD_HIP(hipMalloc(&h->frag, (size_t)L * per * sizeof(__bf16)));
@@ -444,6 +487,138 @@ int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1
     PD_TRY((launch_gemm<1, 2, 4, 1, EPI_POSTERIOR, U_WN_POSTERIOR>(a, st, "wn_outproj_posterior")));
   }
   return PD_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ rectified flow
+namespace {
+// Explicit Runge-Kutta tableaus of RectifiedFlow.sample_{euler,rk2,rk4,rk5} (reflow.py:48-84):
+// stage j evaluates v(x + dt sum_l a[j][l] k_l, t + c[j] dt);  x += dt sum_j b[j] k_j.
+struct RkTableau {
+  int s;
+  double c[6];
+  double a[6][6];
+  double b[6];
+};
+bool reflow_tableau(int algo, RkTableau& T) {
+  T = RkTableau{};
+  switch (algo) {
+    case PD_REFLOW_EULER:
+      T.s = 1; T.b[0] = 1.0;
+      return true;
+    case PD_REFLOW_RK2:
+      T.s = 2; T.c[1] = 0.5; T.a[1][0] = 0.5; T.b[1] = 1.0;
+      return true;
+    case PD_REFLOW_RK4:
+      T.s = 4; T.c[1] = 0.5; T.c[2] = 0.5; T.c[3] = 1.0;
+      T.a[1][0] = 0.5; T.a[2][1] = 0.5; T.a[3][2] = 1.0;
+      T.b[0] = 1.0 / 6; T.b[1] = 2.0 / 6; T.b[2] = 2.0 / 6; T.b[3] = 1.0 / 6;
+      return true;
+    case PD_REFLOW_RK5:
+      T.s = 6; T.c[1] = 0.25; T.c[2] = 0.25; T.c[3] = 0.5; T.c[4] = 0.75; T.c[5] = 1.0;
+      T.a[1][0] = 0.25;
+      T.a[2][0] = 0.125; T.a[2][1] = 0.125;
+      T.a[3][1] = -0.5; T.a[3][2] = 1.0;
+      T.a[4][0] = 0.0625 * 3; T.a[4][3] = 0.0625 * 9;
+      T.a[5][0] = -3.0 / 7; T.a[5][1] = 2.0 / 7; T.a[5][2] = 12.0 / 7; T.a[5][3] = -12.0 / 7; T.a[5][4] = 8.0 / 7;
+      T.b[0] = 7.0 / 90; T.b[2] = 32.0 / 90; T.b[3] = 12.0 / 90; T.b[4] = 32.0 / 90; T.b[5] = 7.0 / 90;
+      return true;
+    default:
+      return false;
+  }
+}
+size_t reflow_kfloats(const pd_wavenet* h, int B, int T) { return ((size_t)B * T * h->M + 63) / 64 * 64; }
+}  // namespace
+
+extern "C" {
+
+size_t pd_reflow_workspace_size(const pd_wavenet* h, int B, int T, int S, int algo) {
+  RkTableau tb;
+  if (!h || B < 1 || T < 1 || S < 1 || !reflow_tableau(algo, tb) || S * tb.s > PD_MAX_STEP_VALS) return 0;
+  return ws_layout(h, B, T, S * tb.s).total + (size_t)(tb.s + 1) * reflow_kfloats(h, B, T) * sizeof(float);
+}
+
+int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, float time_scale,
+                     const float* x_T, unsigned long long seed, float* x, int B, int T, void* workspace,
+                     size_t ws_bytes, void* stream) {
+  PD_CHECK_ARG(h && cond && x && workspace, "null pointer");
+  RkTableau tb;
+  PD_CHECK_ARG(reflow_tableau(algo, tb), "algorithm must be PD_REFLOW_EULER/RK2/RK4/RK5");
+  PD_CHECK_ARG(B > 0 && T > 0 && S >= 1 && S * tb.s <= PD_MAX_STEP_VALS, "bad B/T/S (S * stages <= 128)");
+  if (ws_bytes < pd_reflow_workspace_size(h, B, T, S, algo)) { set_error("workspace too small"); return PD_ERR_WORKSPACE; }
+  const int nst = S * tb.s;
+  WsLayout Lw = ws_layout(h, B, T, nst);
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  const int M = h->M, C = h->C, Ly = h->L;
+  const long long BTM = (long long)B * T * M, BTs = T;
+  float* kb = ws + Lw.total / sizeof(float);
+  const size_t kstride = reflow_kfloats(h, B, T);
+  float* xs = kb + (size_t)tb.s * kstride;
+  // x ~ N(0,1) (reflow.py:88); the state lives in `x`, time-major [B][T][M]
+  if (x_T) {
+    PD_HIP(hipMemcpyAsync(x, x_T, sizeof(float) * BTM, hipMemcpyDeviceToDevice, st));
+  } else {
+    PD_TRY(fill_normal(x, BTM, seed, 0xFFFF0002u, st));
+  }
+  // every evaluation's step value, float32 as the reference forms it (reflow.py:89-98):
+  // t = i * float32(dt), a stage at t + float32(c dt), then time_scale * (.)
+  const double dt = 1.0 / (S > 1 ? S : 1);
+  const float dts = (float)dt;
+  std::vector<float> tv(nst);
+  for (int i = 0; i < S; ++i) {
+    const float t = (float)i * dts;
+    for (int j = 0; j < tb.s; ++j) tv[i * tb.s + j] = time_scale * (j == 0 ? t : t + (float)(tb.c[j] * dt));
+  }
+  PD_TRY(fill_steps(ws + Lw.steps, tv.data(), nst, B, st));
+  PD_TRY(step_mlp(h, ws, Lw, nst * B, st));
+  for (int i = 0; i < S; ++i) {
+    for (int j = 0; j < tb.s; ++j) {
+      const float* xin = x;
+      if (j > 0) {   // stage input x + dt sum_l a[j][l] k_l
+        AxpyTerms terms{};
+        for (int l = 0; l < j; ++l)
+          if (tb.a[j][l] != 0.0) {
+            terms.k[terms.n] = kb + (size_t)l * kstride;
+            terms.c[terms.n] = (float)(tb.a[j][l] * dt);
+            ++terms.n;
+          }
+        PD_TRY(axpy_multi(xs, x, terms, BTM, st));
+        xin = xs;
+      }
+      const int e = i * tb.s + j;
+      PD_TRY(wavenet_core(h, ws, Lw, xin, cond, ws + Lw.dproj + (size_t)e * B * Ly * C, B, T, st));
+      GemmArgs a = make_gemm(B, T, M, h->Wo, C, h->bo, tb.s == 1 ? x : kb + (size_t)j * kstride, BTs * M, M);
+      add_seg(a, make_seg(ws + Lw.hs, BTs * C, C, C, 0));
+      if (tb.s == 1) {   // Euler: x += v dt fused into the output projection (reflow.py:50)
+        a.res = x; a.res_bs = BTs * M; a.res_ld = M;
+        a.c1 = dts; a.c2 = 1.f; a.sigma = 0.f;
+        PD_TRY((launch_gemm<1, 2, 4, 1, EPI_POSTERIOR, U_WN_POSTERIOR>(a, st, "wn_outproj_posterior")));
+      } else {
+        PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_WN_OUT>(a, st, "wn_outproj")));
+      }
+    }
+    if (tb.s > 1) {      // x += dt sum_j b[j] k_j
+      AxpyTerms terms{};
+      for (int j = 0; j < tb.s; ++j)
+        if (tb.b[j] != 0.0) {
+          terms.k[terms.n] = kb + (size_t)j * kstride;
+          terms.c[terms.n] = (float)(tb.b[j] * dt);
+          ++terms.n;
+        }
+      PD_TRY(axpy_multi(x, x, terms, BTM, st));
+    }
+  }
+  return PD_OK;
+}
+
+int pd_reflow_denorm(const float* x, const float* spec_min, const float* spec_max, int nspec, int M, int rows,
+                     int mean_clamp, float clamp_min, float clamp_max, float* out, void* stream) {
+  PD_CHECK_ARG(x && spec_min && spec_max && out, "null pointer");
+  PD_CHECK_ARG(M > 0 && rows >= 0 && (nspec == 1 || nspec == M), "nspec must be 1 or M");
+  return reflow_denorm(x, spec_min, spec_max, nspec, M, rows, mean_clamp, clamp_min, clamp_max, out,
+                       (hipStream_t)stream);
 }
 
 }  // extern "C"

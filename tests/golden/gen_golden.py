@@ -270,8 +270,59 @@ def gen_fastdiff():
              wav=wav)
 
 
+# --------------------------------------------------------------------------
+# Rectified flow (reflow.py:5-144): the teacher's "reflow" sampler and the pitch
+# predictor's PitchRectifiedFlow, every algorithm; x_T = the torch.randn at :88.
+# --------------------------------------------------------------------------
+REFLOW_CASES = {
+    # name: (kind, M, cycle, algorithm, infer_step, B, T, seed)
+    "reflow_euler_m80": ("mel", 80, 1, "euler", 4, 2, 24, 51),
+    "reflow_rk2_m128": ("mel", 128, 1, "rk2", 3, 1, 19, 52),
+    "reflow_rk4_m80": ("mel", 80, 1, "rk4", 2, 2, 17, 53),
+    "reflow_rk5_m80": ("mel", 80, 1, "rk5", 2, 1, 21, 54),
+    "pitch_reflow_rk2_r64": ("pitch", 64, 5, "rk2", 3, 2, 30, 55),
+}
+
+
+def gen_reflow():
+    from modules.diffusion.reflow import PitchRectifiedFlow, RectifiedFlow
+    for name, (kind, M, cyc, algo, S, B, T, seed) in REFLOW_CASES.items():
+        H, L, C = 256, 20, 256
+        net = WaveNet(M, H, L, C, cyc)
+        if kind == "mel":
+            rf = RectifiedFlow(out_dims=M, denoise_fn=net, time_scale=1000, num_features=1,
+                               sampling_algorithm=algo, spec_min=[-12], spec_max=[0]).eval()
+        else:
+            rf = PitchRectifiedFlow(repeat_bins=M, denoise_fn=net, time_scale=1000, sampling_algorithm=algo,
+                                    spec_min=-8.0, spec_max=8.0, clamp_min=-12.0, clamp_max=12.0).eval()
+        load_synth(net, synth.wavenet_param_shapes(M, H, L, C), seed)
+        cond = synth.synth_inputs(seed + 400, (B, T, H))
+        x_T = synth.synth_inputs(seed + 500, (B, 1, M, T))
+        seen = []
+        orig = torch.randn
+
+        def randn(*size, device=None, **kw):
+            seen.append(tuple(size))
+            return torch.from_numpy(x_T.copy())
+
+        torch.randn = randn
+        try:
+            with torch.no_grad():
+                out = rf(torch.from_numpy(cond), infer_step=S, infer=True).numpy()
+                x = rf.inference(torch.from_numpy(cond).transpose(1, 2), b=B, infer_step=S).numpy()
+        finally:
+            torch.randn = orig
+        assert seen[0] == (B, 1, M, T), seen
+        save(name, kind=np.array(kind), dims=np.array([M, H, L, C, cyc]), seed=seed, algo=np.array(algo),
+             infer_step=S, cond=cond, x_T=x_T, x=x, out=out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:          # e.g. `gen_golden.py reflow` regenerates one family
+        globals()["gen_" + sys.argv[1]]()
+        sys.exit(0)
     gen_schedules()
     gen_wavenet()
     gen_prodiff()
     gen_fastdiff()
+    gen_reflow()

@@ -138,3 +138,17 @@ def test_fastdiff_sample_bf16_oracle(monkeypatch, fuse, ts, B, Tc):
     wav = m.sample(tt(mel), b, a, s, st, x_T=tt(xT), noise=tt(nz)).cpu().numpy()
     ref = OF.fastdiff_sample(OF.fold_weight_norm(p), np.transpose(mel, (0, 2, 1)), xT, nz, b, a, s, st)
     assert_bf16_close(wav.reshape(ref.shape), ref)
+
+
+def test_reflow_euler_bf16():
+    """bf16 velocity field over the teacher's 20 Euler steps, against the fp64 oracle."""
+    from oracle import oracle_reflow as OR
+    from prodiff_amd import RectifiedFlow
+    p = synth.synth_params(synth.wavenet_param_shapes(80, 256, 20, 256), 71)
+    net = WaveNet(80, 256, 20, 256, 1)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+    rf = RectifiedFlow(80, net.to(DEV).set_compute_dtype("bf16"), spec_min=[-12], spec_max=[0]).to(DEV)
+    cond = synth.synth_inputs(72, (2, 37, 256))
+    xT = synth.synth_inputs(73, (2, 1, 80, 37))
+    x = rf.sample(tt(cond), infer_step=20, x_T=tt(xT)).cpu().numpy()
+    assert_bf16_close(x, OR.reflow_sample(p, cond, xT, 20, "euler", 1000, 20, 1))

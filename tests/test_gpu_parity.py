@@ -192,3 +192,53 @@ def test_onchip_rng_moments(fdnet):
     mel = gd.sample(tt(np.zeros((4, 4096, 32), np.float32)), seed=1234)
     x = mel.cpu().numpy()
     assert abs(x.mean() - 0.5) < 0.01 and abs(x.var() - 1 / 12) < 0.01 and x.min() >= 0 and x.max() < 1
+
+
+# ------------------------------------------------------------------ rectified flow
+REFLOW = ["reflow_euler_m80", "reflow_rk2_m128", "reflow_rk4_m80", "reflow_rk5_m80", "pitch_reflow_rk2_r64"]
+
+
+def reflow_from(d):
+    from prodiff_amd import PitchRectifiedFlow, RectifiedFlow
+    M, H, L, C, cyc = [int(v) for v in d["dims"]]
+    net = wavenet_from(d["dims"], G.wavenet_params(d["dims"], d["seed"]))
+    if str(d["kind"]) == "pitch":
+        return PitchRectifiedFlow(M, net, time_scale=1000, sampling_algorithm=str(d["algo"])).to(DEV)
+    return RectifiedFlow(M, net, time_scale=1000, sampling_algorithm=str(d["algo"]), spec_min=[-12],
+                         spec_max=[0]).to(DEV)
+
+
+@pytest.mark.parametrize("name", REFLOW)
+def test_reflow_golden(name):
+    """Euler / RK2 / RK4 / RK5 integration and denorm_spec against the reference's outputs."""
+    d = G.load(name)
+    rf = reflow_from(d)
+    x = rf.sample(tt(d["cond"]), infer_step=int(d["infer_step"]), x_T=tt(d["x_T"]))
+    assert_close(x.cpu().numpy(), d["x"])
+    assert_close(rf.denorm_spec(x).cpu().numpy(), d["out"])
+
+
+@pytest.mark.parametrize("B,T,S", [(3, 33, 20), (1, 1, 5)])
+def test_reflow_euler_oracle_shapes(B, T, S):
+    """The teacher's default (20 Euler steps) on ragged shapes against the oracle."""
+    from oracle import oracle_reflow as OR
+    from prodiff_amd import RectifiedFlow
+    p = synth.synth_params(synth.wavenet_param_shapes(80, 256, 20, 256), 61)
+    rf = RectifiedFlow(80, wavenet_from((80, 256, 20, 256, 1), p), spec_min=[-12], spec_max=[0]).to(DEV)
+    cond = synth.synth_inputs(62, (B, T, 256))
+    xT = synth.synth_inputs(63, (B, 1, 80, T))
+    x = rf.sample(tt(cond), infer_step=S, x_T=tt(xT)).cpu().numpy()
+    assert_close(x, OR.reflow_sample(p, cond, xT, S, "euler", 1000, 20, 1))
+
+
+def test_reflow_forward_api():
+    """forward(cond, infer=True) -- the teacher's call (prodiff_teacher.py:167) -- Philox draws."""
+    from prodiff_amd import RectifiedFlow
+    p = synth.synth_params(synth.wavenet_param_shapes(80, 256, 20, 256), 64)
+    rf = RectifiedFlow(80, wavenet_from((80, 256, 20, 256, 1), p), spec_min=[-12], spec_max=[0]).to(DEV)
+    cond = tt(synth.synth_inputs(65, (2, 40, 256)))
+    torch.manual_seed(0)
+    a = rf(cond, infer=True)
+    torch.manual_seed(0)
+    b = rf(cond, infer=True)
+    assert a.shape == (2, 40, 80) and torch.isfinite(a).all() and torch.equal(a, b)

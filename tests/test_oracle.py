@@ -97,3 +97,22 @@ def test_fastdiff_sample_oracle(n_iter):
     np.testing.assert_allclose(st[::-1], d["steps_seen"], atol=1e-4)
     wav = OF.fastdiff_sample(p, d["c"], d["x_T"], d["noise"], b, a, sg, st)
     assert np.abs(wav - d["wav"]).max() < 1e-4
+
+
+REFLOW = ["reflow_euler_m80", "reflow_rk2_m128", "reflow_rk4_m80", "reflow_rk5_m80", "pitch_reflow_rk2_r64"]
+
+
+@pytest.mark.parametrize("name", REFLOW)
+def test_reflow_oracle(name):
+    from oracle import oracle_reflow as OR
+    d = G.load(name)
+    p = G.wavenet_params(d["dims"], d["seed"])
+    L, cyc = int(d["dims"][2]), int(d["dims"][4])
+    x = OR.reflow_sample(p, d["cond"], d["x_T"], int(d["infer_step"]), str(d["algo"]), 1000, L, cyc)
+    assert x.shape == d["x"].shape
+    assert np.abs(x - d["x"]).max() < 2e-5
+    if str(d["kind"]) == "pitch":
+        out = OR.pitch_denorm(x, -8.0, 8.0, -12.0, 12.0)
+    else:
+        out = OR.denorm_spec(x, [-12.0], [0.0])
+    assert np.abs(out - d["out"]).max() < 2e-5
