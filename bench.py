@@ -109,10 +109,10 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
     }
 
 
-# bench tag -> kernel symbol (TS = 128 defaults) for the PMC traffic lookup
+# bench tag -> kernel symbol (the default tile sizes) for the PMC traffic lookup
 TAG_KERNEL = {
-    "fd_lvc_block_final": "lvc_block_bf16_kernel<128, true, true, true, false, false>",
-    "fd_lvc_block_ups": "lvc_block_bf16_kernel<128, true, false, false, false, false>",
+    "fd_lvc_block_final": "lvc_block_bf16_kernel<384, true, true, true, true, false>",
+    "fd_lvc_block_ups": "lvc_block_bf16_kernel<384, true, false, false, true, false>",
     "fd_lvc_block_sub": "lvc_block_bf16_kernel<128, true, false, false, false, true>",
     "fd_kp_kernel": "kp_kernel_bf16_kernel",
     "wn_layer": "wn_layer_bf16_kernel",

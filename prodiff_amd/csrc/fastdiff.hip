@@ -51,9 +51,14 @@ struct fd_model {
   int ratios[4];
   int hops[4];
   int dtype;
-  int lvc_ts = 128;            // whole-block LVC tile (128/256); 0 = one fused launch per layer (PRODIFF_LVC_TS)
+  // Whole-block LVC tile per block kind (measured, r01_ab4): 384 output samples with the
+  // next-layer kernel prefetch (8 waves, 1 block/CU, 256 VGPRs) for hop >= 32; 128 for the
+  // hop-8 block, whose tiles span several frames (no prefetch).  lvc_ts = 0 selects one
+  // fused launch per layer (PRODIFF_LVC_TS, PRODIFF_LVC_TS_SUB, PRODIFF_LVC_PF).
+  int lvc_ts = 384;
+  int lvc_ts_sub = 128;
   bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (PRODIFF_LVC_FUSE)
-  bool lvc_pf = false;         // next-layer kernel fragments prefetched into registers (PRODIFF_LVC_PF)
+  bool lvc_pf = true;          // next-layer kernel fragments prefetched into registers (PRODIFF_LVC_PF)
   bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (PRODIFF_LVC_SUB)
   float* pool = nullptr;
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
@@ -1499,8 +1504,11 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       {
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : hop < 32 ? "fd_lvc_block_sub" : ups ? "fd_lvc_block_ups"
                                                                                    : "fd_lvc_block", st);
-        if (m->lvc_ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, m->lvc_pf, Tout, B, st));
-        else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, m->lvc_pf, Tout, B, st));
+        const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
+        const bool pf = m->lvc_pf && hop >= 32;
+        if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
+        else if (ts == 384) PD_TRY(launch_lvc_block_ts<384>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
+        else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
       }
       if (fuse_fin) { *xout = nullptr; return PD_OK; }
       x = la.xout;
@@ -1586,7 +1594,11 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   fd_model* m = new fd_model();
   m->nblocks = dims->num_blocks;
   m->dtype = dtype;
-  if (const char* e = getenv("PRODIFF_LVC_TS")) m->lvc_ts = atoi(e);   // A/B switch (bench/tests)
+  if (const char* e = getenv("PRODIFF_LVC_TS")) {   // A/B switches (bench/tests)
+    m->lvc_ts = atoi(e);
+    m->lvc_pf = m->lvc_ts >= 384;
+  }
+  if (const char* e = getenv("PRODIFF_LVC_TS_SUB")) m->lvc_ts_sub = atoi(e);
   if (const char* e = getenv("PRODIFF_LVC_FUSE")) m->lvc_fuse = atoi(e) != 0;
   if (const char* e = getenv("PRODIFF_LVC_PF")) m->lvc_pf = atoi(e) != 0;
   if (const char* e = getenv("PRODIFF_LVC_SUB")) m->lvc_sub = atoi(e) != 0;

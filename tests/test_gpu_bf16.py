@@ -97,7 +97,7 @@ def test_fastdiff_sample_bf16(fd16):
     assert_bf16_close(wav, d["wav"])
 
 
-@pytest.mark.parametrize("ts", [0, 128, 256])
+@pytest.mark.parametrize("ts", [0, 128, 256, 384])
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
 def test_fastdiff_lvc_block_bf16(monkeypatch, ts, B, Tc):
     """LVC modes (PRODIFF_LVC_TS: 0 = one fused launch per layer, 128/256 = whole block) against the
@@ -115,7 +115,7 @@ def test_fastdiff_lvc_block_bf16(monkeypatch, ts, B, Tc):
 
 
 @pytest.mark.parametrize("fuse", [0, 1])
-@pytest.mark.parametrize("ts", [128, 256])
+@pytest.mark.parametrize("ts", [128, 256, 384])
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
 def test_fastdiff_sample_bf16_oracle(monkeypatch, fuse, ts, B, Tc):
     """The 4-step sampler with the upsample / first conv / final update fused into the LVC
