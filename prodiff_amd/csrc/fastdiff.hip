@@ -60,6 +60,14 @@ struct fd_model {
   bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (PRODIFF_LVC_FUSE)
   bool lvc_pf = true;          // next-layer kernel fragments prefetched into registers (PRODIFF_LVC_PF)
   bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (PRODIFF_LVC_SUB)
+  // fd_sample (bf16): the kernel-predictor GEMMs run on a second, low-priority stream into a
+  // ring of one K buffer per block, so step j+1's kernels for block n are written while
+  // step j's later blocks run (PRODIFF_KP_SIDE=1).  Created on first use.  Off by default:
+  // the two streams share the CUs, so each kernel slows down by about the time the overlap
+  // saves (r01 ab_v16b: 7.41 vs 7.33 ms/step).
+  bool kp_side = false;
+  mutable hipStream_t side = nullptr;
+  mutable hipEvent_t ev_hidden = nullptr, ev_kp[4] = {}, ev_lvc[4] = {};
   float* pool = nullptr;
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
   // step MLP
@@ -355,7 +363,7 @@ struct LvcBlockArgs {
 #define LB_STAMP(i)                                                                       \
   do {                                                                                    \
     if (lane == 0 && blockIdx.x % 61 == 0)                                                \
-      P.trace[((blockIdx.y * gridDim.x + blockIdx.x) / 61 * NW + wave) * 16 + (i)] =      \
+      P.trace[((blockIdx.y * gridDim.x + blockIdx.x) / 61 * NW + wave) * 24 + (i)] =      \
           __builtin_readcyclecounter();                                                   \
   } while (0)
 #else
@@ -383,8 +391,10 @@ template <int TS> struct LbGeo {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float LOG2E = 1.4426950408889634f;
 __device__ __forceinline__ f32x2 lrelu2(f32x2 v) {
+  // max(v, 0.2 v) as med3(v, 0.2 v, +inf): v_max_f32 would first canonicalize operands
+  // the compiler cannot prove canonical (a register state fed from memory)
   const f32x2 s = v * 0.2f;
-  return f32x2{fmaxf(v.x, s.x), fmaxf(v.y, s.y)};
+  return __builtin_elementwise_maximum(v, s);
 }
 // sigmoid(g) tanh(f) from gs = -log2e (g + b_g), fs = 2 log2e (f + b_f): gate_fast, paired
 __device__ __forceinline__ f32x2 gate2s(f32x2 gs, f32x2 fs) {
@@ -408,6 +418,17 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
   __shared__ float AS[AUD ? GR + 6 : 1];             // audio at times [tg - 3, tg + GR + 3)
   __shared__ __attribute__((aligned(16))) float FW[AUD ? 7 * 32 : 4];   // first conv [tap][c]
   __shared__ __attribute__((aligned(16))) float FWF[FIN ? 7 * 32 : 4];  // final conv [tap][c]
+  __shared__ __attribute__((aligned(16))) float FBL[AUD ? 32 : 4];       // first conv bias
+  __shared__ __attribute__((aligned(16))) float BUL[UPS ? 32 : 4];       // upsample bias
+  // PF: the pre-conv weights (fragment order), their biases and the LVC biases of the
+  // block's frames (pre-scaled for the gate) live in LDS, so no global load but the
+  // next layer's kernel prefetch is in flight across a layer (vmcnt retires in order:
+  // a global weight load behind the prefetch would wait for the whole prefetch).
+  constexpr bool WL = PF;
+  constexpr int BFR = WL ? GR / 32 + 2 : 1;          // frames a block touches at hop >= 32
+  __shared__ __attribute__((aligned(16))) bf16x8 WCL[WL ? NLY * 6 * 64 : 1];
+  __shared__ __attribute__((aligned(16))) float BCL[WL ? NLY * CI : 4];
+  __shared__ __attribute__((aligned(16))) float BFL[WL ? BFR * 2 * CI * NLY : 4];
   __bf16* U = reinterpret_cast<__bf16*>(smem);
   __bf16* Y = U + G::UROWS * LB_LD;
   float* XS = reinterpret_cast<float*>(smem);                       // aliases U/Y outside the layers
@@ -424,78 +445,229 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
     b = logical / gridDim.x;
     bx = logical - b * gridDim.x;
   }
+  // Tiles of wave w: PF -- the adjacent pair 2w, 2w + 1 (one frame, one shared kernel);
+  // otherwise w and w + NW (better balanced over the shrinking per-layer tile ranges).
+#define TILE(j) (PF ? 2 * wave + (j) : wave + (j) * NW)
   const int Tc = P.Tc, hop = P.hop;
   const int Lh = Tc * hop;                           // utterance-local times fit in 32 bits
   const int t0 = bx * TS, tg = t0 - 64;              // time of grid row 0
   const long long base = (long long)b * Lh;
   constexpr int RLO = 64 - 44 - EX, RHI = 64 + TS + 44 + EX;   // x rows the valid region reads
   LB_STAMP(0);
+  // Prologue: every global load of the block -- the LDS-staged operands, x_prev, the
+  // phase-GEMM weights and (last, PF) layer 0's kernel fragments -- is issued before the
+  // first use, so the block pays about one memory round trip before its first layer
+  // (vmcnt retires in order: the prefetch stays in flight while the staging drains).
+  const int fbase = (tg > 0 ? tg : 0) / hop;         // first frame of the block (WL)
+  constexpr int IT = AUD ? (GR + 6 + G::NT - 1) / G::NT : 1;
+  float av[IT], fwv = 0.f, fbv = 0.f, bupv = 0.f, wfv = 0.f;
   if constexpr (AUD) {
-    for (int i = tid; i < GR + 6; i += G::NT) {
-      const int t = tg - 3 + i;
-      AS[i] = (t >= 0 && t < Lh) ? P.audio[base + t] : 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      // unconditional loads at clamped addresses, masked at the LDS store: a load under a
+      // branch makes the compiler wait for it at the branch join
+      const int t = tg - 3 + tid + it * G::NT;
+      av[it] = P.audio[base + min(max(t, 0), Lh - 1)];
     }
+    if (tid < 224) fwv = P.fw[(tid & 31) * 7 + (tid >> 5)];   // fw is [c][tap]
+    if (tid < 32) fbv = P.fb[tid];
   }
-  if constexpr (AUD) {
-    for (int i = tid; i < 224; i += G::NT) FW[i] = P.fw[(i & 31) * 7 + (i >> 5)];   // fw is [c][tap]
+  if constexpr (UPS) {
+    if (tid < 32) bupv = P.bup[tid];
   }
   if constexpr (FIN) {
-    for (int i = tid; i < 224; i += G::NT) FWF[i] = P.wfin[i];                     // already [tap][c]
+    if (tid < 224) wfv = P.wfin[tid];                        // already [tap][c]
   }
-  // ---- prologue: x rows (upsampled in-kernel, or loaded) -> registers
+  constexpr int IW = WL ? (6 * 64 + G::NT - 1) / G::NT : 1;
+  constexpr int N4 = BFR * 2 * CI * NLY / 4, IB = WL ? (N4 + G::NT - 1) / G::NT : 1;
+  bf16x4 wv[IW][NLY][2];
+  float bcv = 0.f;
+  float4 bfv[IB];
+  if constexpr (WL) {
+#pragma unroll
+    for (int it = 0; it < IW; ++it) {
+      const int i = min(tid + it * G::NT, 6 * 64 - 1), kk = i >> 6, ln = i & 63;
+#pragma unroll
+      for (int l = 0; l < NLY; ++l) {
+        const __bf16* w = P.Wc[l] + (ln & 31) * 96 + (kk >> 1) * 32 + 16 * (ln >> 5) + 4 * (kk & 1);
+        wv[it][l][0] = *reinterpret_cast<const bf16x4*>(w);
+        wv[it][l][1] = *reinterpret_cast<const bf16x4*>(w + 8);
+      }
+    }
+    if (tid < NLY * CI) {
+#pragma unroll
+      for (int l = 0; l < NLY; ++l)
+        if (tid / CI == l) bcv = P.bc[l][tid % CI];
+    }
+#pragma unroll
+    for (int it = 0; it < IB; ++it) {
+      const int i = min(tid + it * G::NT, N4 - 1), fr = min(fbase + i / (2 * CI * NLY / 4), Tc - 1);
+      const int c = (i % (2 * CI * NLY / 4)) * 4;
+      bfv[it] = *reinterpret_cast<const float4*>(P.Bf + ((long long)b * Tc + fr) * (2 * CI * NLY) + c);
+    }
+  }
+  // UPS: x_prev rows and this wave's first chunk of phase-GEMM weight fragments
+  const int r = UPS ? P.r : 1, pp = UPS ? P.p : 0, Tin = Lh / r;
+  const int ntj = (GR / r + 2 + 31) / 32;
+  const int jb = floordiv(tg + pp, r) - 2;           // column j0 = jb + 1 + c, c < 32 ntj
+  constexpr int IX = UPS ? ((G::NTJ_MAX * 32 + 1) * 8 + G::NT - 1) / G::NT : 1;
+  float4 xv4[IX];
+  // NW % r == 0: wave w computes phase w % r on columns w / r, w / r + NW / r, ... and
+  // loads that phase's weights once; otherwise jobs run in chunks of 4 (wfj[q]).
+  const bool by_phase = NW % r == 0 && ntj <= 4 * (NW / r);
+  bf16x8 wfj[4][4];
+  auto wup_load = [&](int job0) {
+    if (by_phase) {
+      const __bf16* wa = P.Wup + ((long long)(wave % r) * 32 + n) * 64 + 8 * h;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wfj[0][kk] = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int job = job0 + q * NW, k = job / ntj;
+      if (job < r * ntj) {
+        const __bf16* wa = P.Wup + ((long long)k * 32 + n) * 64 + 8 * h;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) wfj[q][kk] = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
+      }
+    }
+  };
+  if constexpr (UPS) {
+    const float* xp = P.xin + (long long)b * Tin * CI;
+#pragma unroll
+    for (int it = 0; it < IX; ++it) {
+      const int i = tid + it * G::NT, q = (i & 7) * 4, j = min(max(jb + (i >> 3), 0), Tin - 1);
+      xv4[it] = *reinterpret_cast<const float4*>(xp + (long long)j * CI + q);
+    }
+    wup_load(wave);
+  }
+  // PF (hop % 64 == 0): a wave's two tiles are a 64-aligned pair, so they lie in one frame
+  // and share one 64x96 kernel.  Layer l's fragments are loaded into registers while layer
+  // l - 1 finishes (issued right after the pair's MFMAs), so their latency hides behind the
+  // gates, the staging and the pre-conv.  Loads are unconditional (frame clamped).
+  const int fpair = min(max(tg + 64 * wave + 32, 0) / hop, Tc - 1);
+  bf16x8 kn[12];
+  auto kload = [&](int l) {
+    const __bf16* kq = P.Kf[l] + ((long long)b * Tc + fpair) * KPERLAYER;
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk) kn[kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+  };
+  if constexpr (PF) kload(0);
+  // FIN: the sampler noise of this thread's output samples, drawn while the loads fly
+  constexpr int IF = FIN ? (2 * TS + G::NT - 1) / G::NT : 1;
+  float zr[IF];
+  const float bfin = FIN ? P.bfin[0] : 0.f;
+  if constexpr (FIN) {
+#pragma unroll
+    for (int it = 0; it < IF; ++it) {
+      const int s2 = tid + it * G::NT, t = t0 + (s2 >> 1);
+      zr[it] = 0.f;
+      if (s2 < 2 * TS && (s2 & 1) == 0 && t < Lh && P.sig != 0.f)
+        zr[it] = P.noise ? P.noise[base + t] : philox_normal(P.seed, (unsigned long long)(base + t), P.stream);
+    }
+  }
+  // ---- LDS stores of the staged operands
+  if constexpr (AUD) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = tid + it * G::NT;
+      const int t = tg - 3 + i;
+      if (i < GR + 6) AS[i] = (t >= 0 && t < Lh) ? av[it] : 0.f;
+    }
+    if (tid < 224) FW[tid] = fwv;
+    if (tid < 32) FBL[tid] = fbv;
+  }
+  if constexpr (UPS) {
+    if (tid < 32) BUL[tid] = bupv;
+  }
+  if constexpr (FIN) {
+    if (tid < 224) FWF[tid] = wfv;
+  }
+  if constexpr (WL) {
+#pragma unroll
+    for (int it = 0; it < IW; ++it) {
+      const int i = tid + it * G::NT;
+#pragma unroll
+      for (int l = 0; l < NLY; ++l) {
+        const bf16x4 w0 = wv[it][l][0], w1 = wv[it][l][1];
+        if (i < 6 * 64) WCL[l * 384 + i] = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+      }
+    }
+    if (tid < NLY * CI) BCL[tid] = bcv;
+#pragma unroll
+    for (int it = 0; it < IB; ++it) {
+      const int i = tid + it * G::NT, c = (i % (2 * CI * NLY / 4)) * 4;
+      // gate pre-scale; frames past the utterance end are never read (zero them anyway)
+      const float sc = fbase + i / (2 * CI * NLY / 4) >= Tc ? 0.f : (c & 63) < 32 ? -LOG2E : 2.f * LOG2E;
+      if (i < N4)
+        *reinterpret_cast<float4*>(&BFL[4 * i]) = make_float4(bfv[it].x * sc, bfv[it].y * sc, bfv[it].z * sc, bfv[it].w * sc);
+    }
+  }
+  LB_STAMP(16);
+  // ---- x rows (upsampled in-kernel, or loaded) -> registers
   f32x2 xr[2][8], ar[2][8];
   if constexpr (UPS) {
     // (a) XP[j - jb] = bf16 lrelu(x_prev[j]), j in [jb, jb + 32 ntj]: j0 - 1 .. j0 of every column
-    const int r = P.r, pp = P.p, Tin = Lh / r;
-    const int ntj = (GR / r + 2 + 31) / 32;
-    const int jb = floordiv(tg + pp, r) - 2;         // column j0 = jb + 1 + c, c < 32 ntj
-    const float* xp = P.xin + (long long)b * Tin * CI;
-    for (int i = tid; i < (ntj * 32 + 1) * 8; i += G::NT) {
-      const int rr = i >> 3, q = (i & 7) * 4, j = jb + rr;
-      bf16x4 v = {};
-      if (j >= 0 && j < Tin) {
-        const float4 f = *reinterpret_cast<const float4*>(xp + (long long)j * CI + q);
-        const f32x2 u0 = lrelu2(f32x2{f.x, f.y}), u1 = lrelu2(f32x2{f.z, f.w});
-        v = bf16x4{(__bf16)u0.x, (__bf16)u0.y, (__bf16)u1.x, (__bf16)u1.y};
+#pragma unroll
+    for (int it = 0; it < IX; ++it) {
+      const int i = tid + it * G::NT, rr = i >> 3, q = (i & 7) * 4, j = jb + rr;
+      if (i < (ntj * 32 + 1) * 8) {
+        // rows outside x_prev are zero (lrelu(0) = 0)
+        const float m = (j >= 0 && j < Tin) ? 1.f : 0.f;
+        const f32x2 u0 = lrelu2(f32x2{xv4[it].x, xv4[it].y} * m), u1 = lrelu2(f32x2{xv4[it].z, xv4[it].w} * m);
+        *reinterpret_cast<bf16x4*>(&XP[rr * LB_LD + q]) = bf16x4{(__bf16)u0.x, (__bf16)u0.y, (__bf16)u1.x, (__bf16)u1.y};
       }
-      *reinterpret_cast<bf16x4*>(&XP[rr * LB_LD + q]) = v;
     }
     __syncthreads();
+    LB_STAMP(17);
     // (b) phase GEMMs: C^T[co][col] = [W_k^T | W_{k+r}^T] . [xp(j0); xp(j0 - 1)], t = r j0 + k - p
-    for (int job = wave; job < r * ntj; job += NW) {
-      const int k = job / ntj, jt = job - k * ntj;
-      const __bf16* wa = P.Wup + ((long long)k * 32 + n) * 64 + 8 * h;
+    for (int job0 = wave; job0 < r * ntj; job0 += 4 * NW) {
+    if (job0 != wave && !by_phase) wup_load(job0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int k, jt;
+      if (by_phase) {
+        k = wave % r; jt = wave / r + q * (NW / r);
+        if (jt >= ntj) break;
+      } else {
+        const int job = job0 + q * NW;
+        if (job >= r * ntj) break;
+        k = job / ntj; jt = job - k * ntj;
+      }
       f32x16 acc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
         // k-step kk < 2: input j0 (XP row c + 1), kk >= 2: input j0 - 1 (XP row c)
         const bf16x8 xb = *reinterpret_cast<const bf16x8*>(
             &XP[(jt * 32 + n + (kk < 2 ? 1 : 0)) * LB_LD + 16 * (kk & 1) + 8 * h]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xb, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(by_phase ? wfj[0][kk] : wfj[q][kk], xb, acc, 0, 0, 0);
       }
       const int j0 = jb + 1 + jt * 32 + n, row = r * j0 + k - pp - tg;
       if (row >= RLO && row < RHI) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float4 bv = *reinterpret_cast<const float4*>(P.bup + 8 * g + 4 * h);
+          const float4 bv = *reinterpret_cast<const float4*>(&BUL[8 * g + 4 * h]);
           *reinterpret_cast<float4*>(&XS[row * LB_XLD + 8 * g + 4 * h]) =
               make_float4(acc[4 * g] + bv.x, acc[4 * g + 1] + bv.y, acc[4 * g + 2] + bv.z, acc[4 * g + 3] + bv.w);
         }
       }
     }
+    if (by_phase) break;
+    }
     __syncthreads();
   } else if constexpr (AUD) {
     __syncthreads();                                  // AS / FW visible
   }
+  LB_STAMP(18);
   // Transposed C layout: lane (n, h) of tile k holds time tg + 32k + n, channels
   // (reg&3) + 8(reg>>2) + 4h; pair p = regs (2p, 2p+1).  Four float4 loads per tensor
   // (channels 8i + 4h .. +3).
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int k = wave + j * NW, row = k * 32 + n, t = tg + row;
+    const int k = TILE(j), row = k * 32 + n, t = tg + row;
     const bool ok = row >= RLO && row < RHI && t >= 0 && t < Lh;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -507,7 +679,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
           // a0[t][c] = b[c] + sum_tap w[c][tap] audio[t + tap - 3], first_conv_kernel's order
           float a4[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) a4[e] = P.fb[8 * i + 4 * h + e];
+          for (int e = 0; e < 4; ++e) a4[e] = FBL[8 * i + 4 * h + e];
 #pragma unroll
           for (int tap = 0; tap < 7; ++tap) {
             const float s = AS[row + tap];
@@ -520,30 +692,18 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
           av = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + 8 * i + 4 * h);
         }
       }
-      xr[j][2 * i] = f32x2{xv.x, xv.y}; xr[j][2 * i + 1] = f32x2{xv.z, xv.w};
+      // registers hold z = x + a (the reference's `x += audio_down`, modules.py:209)
+      xr[j][2 * i] = f32x2{xv.x + av.x, xv.y + av.y}; xr[j][2 * i + 1] = f32x2{xv.z + av.z, xv.w + av.w};
       ar[j][2 * i] = f32x2{av.x, av.y}; ar[j][2 * i + 1] = f32x2{av.z, av.w};
     }
   }
+  LB_STAMP(19);
   if constexpr (UPS) __syncthreads();                // XS reads done before U/Y (aliased) are zeroed
   {
     const bf16x8 z = {};
     for (int i = tid; i < G::UY_BYTES / 16; i += G::NT) reinterpret_cast<bf16x8*>(smem)[i] = z;
   }
-  // PF: each tile's 64x96 kernel fragments for layer l are loaded into registers while
-  // layer l - 1 finishes (issued right after the tile's previous MFMAs), so their HBM
-  // latency hides behind the gate epilogue, the staging and the pre-conv.
-  bf16x8 kn[2][12];
-  auto kload = [&](int l, int j) {
-    const int e = (l == 0 ? 42 : l == 1 ? 38 : l == 2 ? 28 : 0) + EX;
-    const int kf = (64 - e) / 32, kl = (64 + TS + e - 1) / 32;
-    const int k = wave + j * NW, ts = tg + k * 32;
-    if (k >= kf && k <= kl && ts >= 0 && ts < Lh) {
-      const __bf16* kq = P.Kf[l] + ((long long)b * Tc + ts / hop) * KPERLAYER;
-#pragma unroll
-      for (int kk = 0; kk < 12; ++kk) kn[j][kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
-    }
-  };
-  if constexpr (PF) { kload(0, 0); kload(0, 1); }
+  LB_STAMP(20);
   __syncthreads();
   LB_STAMP(1);
 #pragma unroll
@@ -552,15 +712,15 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
     const int e = (l == 0 ? 42 : l == 1 ? 38 : l == 2 ? 28 : 0) + EX;
     const int kf = (64 - e) / 32, kl = (64 + TS + e - 1) / 32;   // LVC tiles of this layer
     const int kpl = kl + 1 < NG - 1 ? kl + 1 : NG - 1;           // last pre-conv tile
-    // (1) u = lrelu(x + a) of the owned tiles the pre-conv reads: 2 x 16 B per lane
+    // (1) u = lrelu(z) (z = x + a) of the owned tiles the pre-conv reads: 2 x 16 B per lane
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = wave + j * NW;
+      const int k = TILE(j);
       if (k >= kf - 1 && k <= kl + 2) {
         bf16x8 u0, u1;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          const f32x2 v0 = lrelu2(xr[j][p] + ar[j][p]), v1 = lrelu2(xr[j][4 + p] + ar[j][4 + p]);
+          const f32x2 v0 = lrelu2(xr[j][p]), v1 = lrelu2(xr[j][4 + p]);
           u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
           u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
         }
@@ -577,14 +737,18 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
       bf16x8 wf[6];
 #pragma unroll
       for (int kk = 0; kk < 6; ++kk) {
-        const __bf16* w = P.Wc[l] + n * 96 + (kk >> 1) * 32 + 16 * h + 4 * (kk & 1);
-        const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(w), w1 = *reinterpret_cast<const bf16x4*>(w + 8);
-        wf[kk] = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+        if constexpr (WL) {
+          wf[kk] = WCL[(l * 6 + kk) * 64 + lane];
+        } else {
+          const __bf16* w = P.Wc[l] + n * 96 + (kk >> 1) * 32 + 16 * h + 4 * (kk & 1);
+          const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(w), w1 = *reinterpret_cast<const bf16x4*>(w + 8);
+          wf[kk] = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+        }
       }
       f32x2 bias[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float4 bv = *reinterpret_cast<const float4*>(P.bc[l] + 8 * i + 4 * h);
+        const float4 bv = *reinterpret_cast<const float4*>((WL ? &BCL[l * CI] : P.bc[l]) + 8 * i + 4 * h);
         bias[2 * i] = f32x2{bv.x, bv.y}; bias[2 * i + 1] = f32x2{bv.z, bv.w};
       }
       for (int kp = kf + wave; kp <= kpl; kp += NW) {
@@ -622,9 +786,70 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
     __syncthreads();
     LB_STAMP(3 + 3 * l);
     // (3) o^T = K_frame . [y(t-1); y(t); y(t+1)]^T + Bf;  x += a + sigmoid(o_g) tanh(o_f)
+    // K is pre-scaled (gate rows by -log2 e, filter rows by 2 log2 e): the accumulators are
+    // the exp2 arguments.  z = x + a lives in registers: x_{l+1} = z_l + o, and
+    // z_{l+1} = x_{l+1} + a except after the last layer.
+    const f32x2 cg = {-LOG2E, -LOG2E}, cf = {2.f * LOG2E, 2.f * LOG2E};
+    auto gate_update = [&](int j, const f32x16& g, const f32x16& f, const float* bq, float live) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f32x2 gs0 = {g[4 * i], g[4 * i + 1]}, gs1 = {g[4 * i + 2], g[4 * i + 3]};
+        f32x2 fs0 = {f[4 * i], f[4 * i + 1]}, fs1 = {f[4 * i + 2], f[4 * i + 3]};
+        if (bq) {   // bias not folded into the accumulators yet
+          const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
+          const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
+          gs0 = __builtin_elementwise_fma(f32x2{bg.x, bg.y}, cg, gs0);
+          gs1 = __builtin_elementwise_fma(f32x2{bg.z, bg.w}, cg, gs1);
+          fs0 = __builtin_elementwise_fma(f32x2{bl.x, bl.y}, cf, fs0);
+          fs1 = __builtin_elementwise_fma(f32x2{bl.z, bl.w}, cf, fs1);
+        }
+        const f32x2 o0 = gate2s(gs0, fs0), o1 = gate2s(gs1, fs1);
+        if (l + 1 < NLY) {
+          xr[j][2 * i] += ar[j][2 * i] + o0 * live;
+          xr[j][2 * i + 1] += ar[j][2 * i + 1] + o1 * live;
+        } else {
+          xr[j][2 * i] += o0 * live;
+          xr[j][2 * i + 1] += o1 * live;
+        }
+      }
+    };
+    if constexpr (PF) {
+      // the pair's 24 MFMAs as 4 interleaved chains on the shared kernel (an inactive tile
+      // of the pair computes on its own rows and is dropped), then the next layer's
+      // prefetch, then the two gates.  Accumulators start from the frame's staged bias.
+      bool act[2];
+      f32x16 g[2], f[2];
+      const float* bq = &BFL[((fpair - fbase) * NLY + l) * 2 * CI];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = TILE(j), ts = tg + k * 32;
+        act[j] = k >= kf && k <= kl && ts >= 0 && ts < Lh;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
+          const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
+          g[j][4 * i] = bg.x; g[j][4 * i + 1] = bg.y; g[j][4 * i + 2] = bg.z; g[j][4 * i + 3] = bg.w;
+          f[j][4 * i] = bl.x; f[j][4 * i + 1] = bl.y; f[j][4 * i + 2] = bl.z; f[j][4 * i + 3] = bl.w;
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 yb = *reinterpret_cast<const bf16x8*>(
+              &Y[(TILE(j) * 32 + n + (kk >> 1)) * LB_LD + 16 * (kk & 1) + 8 * h]);
+          g[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g[j], 0, 0, 0);
+          f[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f[j], 0, 0, 0);
+        }
+      }
+      if (l + 1 < NLY) kload(l + 1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (act[j]) gate_update(j, g[j], f[j], nullptr, 1.f);
+    } else {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = wave + j * NW, ts = tg + k * 32;
+      const int k = TILE(j), ts = tg + k * 32;
       if (k >= kf && k <= kl && ts >= 0 && ts < Lh) {
         f32x16 g, f;
 #pragma unroll
@@ -654,45 +879,24 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
           }
           bq = P.Bf + ((long long)b * Tc + (fn < Tc ? fn : Tc - 1)) * (2 * CI * NLY) + l * 2 * CI;
         } else {
-        const int frame = ts / hop;
-        const __bf16* kq = P.Kf[l] + ((long long)b * Tc + frame) * KPERLAYER;
-        bq = P.Bf + ((long long)b * Tc + frame) * (2 * CI * NLY) + l * 2 * CI;
+          const int frame = ts / hop;
+          const __bf16* kq = P.Kf[l] + ((long long)b * Tc + frame) * KPERLAYER;
+          bq = P.Bf + ((long long)b * Tc + frame) * (2 * CI * NLY) + l * 2 * CI;
 #pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
-          const int tap = kk >> 1;
-          const bf16x8 yb = *reinterpret_cast<const bf16x8*>(&Y[(k * 32 + n + tap) * LB_LD + 16 * (kk & 1) + 8 * h]);
-          bf16x8 kg, kt;
-          if constexpr (PF) {
-            kg = kn[j][kk]; kt = kn[j][6 + kk];
-          } else {
-            kg = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
-            kt = *reinterpret_cast<const bf16x8*>(kq + ((6 + kk) * 64 + lane) * 8);
+          for (int kk = 0; kk < 6; ++kk) {
+            const int tap = kk >> 1;
+            const bf16x8 yb = *reinterpret_cast<const bf16x8*>(&Y[(k * 32 + n + tap) * LB_LD + 16 * (kk & 1) + 8 * h]);
+            const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+            const bf16x8 kt = *reinterpret_cast<const bf16x8*>(kq + ((6 + kk) * 64 + lane) * 8);
+            g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kg, yb, g, 0, 0, 0);
+            f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, yb, f, 0, 0, 0);
           }
-          g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kg, yb, g, 0, 0, 0);
-          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, yb, f, 0, 0, 0);
         }
-        if constexpr (PF) {
-          if (l + 1 < NLY) kload(l + 1, j);
-        }
-        }
-        const f32x2 cg = {-LOG2E, -LOG2E}, cf = {2.f * LOG2E, 2.f * LOG2E};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
-          const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
-          const f32x2 bg0 = f32x2{bg.x, bg.y} * cg, bg1 = f32x2{bg.z, bg.w} * cg;
-          const f32x2 bl0 = f32x2{bl.x, bl.y} * cf, bl1 = f32x2{bl.z, bl.w} * cf;
-          const f32x2 o0 = gate2s(__builtin_elementwise_fma(f32x2{g[4 * i], g[4 * i + 1]}, cg, bg0),
-                                  __builtin_elementwise_fma(f32x2{f[4 * i], f[4 * i + 1]}, cf, bl0));
-          const f32x2 o1 = gate2s(__builtin_elementwise_fma(f32x2{g[4 * i + 2], g[4 * i + 3]}, cg, bg1),
-                                  __builtin_elementwise_fma(f32x2{f[4 * i + 2], f[4 * i + 3]}, cf, bl1));
-          // hop < 32: a tile can straddle the utterance end; rows past it stay zero
-          // (they are the next layer's conv padding)
-          const float live = (!SUB || ts + n < Lh) ? 1.f : 0.f;
-          xr[j][2 * i] += ar[j][2 * i] + o0 * live;
-          xr[j][2 * i + 1] += ar[j][2 * i + 1] + o1 * live;
-        }
+        // hop < 32: a tile can straddle the utterance end; rows past it stay zero
+        // (they are the next layer's conv padding)
+        gate_update(j, g, f, bq, (!SUB || ts + n < Lh) ? 1.f : 0.f);
       }
+    }
     }
     if (l < NLY - 1) LB_STAMP(4 + 3 * l);
   }
@@ -703,7 +907,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = wave + j * NW, row = k * 32 + n;
+      const int k = TILE(j), row = k * 32 + n;
       if (k >= 1 && k <= NG - 2) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -713,7 +917,10 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
     }
     __syncthreads();
     // two lanes per output sample (16 channels each), combined by one shuffle
-    for (int s2 = tid; s2 < 2 * TS; s2 += G::NT) {
+#pragma unroll
+    for (int it = 0; it < IF; ++it) {
+      const int s2 = tid + it * G::NT;                // wave-uniform bound (2 TS, NT: multiples of 64)
+      if (s2 >= 2 * TS) break;
       const int s = s2 >> 1, c0 = (s2 & 1) * 16, t = t0 + s;
       float e = 0.f;
 #pragma unroll
@@ -728,18 +935,18 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
       }
       e += __shfl_xor(e, 1);
       if ((s2 & 1) == 0 && t < Lh) {
-        e += P.bfin[0];
-        const long long idx = base + t;
-        float v = (P.audio[idx] - P.ce * e) / P.den;
-        if (P.sig != 0.f) v += P.sig * (P.noise ? P.noise[idx] : philox_normal(P.seed, (unsigned long long)idx, P.stream));
-        P.audio_out[idx] = v;
+        e += bfin;
+        // x_t from the staged audio: AS[i] is time tg - 3 + i, t = tg + 64 + s
+        float v = (AS[67 + s] - P.ce * e) / P.den;
+        if (P.sig != 0.f) v += P.sig * zr[it];
+        P.audio_out[base + t] = v;
       }
     }
   } else {
     // centre tiles [2, 2 + TS/32) -> x out
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = wave + j * NW, t = tg + k * 32 + n;
+      const int k = TILE(j), t = tg + k * 32 + n;
       if (k >= 2 && k < 2 + TS / 32 && t < Lh) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -749,6 +956,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
     }
   }
   LB_STAMP(15);
+#undef TILE
 }
 
 // ------------------------------------------------------------------ DiffusionDBlock (bf16)
@@ -1014,7 +1222,7 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
                                                                 const __bf16* __restrict__ W,
                                                                 const float* __restrict__ bias,
                                                                 __bf16* __restrict__ Kf, int Tc, int rows,
-                                                                int groups) {
+                                                                int groups, float sg, float sf) {
   __shared__ __attribute__((aligned(16))) __bf16 Ws[2][KP_NT * KP_LDW];
   __shared__ __attribute__((aligned(16))) __bf16 Ot[4][32 * KP_LDO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
@@ -1090,6 +1298,7 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
     // C[n][frame]: lane owns frame (r32) of tile ft, rows n = 32j + 8g + 4h + (0..3)
     const int layer = t / (KPERLAYER / KP_NT), n0 = (t - layer * (KPERLAYER / KP_NT)) * KP_NT;
     __bf16* kout = Kf + (long long)layer * rows * KPERLAYER + n0;
+    const float sc = n0 < KPERLAYER / 2 ? sg : sf;            // gate rows (k-steps 0..5) / filter rows
 #pragma unroll
     for (int ft = 0; ft < 2; ++ft) {
 #pragma unroll
@@ -1099,8 +1308,8 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
           const int nl = j * 32 + 8 * g + 4 * h;
           const float4 bn = *reinterpret_cast<const float4*>(bias + (long long)t * KP_NT + nl);
           *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + nl]) =
-              bf16x4{(__bf16)(acc[j][ft][4 * g] + bn.x), (__bf16)(acc[j][ft][4 * g + 1] + bn.y),
-                     (__bf16)(acc[j][ft][4 * g + 2] + bn.z), (__bf16)(acc[j][ft][4 * g + 3] + bn.w)};
+              bf16x4{(__bf16)((acc[j][ft][4 * g] + bn.x) * sc), (__bf16)((acc[j][ft][4 * g + 1] + bn.y) * sc),
+                     (__bf16)((acc[j][ft][4 * g + 2] + bn.z) * sc), (__bf16)((acc[j][ft][4 * g + 3] + bn.w) * sc)};
         }
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
       __builtin_amdgcn_wave_barrier();
@@ -1122,14 +1331,17 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
 }
 
 // All 4 layers' kernels of one LVC block into Kb ([4][B*Tc][6144], bf16).
-int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B, int Tc, hipStream_t st) {
+// prescale: the gate half scaled by -log2(e), the filter half by 2 log2(e) (the whole-block
+// LVC kernel's gate takes exp2 arguments straight from its accumulators).
+int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B, int Tc, hipStream_t st,
+                   bool prescale = false) {
   const int rows = B * Tc;
   const int fblocks = cdiv(rows, KP_FR);
   int groups = 512 / fblocks;                 // 2 blocks per CU x 256 CUs, one wave of blocks
   groups = groups < 1 ? 1 : groups > KP_TILES ? KP_TILES : groups;
   ProfScope ps("fd_kp_kernel", st);
   hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(fblocks, groups), dim3(256), 0, st, hk, lookup_bf16(K.kk_w),
-                     K.kk_b, Kb, Tc, rows, groups);
+                     K.kk_b, Kb, Tc, rows, groups, prescale ? -LOG2E : 1.f, prescale ? 2.f * LOG2E : 1.f);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -1220,6 +1432,19 @@ __global__ void pack_final_kernel(float* dst, const float* src) {
 }
 
 // ------------------------------------------------------------------ workspace
+// Does block n run as the whole-block LVC kernel (bf16; hop % 32 == 0: one frame per
+// 32-row tile; hop | 32: several, masked per frame)?
+bool fd_block_fused(const fd_model* m, int n) {
+  return m->pool_bf && m->lvc_ts > 0 && (m->hops[n] % 32 == 0 || (32 % m->hops[n] == 0 && m->lvc_sub));
+}
+// Kernel predictor on the side stream (fd_sample): every block on the whole-block kernel.
+bool fd_kp_side(const fd_model* m) {
+  if (!m->kp_side || !m->pool_bf) return false;
+  for (int n = 0; n < m->nblocks; ++n)
+    if (!fd_block_fused(m, n)) return false;
+  return true;
+}
+
 struct FdWs {
   size_t steps, e128, e512a, e512, nz;  // step MLP (nvec = S*B)
   size_t a0, d[3], dtmp0, dtmp1, xs, wav2;
@@ -1256,7 +1481,8 @@ FdWs fd_layout(const fd_model* m, int B, int Tc, int S) {
   // bf16 path: kernel-predictor hidden outputs of every (step, block), one batched launch
   w.hall = take((size_t)S * m->nblocks * B * Tc * HK);
   w.bfall = take((size_t)S * m->nblocks * B * Tc * 2 * CI * NLY);
-  w.Kf = take((size_t)B * Tc * KPERLAYER * 2);   // fp32: one layer; bf16: all 4 layers
+  // fp32: one layer; bf16: all 4 layers (one block's worth per block with the side stream)
+  w.Kf = take((size_t)B * Tc * KPERLAYER * 2 * (fd_kp_side(m) ? m->nblocks : 1));
   w.condT = take((size_t)B * Tc * CC);
   w.total = off * sizeof(float);
   return w;
@@ -1388,15 +1614,13 @@ int launch_lvc_block_ts(const LvcBlockArgs& la, bool ups, bool aud, bool fin, bo
 // the sampler update itself and sets *xout = nullptr.
 int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const float* condT,
            const float* nz, int step, int B, int Tc, float** xout, hipStream_t st,
-           const FdFinal* fin = nullptr) {
+           const FdFinal* fin = nullptr, bool side = false) {
   const int nb = m->nblocks;
   const long long L = (long long)Tc * m->hops[nb - 1];
   const bool bf = m->pool_bf != nullptr;
   // whole-block LVC kernel with its prologue/epilogue fusions (bf16)
   // (hop % 32 == 0: one frame per 32-row tile; hop | 32: several, masked per frame)
-  auto fused_block = [&](int n) {
-    return bf && m->lvc_ts > 0 && (m->hops[n] % 32 == 0 || (32 % m->hops[n] == 0 && m->lvc_sub));
-  };
+  auto fused_block = [&](int n) { return fd_block_fused(m, n); };
   auto fused_ups = [&](int n) { return fused_block(n) && m->lvc_fuse && m->ratios[n] >= 4; };
   const bool aud = fd_final_fused(m);              // a0 = first_conv(audio) recomputed by its consumers
   float* a0 = ws + W.a0;
@@ -1481,7 +1705,12 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       }
       __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf);
       const int rows = B * Tc;
-      PD_TRY(kp_kernels_all(K, hkb, Kb, B, Tc, st));
+      if (side) {   // written on the side stream (fd_sample)
+        Kb += (size_t)n * rows * NLY * KPERLAYER;
+        PD_HIP(hipStreamWaitEvent(st, m->ev_kp[n], 0));
+      } else {
+        PD_TRY(kp_kernels_all(K, hkb, Kb, B, Tc, st, true));
+      }
       LvcBlockArgs la{};
       for (int i = 0; i < NLY; ++i) {
         la.Kf[i] = Kb + (size_t)i * rows * KPERLAYER;
@@ -1505,11 +1734,12 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : hop < 32 ? "fd_lvc_block_sub" : ups ? "fd_lvc_block_ups"
                                                                                    : "fd_lvc_block", st);
         const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
-        const bool pf = m->lvc_pf && hop >= 32;
+        const bool pf = m->lvc_pf && hop % 64 == 0;   // a 64-row tile pair shares one frame
         if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
         else if (ts == 384) PD_TRY(launch_lvc_block_ts<384>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
         else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
       }
+      if (side) PD_HIP(hipEventRecord(m->ev_lvc[n], st));   // ring slot n free again
       if (fuse_fin) { *xout = nullptr; return PD_OK; }
       x = la.xout;
       Tin = Tout;
@@ -1602,6 +1832,7 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   if (const char* e = getenv("PRODIFF_LVC_FUSE")) m->lvc_fuse = atoi(e) != 0;
   if (const char* e = getenv("PRODIFF_LVC_PF")) m->lvc_pf = atoi(e) != 0;
   if (const char* e = getenv("PRODIFF_LVC_SUB")) m->lvc_sub = atoi(e) != 0;
+  if (const char* e = getenv("PRODIFF_KP_SIDE")) m->kp_side = atoi(e) != 0;
   int hop = 1;
   for (int n = 0; n < m->nblocks; ++n) {
     m->ratios[n] = dims->upsample_ratios[n];
@@ -1729,6 +1960,15 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
 
 void fd_destroy(fd_model* m) {
   if (!m) return;
+  if (m->side) {
+    (void)hipStreamSynchronize(m->side);
+    (void)hipStreamDestroy(m->side);
+    (void)hipEventDestroy(m->ev_hidden);
+    for (int n = 0; n < 4; ++n) {
+      if (m->ev_kp[n]) (void)hipEventDestroy(m->ev_kp[n]);
+      if (m->ev_lvc[n]) (void)hipEventDestroy(m->ev_lvc[n]);
+    }
+  }
   if (m->pool_bf) {
     unregister_bf16_pool(m->pool);
     (void)hipFree(m->pool_bf);
@@ -1793,8 +2033,34 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
   PD_TRY(fill_steps(ws + W.steps, sv.data(), N, B, st));
   PD_TRY(fd_step_mlp(m, ws, W, N * B, st));
   if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, mel, ws + W.nz, N, B, Tc, st));
+  const bool side = fd_kp_side(m);
+  if (side && !m->side) {
+    int lo = 0, hi = 0;
+    PD_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));   // lo = least urgent
+    PD_HIP(hipStreamCreateWithPriority(&m->side, hipStreamNonBlocking, lo));
+    PD_HIP(hipEventCreateWithFlags(&m->ev_hidden, hipEventDisableTiming));
+    for (int b = 0; b < m->nblocks; ++b) {
+      PD_HIP(hipEventCreateWithFlags(&m->ev_kp[b], hipEventDisableTiming));
+      PD_HIP(hipEventCreateWithFlags(&m->ev_lvc[b], hipEventDisableTiming));
+    }
+  }
+  if (side) {
+    PD_HIP(hipEventRecord(m->ev_hidden, st));
+    PD_HIP(hipStreamWaitEvent(m->side, m->ev_hidden, 0));
+  }
+  const int nb = m->nblocks, rows = B * Tc;
   for (int j = 0; j < N; ++j) {
     const int n = N - 1 - j;
+    if (side) {
+      // step j's kernels for every block; slot b is rewritten once step j-1's block b has run
+      for (int b = 0; b < nb; ++b) {
+        if (j > 0) PD_HIP(hipStreamWaitEvent(m->side, m->ev_lvc[b], 0));
+        const __bf16* hkb = reinterpret_cast<const __bf16*>(ws + W.hall) + ((size_t)j * nb + b) * rows * HK;
+        __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf) + (size_t)b * rows * NLY * KPERLAYER;
+        PD_TRY(kp_kernels_all(m->blk[b], hkb, Kb, B, Tc, m->side, true));
+        PD_HIP(hipEventRecord(m->ev_kp[b], m->side));
+      }
+    }
     float* x = nullptr;
     // x = (x - beta/sqrt(1-alpha^2) eps) / sqrt(1-beta) + [n>0] sigma z   (util.py:222-226)
     const float ce = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
@@ -1803,7 +2069,7 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
     const FdFinal fin{other, noise ? noise + (size_t)j * B * L : (const float*)nullptr, ce, den, sg, seed,
                       0x10000u + j};
     PD_TRY(fd_net(m, ws, W, cur, mel, ws + W.nz + (size_t)j * B * m->nblocks * CC, j, B, Tc, &x, st,
-                  fused ? &fin : nullptr));
+                  fused ? &fin : nullptr, side));
     if (x == nullptr) {   // updated inside the last LVC block
       std::swap(cur, other);
       continue;

@@ -1,7 +1,7 @@
 // Standalone probe for lvc_block_bf16_kernel: times the kernel alone on C3-sized
 // synthetic inputs and prints where a block spends its time (s_memtime stamps per
 // phase, LB_TRACE).  Diagnostic only (not a parity check: inputs are random).
-//   build: make -C tools lvc_probe      run: tools/build/lvc_probe [hop] [TS]
+//   build: make -C tools lvc_probe      run: tools/build/lvc_probe [hop] [TS] [final=1]
 #define LB_TRACE 1
 #include "../prodiff_amd/csrc/fastdiff.hip"
 
@@ -33,8 +33,11 @@ template <typename T> static T* upload(size_t n, float scale) {
   return d;
 }
 
-template <int TS> static void run(int hop) {
+// FINAL: the sampler's last block as bench.py runs it (upsample r=4 + first conv + final
+// update fused, next-layer kernel prefetch): lvc_block_bf16_kernel<TS, true, true, true, true>.
+template <int TS, bool FINAL = false> static void run(int hop) {
   using G = LbGeo<TS>;
+  constexpr bool UPS = FINAL, AUD = FINAL, FIN = FINAL, PF = FINAL;
   const int B = 8, Tc = 861;
   const long long Lh = (long long)Tc * hop, rows = B * Lh;
   LvcBlockArgs la{};
@@ -48,16 +51,32 @@ template <int TS> static void run(int hop) {
   }
   la.Bf = upload<float>((size_t)B * Tc * 2 * CI * NLY, 0.1f);
   la.Tc = Tc; la.hop = hop;
+  if (FINAL) {
+    const int r = 4;
+    la.xin = upload<float>(rows / r * CI, 1.f);
+    la.Wup = upload<__bf16>((size_t)r * CI * 64, 0.2f);
+    la.bup = upload<float>(CI, 0.05f);
+    la.r = r; la.p = r / 2 + r % 2;
+    la.a = nullptr;
+    la.audio = upload<float>(rows, 1.f);
+    la.fw = upload<float>(CI * 7, 0.3f);
+    la.fb = upload<float>(CI, 0.05f);
+    la.wfin = upload<float>(7 * CI, 0.1f);
+    la.bfin = upload<float>(1, 0.05f);
+    CK(hipMalloc((void**)&la.audio_out, rows * sizeof(float)));
+    la.ce = 0.3f; la.den = 0.9f; la.sig = 0.1f; la.seed = 7; la.stream = 1;
+  }
   const dim3 grid(cdiv(Lh, TS), B);
   const int nsamp = (grid.x * grid.y) / 61 + 1;
-  CK(hipMalloc((void**)&la.trace, (size_t)nsamp * G::NW * 16 * 8));
-  CK(hipMemset(la.trace, 0, (size_t)nsamp * G::NW * 16 * 8));
+  constexpr int NS = 24;   // stamp slots per wave (LB_STAMP)
+  CK(hipMalloc((void**)&la.trace, (size_t)nsamp * G::NW * NS * 8));
+  CK(hipMemset(la.trace, 0, (size_t)nsamp * G::NW * NS * 8));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, false, false, false>), grid, dim3(G::NT), 0, 0, la);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, UPS, AUD, FIN, PF>), grid, dim3(G::NT), 0, 0, la);
   const int reps = 20;
   CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, false, false, false>), grid, dim3(G::NT), 0, 0, la);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, UPS, AUD, FIN, PF>), grid, dim3(G::NT), 0, 0, la);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -66,31 +85,27 @@ template <int TS> static void run(int hop) {
   const double bytes = (double)rows * 3 * 128 + (double)B * Tc * NLY * (KPERLAYER * 2 + 256);
   printf("TS=%d hop=%d grid=%dx%d  %.1f us/launch  %.2f TB/s (x,a in + x out + kernels)\n", TS, hop, grid.x,
          grid.y, us, bytes / us * 1e-6);
-  std::vector<unsigned long long> tr((size_t)nsamp * G::NW * 16);
+  std::vector<unsigned long long> tr((size_t)nsamp * G::NW * NS);
   CK(hipMemcpy(tr.data(), la.trace, tr.size() * 8, hipMemcpyDeviceToHost));
-  // mean per-phase cycles over sampled waves (last launch's stamps)
-  const char* names[16] = {"start", "zero+load", "L0 stage", "L0 preconv", "L0 lvc", "L1 stage", "L1 preconv",
+  // stamps in time order (0 = start, 15 = end); 16..20 only in the fused prologue
+  std::vector<int> seq = {0};
+  if (FINAL) seq.insert(seq.end(), {16, 17, 18, 19, 20});
+  for (int i = 1; i <= 12; ++i) seq.push_back(i);
+  seq.push_back(14);
+  seq.push_back(15);
+  const char* names[NS] = {"start", "kload+sync", "L0 stage", "L0 preconv", "L0 lvc", "L1 stage", "L1 preconv",
                            "L1 lvc", "L2 stage", "L2 preconv", "L2 lvc", "L3 stage", "L3 preconv", "-",
-                           "L3 lvc", "store"};
+                           "L3 lvc", "store", "staging", "XP fill", "phase GEMM", "x/a regs", "zero U/Y"};
   // median per-phase duration over sampled waves whose stamps are monotone
-  std::vector<std::vector<double>> ph(16);
+  std::vector<std::vector<double>> ph(NS);
   std::vector<double> life;
   for (int s = 0; s < nsamp * G::NW; ++s) {
-    const unsigned long long* t = &tr[(size_t)s * 16];
+    const unsigned long long* t = &tr[(size_t)s * NS];
     bool ok = t[0] != 0;
-    unsigned long long prev = t[0];
-    for (int i = 1; i < 16 && ok; ++i) {
-      if (i == 13) continue;
-      ok = t[i] >= prev && t[i] - prev < 100000000ull;
-      prev = t[i];
-    }
+    for (size_t q = 1; q < seq.size() && ok; ++q)
+      ok = t[seq[q]] >= t[seq[q - 1]] && t[seq[q]] - t[seq[q - 1]] < 100000000ull;
     if (!ok) continue;
-    prev = t[0];
-    for (int i = 1; i < 16; ++i) {
-      if (i == 13) continue;
-      ph[i].push_back((double)(t[i] - prev));
-      prev = t[i];
-    }
+    for (size_t q = 1; q < seq.size(); ++q) ph[seq[q]].push_back((double)(t[seq[q]] - t[seq[q - 1]]));
     life.push_back((double)(t[15] - t[0]));
   }
   auto med = [](std::vector<double> v) {
@@ -100,13 +115,15 @@ template <int TS> static void run(int hop) {
   };
   const double L = med(life);
   printf("  %zu sampled waves, median lifetime %.0f cycles\n", life.size(), L);
-  for (int i = 1; i < 16; ++i)
-    if (i != 13) printf("    %-11s %8.0f cyc  %5.1f%%\n", names[i], med(ph[i]), 100.0 * med(ph[i]) / L);
+  for (size_t q = 1; q < seq.size(); ++q)
+    printf("    %-11s %8.0f cyc  %5.1f%%\n", names[seq[q]], med(ph[seq[q]]), 100.0 * med(ph[seq[q]]) / L);
 }
 
 int main(int argc, char** argv) {
   const int hop = argc > 1 ? atoi(argv[1]) : 256;
   const int ts = argc > 2 ? atoi(argv[2]) : 128;
-  if (ts == 256) run<256>(hop); else run<128>(hop);
+  if (argc > 3 && atoi(argv[3]) == 1) run<384, true>(hop);
+  else if (ts == 256) run<256>(hop);
+  else run<128>(hop);
   return 0;
 }
