@@ -698,8 +698,11 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
     }
   }
   LB_STAMP(19);
-  if constexpr (UPS) __syncthreads();                // XS reads done before U/Y (aliased) are zeroed
-  {
+  if constexpr (UPS) __syncthreads();                // XS reads done before U/Y (aliased) are written
+  // PF: U/Y are not cleared.  A valid row only reads rows staged or computed for it (the
+  // e_l bookkeeping), utterance-edge padding is selected, not multiplied, so stale LDS
+  // (possibly NaN) reaches only rows that are never stored.
+  if constexpr (!PF) {
     const bf16x8 z = {};
     for (int i = tid; i < G::UY_BYTES / 16; i += G::NT) reinterpret_cast<bf16x8*>(smem)[i] = z;
   }
@@ -768,9 +771,9 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
         const int tt = tg + kp * 32 - 1;                  // the tile's first time (wave-uniform)
         if (tt < 0 || tt + 31 >= Lh) {                    // utterance-edge tile: zero-pad
           const int t = tt + n;
-          const float m = (t >= 0 && t < Lh) ? 1.f : 0.f;
+          const bool in = t >= 0 && t < Lh;           // select, not multiply: stale LDS may be NaN
 #pragma unroll
-          for (int p = 0; p < 8; ++p) v[p] = v[p] * m;
+          for (int p = 0; p < 8; ++p) v[p] = in ? v[p] : f32x2{0.f, 0.f};
         }
         bf16x8 y0, y1;
 #pragma unroll
@@ -790,7 +793,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
     // the exp2 arguments.  z = x + a lives in registers: x_{l+1} = z_l + o, and
     // z_{l+1} = x_{l+1} + a except after the last layer.
     const f32x2 cg = {-LOG2E, -LOG2E}, cf = {2.f * LOG2E, 2.f * LOG2E};
-    auto gate_update = [&](int j, const f32x16& g, const f32x16& f, const float* bq, float live) {
+    auto gate_update = [&](int j, const f32x16& g, const f32x16& f, const float* bq, bool live) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         f32x2 gs0 = {g[4 * i], g[4 * i + 1]}, gs1 = {g[4 * i + 2], g[4 * i + 3]};
@@ -804,12 +807,13 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
           fs1 = __builtin_elementwise_fma(f32x2{bl.z, bl.w}, cf, fs1);
         }
         const f32x2 o0 = gate2s(gs0, fs0), o1 = gate2s(gs1, fs1);
+        const f32x2 z2 = {0.f, 0.f};
         if (l + 1 < NLY) {
-          xr[j][2 * i] += ar[j][2 * i] + o0 * live;
-          xr[j][2 * i + 1] += ar[j][2 * i + 1] + o1 * live;
+          xr[j][2 * i] += ar[j][2 * i] + (live ? o0 : z2);
+          xr[j][2 * i + 1] += ar[j][2 * i + 1] + (live ? o1 : z2);
         } else {
-          xr[j][2 * i] += o0 * live;
-          xr[j][2 * i + 1] += o1 * live;
+          xr[j][2 * i] += live ? o0 : z2;
+          xr[j][2 * i + 1] += live ? o1 : z2;
         }
       }
     };
@@ -845,7 +849,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
       if (l + 1 < NLY) kload(l + 1);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        if (act[j]) gate_update(j, g[j], f[j], nullptr, 1.f);
+        if (act[j]) gate_update(j, g[j], f[j], nullptr, true);
     } else {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -894,7 +898,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
         }
         // hop < 32: a tile can straddle the utterance end; rows past it stay zero
         // (they are the next layer's conv padding)
-        gate_update(j, g, f, bq, (!SUB || ts + n < Lh) ? 1.f : 0.f);
+        gate_update(j, g, f, bq, !SUB || ts + n < Lh);
       }
     }
     }
@@ -1225,6 +1229,9 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
                                                                 int groups, float sg, float sf) {
   __shared__ __attribute__((aligned(16))) __bf16 Ws[2][KP_NT * KP_LDW];
   __shared__ __attribute__((aligned(16))) __bf16 Ot[4][32 * KP_LDO];
+  // the block's bias rows (tiles tb .. te - 1), staged once: a global bias load in the
+  // epilogue would wait behind the next tile's weight loads (vmcnt retires in order)
+  __shared__ __attribute__((aligned(16))) float Bs[(KP_TILES / 16 + 2) * KP_NT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int fw = blockIdx.x * KP_FR + wave * 64;            // first frame of this wave
   const int tb = blockIdx.y * KP_TILES / groups, te = (blockIdx.y + 1) * KP_TILES / groups;
@@ -1257,6 +1264,7 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
     *reinterpret_cast<uint4*>(&Ws[buf][loff[4]]) = s4;                   \
     *reinterpret_cast<uint4*>(&Ws[buf][loff[5]]) = s5;                   \
   } while (0)
+  for (int i = tid; i < (te - tb) * KP_NT; i += 256) Bs[i] = bias[(long long)tb * KP_NT + i];
   KP_LD(tb);
   // B fragments: k = tap*64 + ch (tap-major), lane half h holds 8 consecutive channels
   bf16x8 af[2][12];
@@ -1306,7 +1314,7 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int nl = j * 32 + 8 * g + 4 * h;
-          const float4 bn = *reinterpret_cast<const float4*>(bias + (long long)t * KP_NT + nl);
+          const float4 bn = *reinterpret_cast<const float4*>(&Bs[(t - tb) * KP_NT + nl]);
           *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + nl]) =
               bf16x4{(__bf16)((acc[j][ft][4 * g] + bn.x) * sc), (__bf16)((acc[j][ft][4 * g + 1] + bn.y) * sc),
                      (__bf16)((acc[j][ft][4 * g + 2] + bn.z) * sc), (__bf16)((acc[j][ft][4 * g + 3] + bn.w) * sc)};
@@ -1338,7 +1346,7 @@ int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B
   const int rows = B * Tc;
   const int fblocks = cdiv(rows, KP_FR);
   int groups = 512 / fblocks;                 // 2 blocks per CU x 256 CUs, one wave of blocks
-  groups = groups < 1 ? 1 : groups > KP_TILES ? KP_TILES : groups;
+  groups = groups < 16 ? 16 : groups > KP_TILES ? KP_TILES : groups;   // >= 16: Bs holds a block's tiles
   ProfScope ps("fd_kp_kernel", st);
   hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(fblocks, groups), dim3(256), 0, st, hk, lookup_bf16(K.kk_w),
                      K.kk_b, Kb, Tc, rows, groups, prescale ? -LOG2E : 1.f, prescale ? 2.f * LOG2E : 1.f);
