@@ -1213,35 +1213,47 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 // Location-variable kernels of ALL 4 layers of an LVC block, frame-major bf16
 // (modules.py:335-340):  Kf[l][f][n] = b[l][n] + W[l][n] . [h(f-1); h(f); h(f+1)],
 // n < 6144, K = 192.  One GEMM with 4 x 6144 rows (weights = MFMA A operand, staged in
-// LDS 64 rows at a time, double-buffered, next tile's loads in flight under the MFMAs)
-// and one column per frame.  Block = 256 frames; each wave keeps the bf16 h fragments
-// of its 64 frames (two 32-frame MFMA tiles) in registers for the whole block, so each
-// 16-B LDS weight read feeds two MFMAs.  A lane of C holds 4 consecutive kernel values
-// of one frame; a per-wave LDS transpose turns them into full 128-B line stores.
+// LDS 64 rows at a time; the next tile's rows are loaded into registers under the MFMAs)
+// and one column per frame.  Block = 256 frames, 8 waves of 32 frames; a wave keeps the
+// bf16 h fragments of its frames in registers for the whole block (about 120 VGPRs, so
+// two blocks -- 16 waves -- share a CU and hide each other's LDS and store latency).
+// A lane of C holds 4 consecutive kernel values of one frame; a per-wave LDS transpose
+// turns them into full 128-B line stores.
 // Block (x, y) owns frames [256x, 256x + 256) and weight tiles [y T / G, (y+1) T / G).
 constexpr int KP_FR = 256, KP_NT = 64, KP_LDW = 200;   // 400-B LDS rows: conflict-free b128 reads
 constexpr int KP_LDO = 72;                             // output transpose rows: 64 + 8 pad
 constexpr int KP_TILES = NLY * KPERLAYER / KP_NT;      // 384
-__global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __restrict__ hin,
-                                                                const __bf16* __restrict__ W,
-                                                                const float* __restrict__ bias,
-                                                                __bf16* __restrict__ Kf, int Tc, int rows,
-                                                                int groups, float sg, float sf) {
-  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][KP_NT * KP_LDW];
-  __shared__ __attribute__((aligned(16))) __bf16 Ot[4][32 * KP_LDO];
+constexpr int KP_THREADS = 512;
+__global__ __launch_bounds__(KP_THREADS, 2) void kp_kernel_bf16_kernel(const __bf16* __restrict__ hin,
+                                                                       const __bf16* __restrict__ W,
+                                                                       const float* __restrict__ bias,
+                                                                       __bf16* __restrict__ Kf, int Tc, int rows,
+                                                                       int groups, float sg, float sf) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ws[KP_NT * KP_LDW];
+  __shared__ __attribute__((aligned(16))) __bf16 Ot[8][32 * KP_LDO];
   // the block's bias rows (tiles tb .. te - 1), staged once: a global bias load in the
   // epilogue would wait behind the next tile's weight loads (vmcnt retires in order)
   __shared__ __attribute__((aligned(16))) float Bs[(KP_TILES / 16 + 2) * KP_NT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
-  const int fw = blockIdx.x * KP_FR + wave * 64;            // first frame of this wave
-  const int tb = blockIdx.y * KP_TILES / groups, te = (blockIdx.y + 1) * KP_TILES / groups;
-  // W tile = 64 rows x 384 B = 1536 16-B pieces, 6 per thread (named registers: an
+  // XCD-aware order (as in lvc_block_bf16_kernel): each XCD walks a contiguous run of
+  // logical blocks, y-major, so a weight-tile group is read into one XCD's L2, not eight
+  int bx, by;
+  {
+    const int total = gridDim.x * gridDim.y, id = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xcd = id & 7, slot = id >> 3, per = total >> 3, rem = total & 7;
+    const int logical = xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
+    by = logical / gridDim.x;
+    bx = logical - by * gridDim.x;
+  }
+  const int fw = bx * KP_FR + wave * 32;                    // first frame of this wave
+  const int tb = by * KP_TILES / groups, te = (by + 1) * KP_TILES / groups;
+  // W tile = 64 rows x 384 B = 1536 16-B pieces, 3 per thread (named registers: an
   // indexed array here is demoted to scratch by hipcc)
-  uint4 s0, s1, s2, s3, s4, s5;
-  int goff[6], loff[6];
+  uint4 s0, s1, s2;
+  int goff[3], loff[3];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int c = tid + 256 * i, row = c / 24, col = (c - row * 24) * 8;
+  for (int i = 0; i < 3; ++i) {
+    const int c = tid + KP_THREADS * i, row = c / 24, col = (c - row * 24) * 8;
     goff[i] = row * 192 + col;
     loff[i] = row * KP_LDW + col;
   }
@@ -1251,26 +1263,19 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
     s0 = *reinterpret_cast<const uint4*>(src_ + goff[0]);                \
     s1 = *reinterpret_cast<const uint4*>(src_ + goff[1]);                \
     s2 = *reinterpret_cast<const uint4*>(src_ + goff[2]);                \
-    s3 = *reinterpret_cast<const uint4*>(src_ + goff[3]);                \
-    s4 = *reinterpret_cast<const uint4*>(src_ + goff[4]);                \
-    s5 = *reinterpret_cast<const uint4*>(src_ + goff[5]);                \
   } while (0)
-#define KP_ST(buf)                                                       \
+#define KP_ST()                                                          \
   do {                                                                   \
-    *reinterpret_cast<uint4*>(&Ws[buf][loff[0]]) = s0;                   \
-    *reinterpret_cast<uint4*>(&Ws[buf][loff[1]]) = s1;                   \
-    *reinterpret_cast<uint4*>(&Ws[buf][loff[2]]) = s2;                   \
-    *reinterpret_cast<uint4*>(&Ws[buf][loff[3]]) = s3;                   \
-    *reinterpret_cast<uint4*>(&Ws[buf][loff[4]]) = s4;                   \
-    *reinterpret_cast<uint4*>(&Ws[buf][loff[5]]) = s5;                   \
+    *reinterpret_cast<uint4*>(&Ws[loff[0]]) = s0;                        \
+    *reinterpret_cast<uint4*>(&Ws[loff[1]]) = s1;                        \
+    *reinterpret_cast<uint4*>(&Ws[loff[2]]) = s2;                        \
   } while (0)
-  for (int i = tid; i < (te - tb) * KP_NT; i += 256) Bs[i] = bias[(long long)tb * KP_NT + i];
+  for (int i = tid; i < (te - tb) * KP_NT; i += KP_THREADS) Bs[i] = bias[(long long)tb * KP_NT + i];
   KP_LD(tb);
   // B fragments: k = tap*64 + ch (tap-major), lane half h holds 8 consecutive channels
-  bf16x8 af[2][12];
-#pragma unroll
-  for (int ft = 0; ft < 2; ++ft) {
-    const int R = fw + ft * 32 + r32;
+  bf16x8 af[12];
+  {
+    const int R = fw + r32;
     const bool ok = R < rows;
     const int b = ok ? R / Tc : 0, f = R - b * Tc;
 #pragma unroll
@@ -1278,67 +1283,58 @@ __global__ __launch_bounds__(256, 2) void kp_kernel_bf16_kernel(const __bf16* __
       const int tap = kk >> 2, kc = kk & 3, ff = f + tap - 1;
       bf16x8 v = {};
       if (ok && ff >= 0 && ff < Tc) v = *reinterpret_cast<const bf16x8*>(hin + ((long long)b * Tc + ff) * HK + kc * 16 + h * 8);
-      af[ft][kk] = v;
+      af[kk] = v;
     }
   }
-  KP_ST(0);
+  KP_ST();
   __syncthreads();
   __bf16* ot = Ot[wave];
   for (int t = tb; t < te; ++t) {
-    const int buf = (t - tb) & 1;
     if (t + 1 < te) KP_LD(t + 1);
-    f32x16 acc[2][2];
+    f32x16 acc[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][ft][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&Ws[buf][(j * 32 + r32) * KP_LDW + kk * 16 + h * 8]);
-        acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[0][kk], acc[j][0], 0, 0, 0);
-        acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[1][kk], acc[j][1], 0, 0, 0);
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&Ws[(j * 32 + r32) * KP_LDW + kk * 16 + h * 8]);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[kk], acc[j], 0, 0, 0);
       }
     }
-    // C[n][frame]: lane owns frame (r32) of tile ft, rows n = 32j + 8g + 4h + (0..3)
+    // C[n][frame]: lane owns frame r32, rows n = 32j + 8g + 4h + (0..3)
     const int layer = t / (KPERLAYER / KP_NT), n0 = (t - layer * (KPERLAYER / KP_NT)) * KP_NT;
     __bf16* kout = Kf + (long long)layer * rows * KPERLAYER + n0;
     const float sc = n0 < KPERLAYER / 2 ? sg : sf;            // gate rows (k-steps 0..5) / filter rows
 #pragma unroll
-    for (int ft = 0; ft < 2; ++ft) {
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int nl = j * 32 + 8 * g + 4 * h;
-          const float4 bn = *reinterpret_cast<const float4*>(&Bs[(t - tb) * KP_NT + nl]);
-          *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + nl]) =
-              bf16x4{(__bf16)((acc[j][ft][4 * g] + bn.x) * sc), (__bf16)((acc[j][ft][4 * g + 1] + bn.y) * sc),
-                     (__bf16)((acc[j][ft][4 * g + 2] + bn.z) * sc), (__bf16)((acc[j][ft][4 * g + 3] + bn.w) * sc)};
-        }
-      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
-        const int Rf = fw + ft * 32 + fl;
-        const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
-        if (Rf < rows) *reinterpret_cast<uint4*>(kout + (long long)Rf * KPERLAYER + ch) = v;
+      for (int g = 0; g < 4; ++g) {
+        const int nl = j * 32 + 8 * g + 4 * h;
+        const float4 bn = *reinterpret_cast<const float4*>(&Bs[(t - tb) * KP_NT + nl]);
+        *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + nl]) =
+            bf16x4{(__bf16)((acc[j][4 * g] + bn.x) * sc), (__bf16)((acc[j][4 * g + 1] + bn.y) * sc),
+                   (__bf16)((acc[j][4 * g + 2] + bn.z) * sc), (__bf16)((acc[j][4 * g + 3] + bn.w) * sc)};
       }
-      __builtin_amdgcn_s_waitcnt(0xC07F);   // transpose reads done before the next tile's writes
-      __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
+      const int Rf = fw + fl;
+      const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
+      if (Rf < rows) *reinterpret_cast<uint4*>(kout + (long long)Rf * KPERLAYER + ch) = v;
     }
-    if (t + 1 < te) KP_ST(buf ^ 1);
+    __syncthreads();                      // every wave is past its Ws reads (and Ot reads)
+    if (t + 1 < te) KP_ST();
     __syncthreads();
   }
 #undef KP_LD
 #undef KP_ST
 }
 
-// All 4 layers' kernels of one LVC block into Kb ([4][B*Tc][6144], bf16).
 // prescale: the gate half scaled by -log2(e), the filter half by 2 log2(e) (the whole-block
 // LVC kernel's gate takes exp2 arguments straight from its accumulators).
 int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B, int Tc, hipStream_t st,
@@ -1348,7 +1344,7 @@ int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B
   int groups = 512 / fblocks;                 // 2 blocks per CU x 256 CUs, one wave of blocks
   groups = groups < 16 ? 16 : groups > KP_TILES ? KP_TILES : groups;   // >= 16: Bs holds a block's tiles
   ProfScope ps("fd_kp_kernel", st);
-  hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(fblocks, groups), dim3(256), 0, st, hk, lookup_bf16(K.kk_w),
+  hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(fblocks, groups), dim3(KP_THREADS), 0, st, hk, lookup_bf16(K.kk_w),
                      K.kk_b, Kb, Tc, rows, groups, prescale ? -LOG2E : 1.f, prescale ? 2.f * LOG2E : 1.f);
   PD_LAUNCH_CHECK();
   return PD_OK;

@@ -59,11 +59,28 @@ __global__ __launch_bounds__(256) void matvec_kernel(const float* __restrict__ W
   float s[MV_NV];
 #pragma unroll
   for (int j = 0; j < MV_NV; ++j) s[j] = 0.f;
-  for (int k = lane; k < K; k += 64) {
+  // 4 k-steps per trip with every load issued before the FMAs (K is a multiple of 64 for
+  // every caller; the tail loop covers the rest)
+  const float* iv = in + (long long)v0 * in_ld;
+  int k = lane;
+  for (; k + 192 < K; k += 256) {
+    float wk[4], x[4][MV_NV];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      wk[u] = w[k + 64 * u];
+#pragma unroll
+      for (int j = 0; j < MV_NV; ++j) x[u][j] = j < nv ? iv[(long long)j * in_ld + k + 64 * u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < MV_NV; ++j) s[j] = fmaf(wk[u], x[u][j], s[j]);
+  }
+  for (; k < K; k += 64) {
     const float wk = w[k];
 #pragma unroll
     for (int j = 0; j < MV_NV; ++j)
-      if (j < nv) s[j] = fmaf(wk, in[(long long)(v0 + j) * in_ld + k], s[j]);
+      if (j < nv) s[j] = fmaf(wk, iv[(long long)j * in_ld + k], s[j]);
   }
 #pragma unroll
   for (int j = 0; j < MV_NV; ++j) {

@@ -234,6 +234,14 @@ int step_mlp(const pd_wavenet* h, float* ws, const WsLayout& L, int nvec, hipStr
   return PD_OK;
 }
 
+// Small WaveNet projections (rows = B*T, K <= 256): 32 x 128 tiles.  With 4 waves per
+// block, 128-row tiles leave too few blocks in flight for these short K loops (r01 ab_wns:
+// 128x64 40 us, 64x64 25 us, 32x128 21 us for the skip head at B*T = 6888).
+template <int EPI, int ID>
+int launch_small_gemm(const GemmArgs& a, hipStream_t st, const char* tag) {
+  return launch_gemm<1, 1, 1, 4, EPI, ID>(a, st, tag);
+}
+
 // Input projection + residual stack + skip head.  xin: time-major [B][T][M];
 // cond: time-major [B][T][H]; dproj: [B][L][C].  Leaves relu(skip head) in ws.hs.
 int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float* xin,
@@ -248,7 +256,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     GemmArgs a = make_gemm(B, T, C, h->Win, h->ldw_in, h->b_in, x, BTs * C, C);
     add_seg(a, make_seg(xin, BTs * M, M, M, 0));
     a.act = ACT_RELU;
-    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_WN_INPROJ>(a, st, "wn_inproj")));
+    PD_TRY((launch_small_gemm<EPI_STORE, U_WN_INPROJ>(a, st, "wn_inproj")));
   }
   if (h->W1f) {
     // bf16, C == 256: one fused launch per residual layer, x ping-pongs x <-> x2
@@ -296,7 +304,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     s.scale = 1.0f / sqrtf((float)Ly);
     add_seg(a, s);
     a.act = ACT_RELU;
-    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_WN_SKIP>(a, st, "wn_skiphead")));
+    PD_TRY((launch_small_gemm<EPI_STORE, U_WN_SKIP>(a, st, "wn_skiphead")));
   }
   return PD_OK;
 }
@@ -484,7 +492,7 @@ int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1
     a.noise = noise ? noise + (size_t)j * BTM : nullptr;
     a.noise_bs = BTs * M; a.noise_ld = M;
     a.seed = seed; a.stream_id = (unsigned)j;
-    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_POSTERIOR, U_WN_POSTERIOR>(a, st, "wn_outproj_posterior")));
+    PD_TRY((launch_small_gemm<EPI_POSTERIOR, U_WN_POSTERIOR>(a, st, "wn_outproj_posterior")));
   }
   return PD_OK;
 }
@@ -594,7 +602,7 @@ int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, fl
       if (tb.s == 1) {   // Euler: x += v dt fused into the output projection (reflow.py:50)
         a.res = x; a.res_bs = BTs * M; a.res_ld = M;
         a.c1 = dts; a.c2 = 1.f; a.sigma = 0.f;
-        PD_TRY((launch_gemm<1, 2, 4, 1, EPI_POSTERIOR, U_WN_POSTERIOR>(a, st, "wn_outproj_posterior")));
+        PD_TRY((launch_small_gemm<EPI_POSTERIOR, U_WN_POSTERIOR>(a, st, "wn_outproj_posterior")));
       } else {
         PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_WN_OUT>(a, st, "wn_outproj")));
       }
