@@ -48,6 +48,10 @@ int pd_version(void);
  * buffer size needed (including the NUL), or -1 on error. */
 int pd_profile_enable(int on);
 int pd_profile_summary(char* buf, int buflen);
+/* Restrict recording to the tags in a comma-separated list (NULL or "" = every tag).
+ * An event pair costs GPU time at every launch it brackets; bench.py times its step with
+ * only the dominant kernel recorded. */
+int pd_profile_filter(const char* tags);
 
 /* ===================================================================== ProDiff
  * WaveNet denoiser -- replaces modules/decoder/wavenet.py:74-123 (WaveNet) as the

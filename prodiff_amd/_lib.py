@@ -40,6 +40,7 @@ _SIGS = {
     "pd_version": (C.c_int, []),
     "pd_profile_enable": (C.c_int, [C.c_int]),
     "pd_profile_summary": (C.c_int, [C.c_char_p, C.c_int]),
+    "pd_profile_filter": (C.c_int, [C.c_char_p]),
     "pd_wavenet_create": (C.c_int, [C.POINTER(pd_wavenet_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
     "pd_wavenet_destroy": (None, [_VP]),
     "pd_wavenet_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
@@ -113,6 +114,11 @@ def stream_ptr(device=None):
 
 def profile_enable(on=True):
     check(lib().pd_profile_enable(1 if on else 0))
+
+
+def profile_filter(tags=None):
+    """Record only these tags (None = all)."""
+    check(lib().pd_profile_filter(",".join(tags).encode() if tags else None))
 
 
 def profile_summary():

@@ -3,6 +3,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <string>
 #include <mutex>
 #include <vector>
 
@@ -358,12 +359,14 @@ int fill_normal(float* out, long long n, unsigned long long seed, unsigned strea
 namespace {
 struct ProfRec { const char* tag; int slot; };
 bool g_prof_on = false;
+std::string g_prof_filter;   // ",tag1,tag2," or empty (every tag)
 std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pool;
 std::vector<ProfRec> g_recs;
 }  // namespace
 
 ProfScope::ProfScope(const char* tag, hipStream_t st) : tag_(tag), st_(st), slot_(-1) {
   if (!g_prof_on || !tag) return;
+  if (!g_prof_filter.empty() && g_prof_filter.find("," + std::string(tag) + ",") == std::string::npos) return;
   slot_ = (int)g_recs.size();
   if ((size_t)slot_ >= g_pool.size()) {
     hipEvent_t a, b;
@@ -379,6 +382,11 @@ ProfScope::~ProfScope() {
 }
 
 }  // namespace pd
+
+extern "C" int pd_profile_filter(const char* tags) {
+  pd::g_prof_filter = (tags && *tags) ? "," + std::string(tags) + "," : std::string();
+  return PD_OK;
+}
 
 extern "C" int pd_profile_enable(int on) {
   pd::g_prof_on = on != 0;

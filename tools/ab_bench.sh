@@ -20,7 +20,7 @@ for envs in "$@"; do
   python - "$envs" $O/bench_$i.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-k = {t: v["avg_us"] for t, v in d["kernels"].items() if v["ms_total"] > 0.5}
+k = {t: v["avg_us"] for t, v in d["kernels"].items() if v["ms_total"] > 0.2}
 print(f"[{sys.argv[1]}] {d['ms_per_step']} ms/step", k)
 PY
 done
