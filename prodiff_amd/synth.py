@@ -126,6 +126,9 @@ def _gain(name):
     # a trained eps-network predicts ~N(0,1); keep the synthetic one there too
     if "final_conv" in name:
         return 0.2
+    # NSF-HiFiGAN output conv feeds a tanh: keep it out of saturation
+    if name.startswith("conv_post"):
+        return 0.3
     return 1.0
 
 
@@ -139,7 +142,7 @@ def synth_tensor(name, shape, seed):
         return (_gain(name) * (1.0 + 0.1 * z)).astype(np.float32)
     if name.endswith(".weight_v"):
         return z
-    if "upsample" in name:            # ConvTranspose1d [Cin, Cout, k]: 2 taps hit each output
+    if "upsample" in name or name.startswith("ups."):   # ConvTranspose1d [Cin, Cout, k]: 2 taps hit each output
         fan_in = shape[0] * 2
     else:
         fan_in = int(np.prod(shape[1:]))
@@ -161,3 +164,46 @@ def synth_inputs(seed, shape, kind="normal", loc=0.0, scale=1.0):
     if kind == "uniform":
         return rng.random(size=shape, dtype=np.float32)
     return (loc + scale * rng.standard_normal(size=shape, dtype=np.float32)).astype(np.float32)
+
+
+# NSF-HiFiGAN generator (modules/nsf_hifigan/models.py:208-265), plain (weight-norm
+# removed) keys in state-dict order.  Default dims are the SVS vocoder's
+# (handler/base_config.yaml:7-11: 128 mels, hop 512 = 8*8*2*2).
+NSF_DEFAULTS = dict(num_mels=128, upsample_initial_channel=512, upsample_rates=(8, 8, 2, 2),
+                    upsample_kernel_sizes=(16, 16, 4, 4), resblock="1", resblock_kernel_sizes=(3, 7, 11),
+                    resblock_dilation_sizes=((1, 3, 5), (1, 3, 5), (1, 3, 5)), sampling_rate=44100)
+
+
+def nsf_param_shapes(num_mels=128, upsample_initial_channel=512, upsample_rates=(8, 8, 2, 2),
+                     upsample_kernel_sizes=(16, 16, 4, 4), resblock="1", resblock_kernel_sizes=(3, 7, 11),
+                     resblock_dilation_sizes=((1, 3, 5), (1, 3, 5), (1, 3, 5)), harmonic_num=8, **_):
+    s = OrderedDict()
+    s["m_source.l_linear.weight"] = (1, harmonic_num + 1)
+    s["m_source.l_linear.bias"] = (1,)
+    ch0 = upsample_initial_channel
+    for i in range(len(upsample_rates)):
+        c = ch0 // 2 ** (i + 1)
+        if i + 1 < len(upsample_rates):
+            sf = int(np.prod(upsample_rates[i + 1:]))
+            s[f"noise_convs.{i}.weight"] = (c, 1, 2 * sf)
+        else:
+            s[f"noise_convs.{i}.weight"] = (c, 1, 1)
+        s[f"noise_convs.{i}.bias"] = (c,)
+    s["conv_pre.weight"] = (ch0, num_mels, 7)
+    s["conv_pre.bias"] = (ch0,)
+    for i, (u, k) in enumerate(zip(upsample_rates, upsample_kernel_sizes)):
+        s[f"ups.{i}.weight"] = (ch0 // 2 ** i, ch0 // 2 ** (i + 1), k)
+        s[f"ups.{i}.bias"] = (ch0 // 2 ** (i + 1),)
+    n = 0
+    for i in range(len(upsample_rates)):
+        c = ch0 // 2 ** (i + 1)
+        for k, d in zip(resblock_kernel_sizes, resblock_dilation_sizes):
+            names = ([f"convs1.{j}" for j in range(len(d))] + [f"convs2.{j}" for j in range(len(d))]
+                     if str(resblock) == "1" else [f"convs.{j}" for j in range(len(d))])
+            for nm in names:
+                s[f"resblocks.{n}.{nm}.weight"] = (c, c, k)
+                s[f"resblocks.{n}.{nm}.bias"] = (c,)
+            n += 1
+    s["conv_post.weight"] = (1, ch0 // 2 ** len(upsample_rates), 7)
+    s["conv_post.bias"] = (1,)
+    return s
