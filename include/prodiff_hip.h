@@ -199,6 +199,52 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
               const float* noise, unsigned long long seed, float* wav, int B, int Tc,
               void* workspace, size_t ws_bytes, void* stream);
 
+
+/* ==================================================================== NSF-HiFiGAN
+ * SVS vocoder -- replaces modules/nsf_hifigan/models.py:222-283
+ * (Generator, with SourceModuleHnNSF/SineGen :100-219 and ResBlock1/2 :36-97) as
+ * called by NsfHifiGAN.spec2wav_torch (component/vocoder/nsf_hifigan.py:29-56).
+ */
+typedef struct nsf_model nsf_model;
+
+typedef struct {
+  int num_mels;                    /* 128 (handler/base_config.yaml:7) */
+  int upsample_initial_channel;    /* 512 */
+  int num_upsamples;               /* len(upsample_rates) <= 6 */
+  int upsample_rates[6];           /* 8, 8, 2, 2 (hop 512) */
+  int upsample_kernel_sizes[6];    /* 16, 16, 4, 4; k % u == 0, k - u even */
+  int resblock;                    /* 1 (ResBlock1) or 2 (ResBlock2) */
+  int num_kernels;                 /* len(resblock_kernel_sizes) <= 4 */
+  int resblock_kernel_sizes[4];    /* 3, 7, 11 (odd, <= 11) */
+  int num_dilations;               /* len(resblock_dilation_sizes[j]) <= 4 */
+  int resblock_dilation_sizes[4][4];
+  int sampling_rate;               /* 44100 */
+  int harmonic_num;                /* 8 (models.py:229) */
+} nsf_dims;
+
+/* Parameter order = the reference state dict after remove_weight_norm (models.py:285-293):
+ *   m_source.l_linear.{weight,bias}, noise_convs.i.{weight,bias} (i < num_upsamples),
+ *   conv_pre.{weight,bias}, ups.i.{weight [Cin,Cout,k], bias},
+ *   resblocks.n.convs1.j / convs2.j (ResBlock1) or convs.j (ResBlock2) {weight,bias},
+ *   conv_post.{weight,bias}.  All device pointers, fp32. */
+int nsf_num_params(const nsf_dims* dims);
+int nsf_create(const nsf_dims* dims, const float* const* params, void* stream, nsf_model** out);
+void nsf_destroy(nsf_model* m);
+int nsf_hop(const nsf_model* m);   /* prod(upsample_rates) */
+size_t nsf_workspace_size(const nsf_model* m, int B, int T);
+
+/* spec2wav_torch(mel, f0=f0) for a batch of independent utterances:
+ *   mel [B,T,num_mels] time-major, scaled by mel_scale on load: 2.30259 turns the log10
+ *   mel of spec2wav_torch into the natural-log mel the Generator takes (nsf_hifigan.py:50-53);
+ *   1.0 is Generator.forward(c, f0) itself (models.py:265)
+ *   f0  [B,T] Hz (0 = unvoiced)
+ *   rand_ini [harmonic_num+1] (torch.rand(1,dim), models.py:139; element 0 ignored) and
+ *   noise [B, T*hop, harmonic_num+1] (randn_like, models.py:182), or NULL -> Philox from seed
+ *   wav [B, T*hop] output in [-1, 1]. */
+int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const float* f0, const float* rand_ini,
+                const float* noise, unsigned long long seed, float* wav, int B, int T,
+                void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

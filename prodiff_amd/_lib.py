@@ -34,6 +34,14 @@ class fd_dims(C.Structure):
                 ("step_embed_mid", C.c_int), ("step_embed_out", C.c_int)]
 
 
+class nsf_dims(C.Structure):
+    _fields_ = [("num_mels", C.c_int), ("upsample_initial_channel", C.c_int), ("num_upsamples", C.c_int),
+                ("upsample_rates", C.c_int * 6), ("upsample_kernel_sizes", C.c_int * 6), ("resblock", C.c_int),
+                ("num_kernels", C.c_int), ("resblock_kernel_sizes", C.c_int * 4), ("num_dilations", C.c_int),
+                ("resblock_dilation_sizes", (C.c_int * 4) * 4), ("sampling_rate", C.c_int),
+                ("harmonic_num", C.c_int)]
+
+
 _VP = C.c_void_p
 _SIGS = {
     "pd_last_error": (C.c_char_p, []),
@@ -62,6 +70,13 @@ _SIGS = {
     "fd_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                             C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, C.c_int,
                             C.c_int, _VP, C.c_size_t, _VP]),
+    "nsf_num_params": (C.c_int, [C.POINTER(nsf_dims)]),
+    "nsf_create": (C.c_int, [C.POINTER(nsf_dims), C.POINTER(_VP), _VP, C.POINTER(_VP)]),
+    "nsf_destroy": (None, [_VP]),
+    "nsf_hop": (C.c_int, [_VP]),
+    "nsf_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int]),
+    "nsf_forward": (C.c_int, [_VP, _VP, C.c_float, _VP, _VP, _VP, C.c_ulonglong, _VP, C.c_int, C.c_int, _VP, C.c_size_t,
+                              _VP]),
 }
 EXPORTS = tuple(_SIGS)
 

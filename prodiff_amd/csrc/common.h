@@ -52,7 +52,7 @@ const char* get_error();
 
 namespace pd {
 
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_MISH = 3, ACT_SWISH = 4 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_MISH = 3, ACT_SWISH = 4, ACT_TANH = 5 };
 
 __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
   switch (act) {
@@ -64,6 +64,7 @@ __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
       return v * tanhf(sp);
     }
     case ACT_SWISH: return v / (1.f + expf(-v));
+    case ACT_TANH: return tanhf(v);
     default: return v;
   }
 }

@@ -21,7 +21,7 @@
 namespace pd {
 
 constexpr int GEMM_BK = 32;
-constexpr int MAX_SEGS = 8;
+constexpr int MAX_SEGS = 12;   // NSF-HiFiGAN resblock convs have up to 11 taps
 
 struct Seg {
   const float* src;        // points at channel c_off of batch 0, row 0
@@ -45,7 +45,8 @@ enum Epi { EPI_STORE = 0, EPI_GATE = 1, EPI_RESSKIP = 2, EPI_POSTERIOR = 3 };
 enum GemmUse {
   U_WN_INPROJ = 0, U_WN_GATE = 1, U_WN_RESSKIP = 2, U_WN_SKIP = 3, U_WN_OUT = 4, U_WN_POSTERIOR = 5,
   U_FD_DBLOCK = 10, U_FD_KP_IN = 11, U_FD_KP_RES = 12, U_FD_KP_BIAS = 13, U_FD_KP_KERNEL = 14,
-  U_FD_LVC_PRECONV = 15
+  U_FD_LVC_PRECONV = 15,
+  U_NSF_CONV_PRE = 20, U_NSF_UPS = 21, U_NSF_RES = 22, U_NSF_POST = 23
 };
 
 struct GemmArgs {

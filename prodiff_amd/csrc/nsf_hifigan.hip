@@ -1,0 +1,496 @@
+// NSF-HiFiGAN generator on gfx950.
+//
+// Reference: modules/nsf_hifigan/models.py:222-283 (Generator), :100-219 (SineGen,
+// SourceModuleHnNSF), :36-97 (ResBlock1/2); called by NsfHifiGAN.spec2wav_torch
+// (component/vocoder/nsf_hifigan.py:29-56).
+//
+// Layout: every activation is time-major [B][t][c] (the ProDiff/FastDiff convention),
+// so the mel the acoustic model produces feeds conv_pre with no transpose.
+//  * harmonic source: the reference cumsums the per-sample phase increment in float64
+//    over the whole upsampled signal (models.py:136-161).  The increment is constant
+//    inside a frame (nearest upsampling), so sample t = f*upp + j has phase
+//    upp * P[f] + (j+1) * rad[f] with P the per-frame prefix: one short double scan per
+//    (utterance, harmonic), then every sample is independent.  The reference's
+//    "cumsum_shift" only adds whole cycles and leaves sin(2*pi*phase) unchanged.
+//  * Conv1d / ConvTranspose1d run on the implicit-GEMM engine (gemm.h, fp32 MFMA):
+//    a conv is one segment per tap; a ConvTranspose1d with stride u is u phase GEMMs
+//    (output rows t = q*u + o_phi, k/u taps each) whose epilogue also adds the
+//    noise_convs output (x = ups(x) + noise_conv(har), models.py:272-274).
+//  * ResBlock pre-activations (leaky_relu 0.1) and the 1/num_kernels average are
+//    applied on load by the consuming GEMM, so no elementwise pass materialises them.
+#include <algorithm>
+#include <vector>
+
+#include "../../include/prodiff_hip.h"
+#include "gemm.h"
+#include "kernels.h"
+
+using namespace pd;
+
+struct NsfConv {
+  const float* w = nullptr;   // packed [cout][taps * kpad]
+  const float* b = nullptr;
+  int taps = 0, dil = 1, cin = 0, cout = 0, kpad = 0;
+};
+
+struct NsfUps {
+  int u = 0, k = 0, cin = 0, cout = 0, ntap = 0, kpad = 0;
+  std::vector<const float*> w;   // per phase: packed [cout][ntap * kpad]
+  std::vector<int> qmin;         // per phase: first input row offset
+  const float* b = nullptr;
+  const float* nc_w = nullptr;   // noise conv [cout][nc_k]
+  const float* nc_b = nullptr;
+  int nc_k = 0, nc_stride = 1, nc_pad = 0;
+};
+
+struct nsf_model {
+  nsf_dims d{};
+  int dim = 9, C0 = 0, upp = 1;
+  float* pool = nullptr;
+  const float* lin_w = nullptr;
+  const float* lin_b = nullptr;
+  NsfConv pre, post;
+  std::vector<NsfUps> ups;
+  std::vector<NsfConv> res;      // [stage][kernel][conv] flattened in state-dict order
+  int convs_per_block = 0;
+};
+
+namespace {
+
+constexpr float NSF_LRELU = 0.1f;
+constexpr float NSF_SINE_AMP = 0.1f;     // SineGen defaults (models.py:118-119)
+constexpr float NSF_NOISE_STD = 0.003f;
+constexpr unsigned NSF_STREAM_INI = 0x4e534600u, NSF_STREAM_NOISE = 0x4e534601u;
+
+// rad_values of SineGen._f02sine (models.py:137-141), bit-for-bit in fp32:
+// fn = f0 * (h+1); rad = fmod(fn / sr, 1); frame 0 adds rand_ini[h] (rand_ini[0] = 0).
+__device__ __forceinline__ float nsf_rad(float f0, int h, int f, float sr, const float* rand_ini,
+                                         unsigned long long seed, int b, int dim) {
+  float fn = __fmul_rn(f0, (float)(h + 1));
+  float r = fmodf(__fdiv_rn(fn, sr), 1.0f);
+  if (f == 0 && h > 0) {
+    float ini = rand_ini ? rand_ini[h] : philox_uniform(seed, (unsigned long long)b * dim + h, NSF_STREAM_INI);
+    r = __fadd_rn(r, ini);
+  }
+  return r;
+}
+
+// P[b][f][h] = sum_{f' < f} rad[b][f'][h] in double (one thread per (b, h)).
+__global__ __launch_bounds__(64) void nsf_phase_prefix_kernel(const float* __restrict__ f0, int B, int T, int dim,
+                                                              float sr, const float* __restrict__ rand_ini,
+                                                              unsigned long long seed, double* __restrict__ P) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * dim) return;
+  int b = i / dim, h = i - b * dim;
+  double acc = 0.0;
+  for (int f = 0; f < T; ++f) {
+    P[((long long)b * T + f) * dim + h] = acc;
+    acc += (double)nsf_rad(f0[(long long)b * T + f], h, f, sr, rand_ini, seed, b, dim);
+  }
+}
+
+// har[b][t] = tanh(l_linear(sine_waves)) (models.py:168-219), one thread per sample.
+__global__ __launch_bounds__(256) void nsf_source_kernel(const float* __restrict__ f0, const double* __restrict__ P,
+                                                         int B, int T, int upp, int dim, float sr,
+                                                         const float* __restrict__ rand_ini,
+                                                         const float* __restrict__ noise, unsigned long long seed,
+                                                         const float* __restrict__ lw, const float* __restrict__ lb,
+                                                         float* __restrict__ har) {
+  const long long L = (long long)T * upp;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * L) return;
+  const int b = (int)(i / L);
+  const long long t = i - (long long)b * L;
+  const int f = (int)(t / upp), j = (int)(t - (long long)f * upp);
+  const float fv = f0[(long long)b * T + f];
+  const float uv = fv > 0.f ? 1.f : 0.f;
+  const float namp = uv * NSF_NOISE_STD + (1.f - uv) * NSF_SINE_AMP / 3.f;
+  float acc = 0.f;
+  for (int h = 0; h < dim; ++h) {
+    double ph = (double)upp * P[((long long)b * T + f) * dim + h] +
+                (double)(j + 1) * (double)nsf_rad(fv, h, f, sr, rand_ini, seed, b, dim);
+    ph -= floor(ph);
+    float s = (float)sin(ph * 6.283185307179586) * NSF_SINE_AMP;
+    long long ni = i * dim + h;
+    float z = noise ? noise[ni] : philox_normal(seed, (unsigned long long)ni, NSF_STREAM_NOISE);
+    acc = fmaf(lw[h], s * uv + namp * z, acc);
+  }
+  har[i] = tanhf(acc + lb[0]);
+}
+
+// noise_convs[i] (models.py:241-245): Conv1d(1, C, K, stride, pad) over har [B][L]
+// -> out [B][Tout][C] time-major.  One thread per output; har reads are shared
+// by the C consecutive threads of a row.
+__global__ __launch_bounds__(256) void nsf_noise_conv_kernel(const float* __restrict__ har, long long L,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ bias, int C, int K,
+                                                             int stride, int pad, long long Tout, int B,
+                                                             float* __restrict__ out) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * Tout * C) return;
+  const int o = (int)(i % C);
+  const long long r = i / C;
+  const int b = (int)(r / Tout);
+  const long long to = r - (long long)b * Tout;
+  const float* hb = har + (long long)b * L;
+  const float* wo = w + (long long)o * K;
+  float acc = bias[o];
+  long long s0 = to * stride - pad;
+  for (int j = 0; j < K; ++j) {
+    long long s = s0 + j;
+    if (s >= 0 && s < L) acc = fmaf(wo[j], hb[s], acc);
+  }
+  out[i] = acc;
+}
+
+// ConvTranspose1d weight [Cin][Cout][K] -> phase phi: dst[co][m*cpad + ci] = W[ci][co][phi + m*u]
+__global__ void nsf_pack_ups_kernel(float* __restrict__ dst, const float* __restrict__ src, int Cin, int Cout,
+                                    int K, int u, int phi, int ntap, int cpad) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)Cout * ntap * Cin) return;
+  int ci = (int)(i % Cin);
+  long long r = i / Cin;
+  int m = (int)(r % ntap);
+  int co = (int)(r / ntap);
+  dst[(long long)co * ntap * cpad + m * cpad + ci] = src[((long long)ci * Cout + co) * K + phi + m * u];
+}
+
+// xs = v (assign) or xs += v
+__global__ __launch_bounds__(256) void nsf_accum_kernel(float4* __restrict__ xs, const float4* __restrict__ v,
+                                                        long long n4, int assign) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 a = v[i];
+  if (!assign) {
+    float4 x = xs[i];
+    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+  }
+  xs[i] = a;
+}
+
+struct NsfWs {
+  size_t P = 0, har = 0, X = 0, T1 = 0, R = 0, XS = 0, src = 0, total = 0;   // float offsets
+};
+
+NsfWs nsf_layout(const nsf_model* m, int B, int T) {
+  NsfWs W;
+  auto al = [](size_t n) { return (n + 63) / 64 * 64; };
+  long long per_frame = m->C0;
+  long long len = 1;
+  for (const NsfUps& u : m->ups) {
+    len *= u.u;
+    per_frame = std::max(per_frame, len * u.cout);
+  }
+  size_t act = al((size_t)B * T * per_frame);
+  size_t off = 0;
+  W.P = off; off += al((size_t)B * T * m->dim * 2);
+  W.har = off; off += al((size_t)B * T * m->upp);
+  W.X = off; off += act;
+  W.T1 = off; off += act;
+  W.R = off; off += act;
+  W.XS = off; off += act;
+  W.src = off; off += act;
+  W.total = off * sizeof(float);
+  return W;
+}
+
+// conv over time-major `in` [B][Tl][cin] (taps with dilation, zero padding (taps-1)*dil/2),
+// pre-activation leaky_relu(alpha) * in_scale on load; out = act(conv + b) (+ res).
+int nsf_conv(const NsfConv& c, const float* in, float in_alpha, float in_scale, int B, int Tl, float* out,
+             const float* res, int act, hipStream_t st, int use) {
+  const int pad = (c.taps - 1) * c.dil / 2;
+  GemmArgs a = make_gemm(B, Tl, c.cout, c.w, c.taps * c.kpad, c.b, out, (long long)Tl * c.cout, c.cout);
+  for (int k = 0; k < c.taps; ++k) {
+    Seg s = make_seg(in, (long long)Tl * c.cin, c.cin, c.cin, k * c.dil - pad);
+    s.kpad = c.kpad;
+    if (in_alpha >= 0.f) { s.act = ACT_LRELU; s.alpha = in_alpha; }
+    s.scale = in_scale;
+    add_seg(a, s);
+  }
+  a.act = act;
+  if (res) { a.res = res; a.res_bs = (long long)Tl * c.cout; a.res_ld = c.cout; }
+  if (use == U_NSF_POST) return launch_gemm<1, 1, 4, 1, EPI_STORE, U_NSF_POST>(a, st, "nsf_post");
+  if (use == U_NSF_CONV_PRE) return launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_CONV_PRE>(a, st, "nsf_conv_pre");
+  return launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_RES>(a, st, "nsf_res");
+}
+
+}  // namespace
+
+extern "C" {
+
+int nsf_num_params(const nsf_dims* d) {
+  if (!d || d->num_upsamples < 1 || d->num_upsamples > 6 || d->num_kernels < 1 || d->num_kernels > 4 ||
+      d->num_dilations < 1 || d->num_dilations > 4 || (d->resblock != 1 && d->resblock != 2))
+    return -1;
+  int per_block = (d->resblock == 1 ? 2 : 1) * d->num_dilations;
+  return 2 + 2 * d->num_upsamples + 2 + 2 * d->num_upsamples + 2 * per_block * d->num_kernels * d->num_upsamples + 2;
+}
+
+int nsf_create(const nsf_dims* dims, const float* const* params, void* stream, nsf_model** out) {
+  PD_CHECK_ARG(dims && params && out, "null argument");
+  const int np = nsf_num_params(dims);
+  PD_CHECK_ARG(np > 0, "nsf_dims: bad counts");
+  for (int i = 0; i < np; ++i) PD_CHECK_ARG(params[i] != nullptr, "null parameter " + std::to_string(i));
+  const nsf_dims& d = *dims;
+  PD_CHECK_ARG(d.num_mels > 0 && d.num_mels % 4 == 0, "num_mels must be a multiple of 4");
+  PD_CHECK_ARG(d.harmonic_num >= 0 && d.sampling_rate > 0, "harmonic_num / sampling_rate");
+  PD_CHECK_ARG(d.upsample_initial_channel % (4 << d.num_upsamples) == 0,
+               "upsample_initial_channel / 2^num_upsamples must be a multiple of 4");
+  for (int j = 0; j < d.num_kernels; ++j)
+    PD_CHECK_ARG(d.resblock_kernel_sizes[j] % 2 == 1 && d.resblock_kernel_sizes[j] <= MAX_SEGS,
+                 "resblock kernel sizes must be odd and <= 11");
+  for (int i = 0; i < d.num_upsamples; ++i) {
+    int u = d.upsample_rates[i], k = d.upsample_kernel_sizes[i];
+    PD_CHECK_ARG(u >= 1 && k >= u && k % u == 0 && (k - u) % 2 == 0 && k / u <= MAX_SEGS,
+                 "upsample kernel must be a multiple of the rate with k - u even");
+  }
+  hipStream_t st = (hipStream_t)stream;
+  nsf_model* m = new nsf_model();
+  m->d = d;
+  m->dim = d.harmonic_num + 1;
+  m->C0 = d.upsample_initial_channel;
+  m->upp = 1;
+  for (int i = 0; i < d.num_upsamples; ++i) m->upp *= d.upsample_rates[i];
+  m->convs_per_block = (d.resblock == 1 ? 2 : 1) * d.num_dilations;
+
+  // --- pool layout (floats)
+  size_t off = 0;
+  auto take = [&](size_t n) { size_t o = off; off += (n + 63) / 64 * 64; return o; };
+  const int dim = m->dim;
+  size_t o_lin_w = take(dim), o_lin_b = take(1);
+  std::vector<size_t> o_nc_w, o_nc_b, o_ups_b;
+  std::vector<std::vector<size_t>> o_ups_w;
+  m->ups.resize(d.num_upsamples);
+  for (int i = 0; i < d.num_upsamples; ++i) {
+    NsfUps& U = m->ups[i];
+    U.u = d.upsample_rates[i];
+    U.k = d.upsample_kernel_sizes[i];
+    U.cin = m->C0 >> i;
+    U.cout = m->C0 >> (i + 1);
+    U.ntap = U.k / U.u;
+    U.kpad = round_up(U.cin, GEMM_BK);
+    if (i + 1 < d.num_upsamples) {
+      int sf = 1;
+      for (int r = i + 1; r < d.num_upsamples; ++r) sf *= d.upsample_rates[r];
+      U.nc_k = 2 * sf; U.nc_stride = sf; U.nc_pad = sf / 2;
+    } else {
+      U.nc_k = 1; U.nc_stride = 1; U.nc_pad = 0;
+    }
+    o_nc_w.push_back(take((size_t)U.cout * U.nc_k));
+    o_nc_b.push_back(take(U.cout));
+    const int p = (U.k - U.u) / 2;
+    std::vector<size_t> ph;
+    U.qmin.resize(U.u);
+    for (int phi = 0; phi < U.u; ++phi) {
+      ph.push_back(take((size_t)U.cout * U.ntap * U.kpad));
+      const int num = p - phi;              // first q with q*u + phi - p >= 0
+      U.qmin[phi] = num > 0 ? (num + U.u - 1) / U.u : 0;
+    }
+    o_ups_w.push_back(ph);
+    o_ups_b.push_back(take(U.cout));
+  }
+  auto conv_init = [&](NsfConv& c, int cin, int cout, int taps, int dil, size_t& ow, size_t& ob) {
+    c.cin = cin; c.cout = cout; c.taps = taps; c.dil = dil; c.kpad = round_up(cin, GEMM_BK);
+    ow = take((size_t)cout * taps * c.kpad);
+    ob = take(cout);
+  };
+  size_t o_pre_w, o_pre_b, o_post_w, o_post_b;
+  conv_init(m->pre, d.num_mels, m->C0, 7, 1, o_pre_w, o_pre_b);
+  std::vector<size_t> o_res_w, o_res_b;
+  for (int i = 0; i < d.num_upsamples; ++i) {
+    const int c = m->C0 >> (i + 1);
+    for (int j = 0; j < d.num_kernels; ++j) {
+      const int k = d.resblock_kernel_sizes[j];
+      for (int q = 0; q < m->convs_per_block; ++q) {
+        // ResBlock1: convs1.{0..D-1} (dilated) then convs2.{0..D-1} (dilation 1); ResBlock2: convs.{0..D-1}
+        int dil = (d.resblock == 1 && q >= d.num_dilations) ? 1 : d.resblock_dilation_sizes[j][q % d.num_dilations];
+        NsfConv cv;
+        size_t ow, ob;
+        conv_init(cv, c, c, k, dil, ow, ob);
+        m->res.push_back(cv);
+        o_res_w.push_back(ow);
+        o_res_b.push_back(ob);
+      }
+    }
+  }
+  conv_init(m->post, m->C0 >> d.num_upsamples, 1, 7, 1, o_post_w, o_post_b);
+
+  auto run = [&]() -> int {
+    PD_HIP(hipMalloc((void**)&m->pool, off * sizeof(float)));
+    PD_HIP(hipMemsetAsync(m->pool, 0, off * sizeof(float), st));
+    float* P = m->pool;
+    auto cp = [&](size_t o, const float* src, size_t n) -> int {
+      PD_HIP(hipMemcpyAsync(P + o, src, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+      return PD_OK;
+    };
+    int p = 0;
+    PD_TRY(cp(o_lin_w, params[p++], dim));
+    PD_TRY(cp(o_lin_b, params[p++], 1));
+    m->lin_w = P + o_lin_w;
+    m->lin_b = P + o_lin_b;
+    for (int i = 0; i < d.num_upsamples; ++i) {
+      NsfUps& U = m->ups[i];
+      PD_TRY(cp(o_nc_w[i], params[p++], (size_t)U.cout * U.nc_k));
+      PD_TRY(cp(o_nc_b[i], params[p++], U.cout));
+      U.nc_w = P + o_nc_w[i];
+      U.nc_b = P + o_nc_b[i];
+    }
+    PD_TRY(pack_conv(P + o_pre_w, 7 * m->pre.kpad, 0, 0, m->pre.kpad, params[p++], m->C0, d.num_mels, 7, st));
+    PD_TRY(cp(o_pre_b, params[p++], m->C0));
+    m->pre.w = P + o_pre_w;
+    m->pre.b = P + o_pre_b;
+    for (int i = 0; i < d.num_upsamples; ++i) {
+      NsfUps& U = m->ups[i];
+      const float* w = params[p++];
+      for (int phi = 0; phi < U.u; ++phi) {
+        long long n = (long long)U.cout * U.ntap * U.cin;
+        hipLaunchKernelGGL(nsf_pack_ups_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, P + o_ups_w[i][phi], w, U.cin,
+                           U.cout, U.k, U.u, phi, U.ntap, U.kpad);
+        PD_LAUNCH_CHECK();
+        U.w.push_back(P + o_ups_w[i][phi]);
+      }
+      PD_TRY(cp(o_ups_b[i], params[p++], U.cout));
+      U.b = P + o_ups_b[i];
+    }
+    for (size_t r = 0; r < m->res.size(); ++r) {
+      NsfConv& c = m->res[r];
+      PD_TRY(pack_conv(P + o_res_w[r], c.taps * c.kpad, 0, 0, c.kpad, params[p++], c.cout, c.cin, c.taps, st));
+      PD_TRY(cp(o_res_b[r], params[p++], c.cout));
+      c.w = P + o_res_w[r];
+      c.b = P + o_res_b[r];
+    }
+    PD_TRY(pack_conv(P + o_post_w, 7 * m->post.kpad, 0, 0, m->post.kpad, params[p++], 1, m->post.cin, 7, st));
+    PD_TRY(cp(o_post_b, params[p++], 1));
+    m->post.w = P + o_post_w;
+    m->post.b = P + o_post_b;
+    if (p != np) { set_error("nsf_create: parameter count mismatch"); return PD_ERR_ARG; }
+    return PD_OK;
+  };
+  int rc = run();
+  if (rc != PD_OK) {
+    if (m->pool) (void)hipFree(m->pool);
+    delete m;
+    return rc;
+  }
+  *out = m;
+  return PD_OK;
+}
+
+void nsf_destroy(nsf_model* m) {
+  if (!m) return;
+  (void)hipFree(m->pool);
+  delete m;
+}
+
+int nsf_hop(const nsf_model* m) { return m ? m->upp : 0; }
+
+size_t nsf_workspace_size(const nsf_model* m, int B, int T) {
+  if (!m || B < 0 || T < 0) return 0;
+  return nsf_layout(m, B, T).total;
+}
+
+int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const float* f0, const float* rand_ini, const float* noise,
+                unsigned long long seed, float* wav, int B, int T, void* workspace, size_t ws_bytes, void* stream) {
+  PD_CHECK_ARG(m && mel && f0 && wav && B >= 0 && T >= 0, "null argument");
+  if (B == 0 || T == 0) return PD_OK;
+  const NsfWs W = nsf_layout(m, B, T);
+  if (!workspace || ws_bytes < W.total) { set_error("workspace too small"); return PD_ERR_WORKSPACE; }
+  PD_CHECK_ARG((reinterpret_cast<uintptr_t>(mel) & 15) == 0, "mel must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = static_cast<float*>(workspace);
+  const nsf_dims& d = m->d;
+  const int dim = m->dim, nk = d.num_kernels;
+  const long long L = (long long)T * m->upp;
+  double* P = reinterpret_cast<double*>(ws + W.P);
+  float* har = ws + W.har;
+  float *X = ws + W.X, *T1 = ws + W.T1, *R = ws + W.R, *XS = ws + W.XS, *XSRC = ws + W.src;
+  const float sr = (float)d.sampling_rate;
+  {
+    ProfScope ps("nsf_source", st);
+    hipLaunchKernelGGL(nsf_phase_prefix_kernel, dim3(cdiv((long long)B * dim, 64)), dim3(64), 0, st, f0, B, T, dim,
+                       sr, rand_ini, seed, P);
+    hipLaunchKernelGGL(nsf_source_kernel, dim3(cdiv((long long)B * L, 256)), dim3(256), 0, st, f0, P, B, T, m->upp,
+                       dim, sr, rand_ini, noise, seed, m->lin_w, m->lin_b, har);
+  }
+  PD_LAUNCH_CHECK();
+  // conv_pre(mel_scale * mel^T) (nsf_hifigan.py:53, models.py:267)
+  {
+    const NsfConv& c = m->pre;
+    GemmArgs a = make_gemm(B, T, c.cout, c.w, 7 * c.kpad, c.b, XS, (long long)T * c.cout, c.cout);
+    for (int k = 0; k < 7; ++k) {
+      Seg s = make_seg(mel, (long long)T * d.num_mels, d.num_mels, d.num_mels, k - 3);
+      s.kpad = c.kpad;
+      s.scale = mel_scale;
+      add_seg(a, s);
+    }
+    PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_CONV_PRE>(a, st, "nsf_conv_pre")));
+  }
+  int Tin = T;
+  float in_scale = 1.f;
+  size_t r = 0;
+  for (int i = 0; i < d.num_upsamples; ++i) {
+    const NsfUps& U = m->ups[i];
+    const int Lc = Tin * U.u;
+    {
+      long long n = (long long)B * Lc * U.cout;
+      ProfScope ps("nsf_noise_conv", st);
+      hipLaunchKernelGGL(nsf_noise_conv_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, har, L, U.nc_w, U.nc_b, U.cout,
+                         U.nc_k, U.nc_stride, U.nc_pad, (long long)Lc, B, XSRC);
+      PD_LAUNCH_CHECK();
+    }
+    // x = ups(leaky_relu(x, 0.1)) + noise_conv(har)  (models.py:270-274), one GEMM per phase
+    const int p = (U.k - U.u) / 2;
+    for (int phi = 0; phi < U.u; ++phi) {
+      const int q0 = U.qmin[phi];
+      const int o = q0 * U.u + phi - p;        // first output row of this phase, in [0, u)
+      GemmArgs a = make_gemm(B, Tin, U.cout, U.w[phi], U.ntap * U.kpad, U.b, X + (long long)o * U.cout,
+                             (long long)Lc * U.cout, U.u * U.cout);
+      for (int mt = 0; mt < U.ntap; ++mt) {
+        Seg s = make_seg(XS, (long long)Tin * U.cin, U.cin, U.cin, q0 - mt);
+        s.kpad = U.kpad;
+        s.act = ACT_LRELU;
+        s.alpha = NSF_LRELU;
+        s.scale = in_scale;
+        add_seg(a, s);
+      }
+      a.res = XSRC + (long long)o * U.cout;
+      a.res_bs = (long long)Lc * U.cout;
+      a.res_ld = U.u * U.cout;
+      PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_UPS>(a, st, "nsf_ups")));
+    }
+    // xs = sum_j resblock_j(x); x = xs / num_kernels (models.py:275-281); the division is
+    // folded into the next consumer's load scale.
+    const long long n4 = (long long)B * Lc * U.cout / 4;
+    for (int j = 0; j < nk; ++j) {
+      float* target = j == 0 ? XS : R;
+      const float* cur = X;
+      for (int q = 0; q < d.num_dilations; ++q) {
+        if (d.resblock == 1) {
+          const NsfConv& c1 = m->res[r + q];
+          const NsfConv& c2 = m->res[r + d.num_dilations + q];
+          PD_TRY(nsf_conv(c1, cur, NSF_LRELU, 1.f, B, Lc, T1, nullptr, ACT_NONE, st, U_NSF_RES));
+          PD_TRY(nsf_conv(c2, T1, NSF_LRELU, 1.f, B, Lc, target, cur, ACT_NONE, st, U_NSF_RES));
+          cur = target;
+        } else {
+          // out must not alias the taps being read: ping-pong target <-> T1
+          float* dst = (cur == target) ? T1 : target;
+          PD_TRY(nsf_conv(m->res[r + q], cur, NSF_LRELU, 1.f, B, Lc, dst, cur, ACT_NONE, st, U_NSF_RES));
+          cur = dst;
+        }
+      }
+      r += m->convs_per_block;
+      if (j == 0 && cur == XS) continue;
+      ProfScope ps("nsf_accum", st);
+      hipLaunchKernelGGL(nsf_accum_kernel, dim3(cdiv(n4, 256)), dim3(256), 0, st, reinterpret_cast<float4*>(XS),
+                         reinterpret_cast<const float4*>(cur), n4, j == 0 ? 1 : 0);
+      PD_LAUNCH_CHECK();
+    }
+    Tin = Lc;
+    in_scale = 1.f / (float)nk;
+  }
+  // tanh(conv_post(leaky_relu(x, 0.01)))  (models.py:280-282)
+  PD_TRY(nsf_conv(m->post, XS, 0.01f, in_scale, B, Tin, wav, nullptr, ACT_TANH, st, U_NSF_POST));
+  return PD_OK;
+}
+
+}  // extern "C"

@@ -168,14 +168,14 @@ def synth_inputs(seed, shape, kind="normal", loc=0.0, scale=1.0):
 
 # NSF-HiFiGAN generator (modules/nsf_hifigan/models.py:208-265), plain (weight-norm
 # removed) keys in state-dict order.  Default dims are the SVS vocoder's
-# (handler/base_config.yaml:7-11: 128 mels, hop 512 = 8*8*2*2).
-NSF_DEFAULTS = dict(num_mels=128, upsample_initial_channel=512, upsample_rates=(8, 8, 2, 2),
-                    upsample_kernel_sizes=(16, 16, 4, 4), resblock="1", resblock_kernel_sizes=(3, 7, 11),
+# (handler/base_config.yaml:7-11: 128 mels, 44.1 kHz, hop 512 = 8*8*2*2*2).
+NSF_DEFAULTS = dict(num_mels=128, upsample_initial_channel=512, upsample_rates=(8, 8, 2, 2, 2),
+                    upsample_kernel_sizes=(16, 16, 4, 4, 4), resblock="1", resblock_kernel_sizes=(3, 7, 11),
                     resblock_dilation_sizes=((1, 3, 5), (1, 3, 5), (1, 3, 5)), sampling_rate=44100)
 
 
-def nsf_param_shapes(num_mels=128, upsample_initial_channel=512, upsample_rates=(8, 8, 2, 2),
-                     upsample_kernel_sizes=(16, 16, 4, 4), resblock="1", resblock_kernel_sizes=(3, 7, 11),
+def nsf_param_shapes(num_mels=128, upsample_initial_channel=512, upsample_rates=(8, 8, 2, 2, 2),
+                     upsample_kernel_sizes=(16, 16, 4, 4, 4), resblock="1", resblock_kernel_sizes=(3, 7, 11),
                      resblock_dilation_sizes=((1, 3, 5), (1, 3, 5), (1, 3, 5)), harmonic_num=8, **_):
     s = OrderedDict()
     s["m_source.l_linear.weight"] = (1, harmonic_num + 1)

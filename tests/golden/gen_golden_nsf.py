@@ -27,14 +27,15 @@ from modules.nsf_hifigan.models import Generator  # noqa: E402
 
 CASES = {
     # The reference SineGen is batch-1 only (models.py:162-163 concatenates a [1,1,dim] zero row).
-    # small channels, the SVS rates/kernels/resblocks
-    "nsf_c64_r8822": dict(synth.NSF_DEFAULTS, upsample_initial_channel=64, B=1, T=8, seed=41),
+    # small channels, hop 256 (8*8*2*2), the SVS kernels/resblocks
+    "nsf_c64_r8822": dict(synth.NSF_DEFAULTS, upsample_initial_channel=64, upsample_rates=(8, 8, 2, 2),
+                          upsample_kernel_sizes=(16, 16, 4, 4), B=1, T=8, seed=41),
     # ResBlock2, two upsamples
     "nsf_c32_r44_rb2": dict(synth.NSF_DEFAULTS, upsample_initial_channel=32, upsample_rates=(4, 4),
                             upsample_kernel_sizes=(8, 8), resblock="2", resblock_kernel_sizes=(3, 5),
                             resblock_dilation_sizes=((1, 3), (2, 6)), sampling_rate=22050, B=1, T=7, seed=42),
-    # the full SVS vocoder dims (512 channels), short input
-    "nsf_c512_full": dict(synth.NSF_DEFAULTS, B=1, T=3, seed=43),
+    # the full SVS vocoder dims (512 channels, hop 512), short input
+    "nsf_c512_full": dict(synth.NSF_DEFAULTS, B=1, T=2, seed=43),
 }
 
 

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def header_functions():
     txt = open(os.path.join(ROOT, "include", "prodiff_hip.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(pd_\w+|fd_\w+)\s*\(", txt, flags=re.M))
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(pd_\w+|fd_\w+|nsf_\w+)\s*\(", txt, flags=re.M))
 
 
 def test_library_exports_every_header_symbol():
