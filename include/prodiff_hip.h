@@ -228,7 +228,9 @@ typedef struct {
  *   resblocks.n.convs1.j / convs2.j (ResBlock1) or convs.j (ResBlock2) {weight,bias},
  *   conv_post.{weight,bias}.  All device pointers, fp32. */
 int nsf_num_params(const nsf_dims* dims);
-int nsf_create(const nsf_dims* dims, const float* const* params, void* stream, nsf_model** out);
+/* dtype PD_DTYPE_F32: exact fp32 (parity path); PD_DTYPE_BF16: bf16 weights/activations on the
+ * MFMA, fp32 accumulate, fp32 source module and epilogues. */
+int nsf_create(const nsf_dims* dims, const float* const* params, int dtype, void* stream, nsf_model** out);
 void nsf_destroy(nsf_model* m);
 int nsf_hop(const nsf_model* m);   /* prod(upsample_rates) */
 size_t nsf_workspace_size(const nsf_model* m, int B, int T);

@@ -71,7 +71,7 @@ _SIGS = {
                             C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, C.c_int,
                             C.c_int, _VP, C.c_size_t, _VP]),
     "nsf_num_params": (C.c_int, [C.POINTER(nsf_dims)]),
-    "nsf_create": (C.c_int, [C.POINTER(nsf_dims), C.POINTER(_VP), _VP, C.POINTER(_VP)]),
+    "nsf_create": (C.c_int, [C.POINTER(nsf_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
     "nsf_destroy": (None, [_VP]),
     "nsf_hop": (C.c_int, [_VP]),
     "nsf_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int]),

@@ -47,6 +47,8 @@ struct nsf_model {
   nsf_dims d{};
   int dim = 9, C0 = 0, upp = 1;
   float* pool = nullptr;
+  __bf16* pool_bf = nullptr;     // PD_DTYPE_BF16: bf16 mirror, registered with launch_gemm
+  size_t pool_n = 0;
   const float* lin_w = nullptr;
   const float* lin_b = nullptr;
   NsfConv pre, post;
@@ -226,10 +228,11 @@ int nsf_num_params(const nsf_dims* d) {
   return 2 + 2 * d->num_upsamples + 2 + 2 * d->num_upsamples + 2 * per_block * d->num_kernels * d->num_upsamples + 2;
 }
 
-int nsf_create(const nsf_dims* dims, const float* const* params, void* stream, nsf_model** out) {
+int nsf_create(const nsf_dims* dims, const float* const* params, int dtype, void* stream, nsf_model** out) {
   PD_CHECK_ARG(dims && params && out, "null argument");
   const int np = nsf_num_params(dims);
   PD_CHECK_ARG(np > 0, "nsf_dims: bad counts");
+  PD_CHECK_ARG(dtype == PD_DTYPE_F32 || dtype == PD_DTYPE_BF16, "dtype");
   for (int i = 0; i < np; ++i) PD_CHECK_ARG(params[i] != nullptr, "null parameter " + std::to_string(i));
   const nsf_dims& d = *dims;
   PD_CHECK_ARG(d.num_mels > 0 && d.num_mels % 4 == 0, "num_mels must be a multiple of 4");
@@ -364,11 +367,19 @@ int nsf_create(const nsf_dims* dims, const float* const* params, void* stream, n
     m->post.w = P + o_post_w;
     m->post.b = P + o_post_b;
     if (p != np) { set_error("nsf_create: parameter count mismatch"); return PD_ERR_ARG; }
+    m->pool_n = off;
+    if (dtype == PD_DTYPE_BF16) {
+      // every GEMM weight then streams as bf16 (v_mfma_f32_32x32x16_bf16, fp32 accumulate)
+      PD_HIP(hipMalloc((void**)&m->pool_bf, off * sizeof(__bf16)));
+      PD_TRY(convert_f32_bf16(m->pool, m->pool_bf, (long long)off, st));
+      register_bf16_pool(m->pool, off, m->pool_bf);
+    }
     return PD_OK;
   };
   int rc = run();
   if (rc != PD_OK) {
     if (m->pool) (void)hipFree(m->pool);
+    if (m->pool_bf) (void)hipFree(m->pool_bf);
     delete m;
     return rc;
   }
@@ -378,6 +389,10 @@ int nsf_create(const nsf_dims* dims, const float* const* params, void* stream, n
 
 void nsf_destroy(nsf_model* m) {
   if (!m) return;
+  if (m->pool_bf) {
+    unregister_bf16_pool(m->pool);
+    (void)hipFree(m->pool_bf);
+  }
   (void)hipFree(m->pool);
   delete m;
 }

@@ -90,6 +90,16 @@ class Generator(nn.Module):
         self._h = None
         self._sig = None
         self._ws = _lib.Workspace()
+        self.compute_dtype = "fp32"
+
+    def set_compute_dtype(self, dtype):
+        """"fp32" (exact parity path) or "bf16" (bf16 MFMA GEMMs, fp32 accumulate)."""
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(dtype)
+        if dtype != self.compute_dtype:
+            self._release()
+            self.compute_dtype = dtype
+        return self
 
     # ------------------------------------------------------------------ weights
     def load_state_dict(self, state_dict, strict=True):
@@ -156,7 +166,8 @@ class Generator(nn.Module):
         self._keep = params
         arr = (_lib.C.c_void_p * len(params))(*[p.data_ptr() for p in params])
         h = _lib.C.c_void_p()
-        _lib.check(L.nsf_create(C_byref(dims), arr, _lib.stream_ptr(dev), _lib.C.byref(h)))
+        dt = _lib.PD_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.PD_DTYPE_F32
+        _lib.check(L.nsf_create(C_byref(dims), arr, dt, _lib.stream_ptr(dev), _lib.C.byref(h)))
         self._h, self._sig = h, sig
         return h
 

@@ -80,3 +80,23 @@ def test_device_draws_deterministic_and_bounded():
     assert not torch.equal(a[0], a[1])
     # the draws only perturb the source: output stays near the golden one
     assert float((a[0].cpu() - torch.from_numpy(io["wav"][0])).abs().mean()) < 0.1
+
+
+def test_bf16_full_dims_vs_oracle():
+    """bf16 MFMA GEMMs: stated bar rel-L2 <= 2e-2 and max error <= 10% of max|ref| (as the
+    other bf16 paths)."""
+    h = dict(synth.NSF_DEFAULTS)
+    g, p = _gen(h, 7)
+    g.set_compute_dtype("bf16")
+    T, L = 24, 24 * 512
+    rng = np.random.default_rng(11)
+    mel = rng.normal(-2.0, 1.0, size=(1, T, 128)).astype(np.float32)
+    f0 = rng.uniform(60.0, 900.0, size=(1, T)).astype(np.float32)
+    ri = rng.random(9, dtype=np.float32)
+    nz = rng.standard_normal((1, L, 9), dtype=np.float32)
+    wav = g.synthesize(torch.from_numpy(mel).to(DEV), torch.from_numpy(f0).to(DEV), 2.30259,
+                       rand_ini=torch.from_numpy(ri), noise=torch.from_numpy(nz)).cpu().numpy()[0]
+    ref = ON.spec2wav(p, h, mel, f0, ri, nz)[0]
+    rel = float(np.linalg.norm(wav - ref) / np.linalg.norm(ref))
+    assert rel < 2e-2, rel
+    assert float(np.abs(wav - ref).max()) < 0.1 * float(np.abs(ref).max())
