@@ -19,6 +19,7 @@
 //  * ResBlock pre-activations (leaky_relu 0.1) and the 1/num_kernels average are
 //    applied on load by the consuming GEMM, so no elementwise pass materialises them.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/prodiff_hip.h"
@@ -121,28 +122,134 @@ __global__ __launch_bounds__(256) void nsf_source_kernel(const float* __restrict
 }
 
 // noise_convs[i] (models.py:241-245): Conv1d(1, C, K, stride, pad) over har [B][L]
-// -> out [B][Tout][C] time-major.  One thread per output; har reads are shared
-// by the C consecutive threads of a row.
+// -> out [B][Tout][C] time-major.  A block stages one window of har in LDS and
+// computes NC_ROWS rows per thread group; weights are stored tap-major [K][C] so a
+// tap's weights are one coalesced load, reused for NC_ROWS outputs.
+constexpr int NC_ROWS = 8;
 __global__ __launch_bounds__(256) void nsf_noise_conv_kernel(const float* __restrict__ har, long long L,
-                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ wt,
                                                              const float* __restrict__ bias, int C, int K,
-                                                             int stride, int pad, long long Tout, int B,
+                                                             int stride, int pad, long long Tout,
                                                              float* __restrict__ out) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long long)B * Tout * C) return;
-  const int o = (int)(i % C);
-  const long long r = i / C;
-  const int b = (int)(r / Tout);
-  const long long to = r - (long long)b * Tout;
+  extern __shared__ float s_har[];
+  const int CT = C < 256 ? C : 256, G = 256 / CT;
+  const int tid = threadIdx.x;
+  const int o = blockIdx.y * CT + tid % CT, rg = tid / CT;
+  const int b = blockIdx.z;
+  const long long row0 = (long long)blockIdx.x * G * NC_ROWS;
+  const int win = (G * NC_ROWS - 1) * stride + K;
   const float* hb = har + (long long)b * L;
-  const float* wo = w + (long long)o * K;
-  float acc = bias[o];
-  long long s0 = to * stride - pad;
-  for (int j = 0; j < K; ++j) {
-    long long s = s0 + j;
-    if (s >= 0 && s < L) acc = fmaf(wo[j], hb[s], acc);
+  const long long s0 = row0 * stride - pad;
+  for (int i = tid; i < win; i += 256) {
+    long long sidx = s0 + i;
+    s_har[i] = (sidx >= 0 && sidx < L) ? hb[sidx] : 0.f;
   }
-  out[i] = acc;
+  __syncthreads();
+  float acc[NC_ROWS];
+  const float bo = bias[o];
+#pragma unroll
+  for (int i = 0; i < NC_ROWS; ++i) acc[i] = bo;
+  for (int j = 0; j < K; ++j) {
+    const float w = wt[(long long)j * C + o];
+#pragma unroll
+    for (int i = 0; i < NC_ROWS; ++i) acc[i] = fmaf(w, s_har[(rg + G * i) * stride + j], acc[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < NC_ROWS; ++i) {
+    long long r = row0 + rg + G * i;
+    if (r < Tout) out[((long long)b * Tout + r) * C + o] = acc[i];
+  }
+}
+
+// noise conv weight [C][1][K] -> tap-major [K][C]
+__global__ void nsf_pack_noise_kernel(float* __restrict__ dst, const float* __restrict__ src, int C, int K) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * K) return;
+  int o = i / K, j = i - o * K;
+  dst[j * C + o] = src[i];
+}
+
+// Small-channel Conv1d (C in {4, 8, 16, 32}: the last ResBlock stages, where a 64-wide
+// GEMM tile would be 1/2 .. 1/16 empty and every tap re-reads the rows).  One block
+// stages TR + halo input rows (leaky_relu * scale applied once, on load) and the layer's
+// weights in LDS, then each thread accumulates RR rows x OC channels on the VALU in
+// fp32.  Rows are interleaved across threads (row = rg + i * NRG) and the LDS row pitch
+// is C + 1, so a wave's reads hit 32 distinct banks.
+template <int C>
+__global__ __launch_bounds__(256) void nsf_conv_small_kernel(const float* __restrict__ in, const float* __restrict__ wp,
+                                                             int ldw, int kpad, const float* __restrict__ bias,
+                                                             int taps, int dil, float alpha, float scale, int Tl,
+                                                             const float* __restrict__ res, float* __restrict__ out) {
+  constexpr int OC = C < 8 ? C : 8, NG = C / OC, NRG = 256 / NG, RR = 4, TR = NRG * RR, P = C + 1;
+  extern __shared__ float lds[];
+  const int pad = (taps - 1) * dil / 2;
+  const int win = TR + (taps - 1) * dil;
+  float* s_w = lds;                          // [tap][ci][co]
+  float* s_x = lds + taps * C * C;           // [win][P]
+  const int tid = threadIdx.x, b = blockIdx.y;
+  const int t0 = blockIdx.x * TR;
+  const float* ib = in + (long long)b * Tl * C;
+  for (int i = tid; i < taps * C * C; i += 256) {
+    int co = i % C, r = i / C, ci = r % C, k = r / C;
+    s_w[i] = wp[(long long)co * ldw + k * kpad + ci];
+  }
+  for (int i = tid; i < win * C; i += 256) {
+    int row = i / C, c = i - row * C;
+    int t = t0 - pad + row;
+    float v = 0.f;
+    if (t >= 0 && t < Tl) {
+      v = ib[(long long)t * C + c];
+      v = (v >= 0.f ? v : alpha * v) * scale;
+    }
+    s_x[row * P + c] = v;
+  }
+  __syncthreads();
+  const int og = tid % NG, rg = tid / NG;
+  float acc[RR][OC];
+#pragma unroll
+  for (int i = 0; i < RR; ++i)
+#pragma unroll
+    for (int c = 0; c < OC; ++c) acc[i][c] = bias[og * OC + c];
+  for (int k = 0; k < taps; ++k) {
+    const float* xk = s_x + (rg + k * dil) * P;
+    const float* wk = s_w + k * C * C + og * OC;
+#pragma unroll 4
+    for (int ci = 0; ci < C; ++ci) {
+      float w[OC];
+#pragma unroll
+      for (int c = 0; c < OC; ++c) w[c] = wk[ci * C + c];
+#pragma unroll
+      for (int i = 0; i < RR; ++i) {
+        const float x = xk[i * NRG * P + ci];
+#pragma unroll
+        for (int c = 0; c < OC; ++c) acc[i][c] = fmaf(w[c], x, acc[i][c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RR; ++i) {
+    const int t = t0 + rg + i * NRG;
+    if (t >= Tl) continue;
+    const long long o = ((long long)b * Tl + t) * C + og * OC;
+#pragma unroll
+    for (int c = 0; c < OC; ++c) out[o + c] = acc[i][c] + (res ? res[o + c] : 0.f);
+  }
+}
+
+template <int C>
+int launch_conv_small(const NsfConv& c, const float* in, float alpha, float scale, int B, int Tl, float* out,
+                      const float* res, hipStream_t st) {
+  constexpr int OC = C < 8 ? C : 8, NG = C / OC, TR = 256 / NG * 4;
+  const size_t lds = ((size_t)c.taps * C * C + (size_t)(TR + (c.taps - 1) * c.dil) * (C + 1)) * sizeof(float);
+  if (lds > 160 * 1024) { set_error("nsf conv: LDS window too large"); return PD_ERR_UNSUPPORTED; }
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&nsf_conv_small_kernel<C>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) { set_error("nsf conv: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
+  ProfScope ps("nsf_res_small", st);
+  hipLaunchKernelGGL(nsf_conv_small_kernel<C>, dim3(cdiv(Tl, TR), B), dim3(256), lds, st, in, c.w, c.taps * c.kpad,
+                     c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
 }
 
 // ConvTranspose1d weight [Cin][Cout][K] -> phase phi: dst[co][m*cpad + ci] = W[ci][co][phi + m*u]
@@ -196,10 +303,28 @@ NsfWs nsf_layout(const nsf_model* m, int B, int T) {
   return W;
 }
 
+// Channel counts up to this use nsf_conv_small_kernel (env PRODIFF_NSF_SMALL_MAX, default 16; 0 = off).
+int nsf_small_max() {
+  static int v = [] {
+    const char* e = getenv("PRODIFF_NSF_SMALL_MAX");
+    return e ? atoi(e) : 16;   // measured: 32 channels run faster on the bf16 GEMM
+  }();
+  return v;
+}
+
 // conv over time-major `in` [B][Tl][cin] (taps with dilation, zero padding (taps-1)*dil/2),
 // pre-activation leaky_relu(alpha) * in_scale on load; out = act(conv + b) (+ res).
 int nsf_conv(const NsfConv& c, const float* in, float in_alpha, float in_scale, int B, int Tl, float* out,
              const float* res, int act, hipStream_t st, int use) {
+  if (use == U_NSF_RES && c.cin == c.cout && c.cout <= nsf_small_max() && in_alpha >= 0.f) {
+    switch (c.cout) {
+      case 4: return launch_conv_small<4>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
+      case 8: return launch_conv_small<8>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
+      case 16: return launch_conv_small<16>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
+      case 32: return launch_conv_small<32>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
+      default: break;
+    }
+  }
   const int pad = (c.taps - 1) * c.dil / 2;
   GemmArgs a = make_gemm(B, Tl, c.cout, c.w, c.taps * c.kpad, c.b, out, (long long)Tl * c.cout, c.cout);
   for (int k = 0; k < c.taps; ++k) {
@@ -213,6 +338,7 @@ int nsf_conv(const NsfConv& c, const float* in, float in_alpha, float in_scale, 
   if (res) { a.res = res; a.res_bs = (long long)Tl * c.cout; a.res_ld = c.cout; }
   if (use == U_NSF_POST) return launch_gemm<1, 1, 4, 1, EPI_STORE, U_NSF_POST>(a, st, "nsf_post");
   if (use == U_NSF_CONV_PRE) return launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_CONV_PRE>(a, st, "nsf_conv_pre");
+  // (a 256 x 32 tile for the 32-channel stage measured slower: 11.9 vs 9.9 ms per step)
   return launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_RES>(a, st, "nsf_res");
 }
 
@@ -246,6 +372,8 @@ int nsf_create(const nsf_dims* dims, const float* const* params, int dtype, void
     int u = d.upsample_rates[i], k = d.upsample_kernel_sizes[i];
     PD_CHECK_ARG(u >= 1 && k >= u && k % u == 0 && (k - u) % 2 == 0 && k / u <= MAX_SEGS,
                  "upsample kernel must be a multiple of the rate with k - u even");
+    const int co = d.upsample_initial_channel >> (i + 1);
+    PD_CHECK_ARG(co >= 256 ? co % 256 == 0 : 256 % co == 0, "stage channels must divide 256 or be a multiple of it");
   }
   hipStream_t st = (hipStream_t)stream;
   nsf_model* m = new nsf_model();
@@ -333,7 +461,9 @@ int nsf_create(const nsf_dims* dims, const float* const* params, int dtype, void
     m->lin_b = P + o_lin_b;
     for (int i = 0; i < d.num_upsamples; ++i) {
       NsfUps& U = m->ups[i];
-      PD_TRY(cp(o_nc_w[i], params[p++], (size_t)U.cout * U.nc_k));
+      hipLaunchKernelGGL(nsf_pack_noise_kernel, dim3(cdiv((long long)U.cout * U.nc_k, 256)), dim3(256), 0, st,
+                         P + o_nc_w[i], params[p++], U.cout, U.nc_k);
+      PD_LAUNCH_CHECK();
       PD_TRY(cp(o_nc_b[i], params[p++], U.cout));
       U.nc_w = P + o_nc_w[i];
       U.nc_b = P + o_nc_b[i];
@@ -447,10 +577,11 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
     const NsfUps& U = m->ups[i];
     const int Lc = Tin * U.u;
     {
-      long long n = (long long)B * Lc * U.cout;
+      const int CT = U.cout < 256 ? U.cout : 256, G = 256 / CT;
+      const size_t lds = (size_t)((G * NC_ROWS - 1) * U.nc_stride + U.nc_k) * sizeof(float);
       ProfScope ps("nsf_noise_conv", st);
-      hipLaunchKernelGGL(nsf_noise_conv_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, har, L, U.nc_w, U.nc_b, U.cout,
-                         U.nc_k, U.nc_stride, U.nc_pad, (long long)Lc, B, XSRC);
+      hipLaunchKernelGGL(nsf_noise_conv_kernel, dim3(cdiv(Lc, G * NC_ROWS), U.cout / CT, B), dim3(256), lds, st, har,
+                         L, U.nc_w, U.nc_b, U.cout, U.nc_k, U.nc_stride, U.nc_pad, (long long)Lc, XSRC);
       PD_LAUNCH_CHECK();
     }
     // x = ups(leaky_relu(x, 0.1)) + noise_conv(har)  (models.py:270-274), one GEMM per phase
