@@ -1325,7 +1325,11 @@ __global__ __launch_bounds__(KP_THREADS, 2) void kp_kernel_bf16_kernel(const __b
       const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
       const int Rf = fw + fl;
       const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
-      if (Rf < rows) *reinterpret_cast<uint4*>(kout + (long long)Rf * KPERLAYER + ch) = v;
+      // streaming (non-temporal) store: 340 MB per launch, read back by the next launch from HBM
+      typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+      if (Rf < rows)
+        __builtin_nontemporal_store(u32x4_{v.x, v.y, v.z, v.w},
+                                    reinterpret_cast<u32x4_*>(kout + (long long)Rf * KPERLAYER + ch));
     }
     __syncthreads();                      // every wave is past its Ws reads (and Ot reads)
     if (t + 1 < te) KP_ST();
