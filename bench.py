@@ -1,22 +1,34 @@
 #!/usr/bin/env python
 """ProDiff 2-iter + FastDiff 4-iter end-to-end synthesis throughput on MI355X.
 
-One step = one pass of the hot path over one batch per GPU: the ProDiff x0-predict
+One step = one pass of the hot path over one batch: the ProDiff x0-predict
 sampler (WaveNet 20x256, M=80, 2 reverse steps) turns cond [B,861,256] into mel
 [B,861,80], the FastDiff sampler (base.yaml, 4 reverse steps) turns that into
-wav [B,220416] (10 s at 22.05 kHz, hop 256).  For N>1 every rank runs its own
-shard (weak scaling, no data-path collective) and the step ends with the
-point-to-point gather of mel+wav to rank 0 (RCCL over xGMI).
+wav [B,220416] (10 s at 22.05 kHz, hop 256).  Configurations (BASELINE.json):
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--frames T]
+  C3   (default at N=1)  8 utterances per GPU, bf16                   weak scaling
+  C4   (default at N>1)  32 utterances per GPU (256 at N=8), bf16     weak scaling
+  C4S                    256 utterances over all N GPUs, bf16         strong scaling
+  C2                     ProDiff 2-iter only, B=1, T=1000, fp32, mel-only (hipGraph replay)
+
+For N>1 every rank runs its LPT shard (pipeline.distributed_synthesize: no
+data-path collective) and the step ends with the ragged point-to-point gather of
+mel+wav to rank 0 (RCCL over xGMI).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3|C4|C4S|C2]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.  Synthetic inputs and random-init weights of the
+Without torchrun, ``--gpus N`` (N>1) re-launches itself as N ranks under
+torch.distributed.run before anything touches the GPU.  ``--dry-run`` runs the
+launcher, sharding and gather on CPU/gloo with a stub synthesizer (no GPU).
+Rank 0 prints ONE JSON line.  Synthetic inputs and random-init weights of the
 reference architectures (no checkpoints or datasets offline).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,15 +43,32 @@ METRIC = "mel-frames/sec + audio RTF, 2-iter ProDiff + 4-iter FastDiff @1/2/4/8 
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
 BF16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
+HOP, SAMPLE_RATE = 256, 22050
+
+CONFIGS = {
+    # name: (utterances per GPU or global, global?, frames, dtype, vocoder, description)
+    "C3": dict(batch=8, strong=False, frames=861, dtype="bf16", vocoder=True, timesteps=2,
+               desc="C3: ProDiff 2-iter (WaveNet 20x256, M=80, vpsde max_beta 40) + FastDiff 4-iter "
+                    "(base.yaml, hop 256), {b} x {t}-frame utterances per GPU"),
+    "C4": dict(batch=32, strong=False, frames=861, dtype="bf16", vocoder=True, timesteps=2,
+               desc="C4: 32 x {t}-frame utterances per GPU (256 at N=8), ProDiff 2-iter + FastDiff 4-iter, "
+                    "LPT utterance shards + RCCL gather to rank 0"),
+    "C4S": dict(batch=256, strong=True, frames=861, dtype="bf16", vocoder=True, timesteps=2,
+                desc="C4 strong scaling: {b} x {t}-frame utterances in total over all GPUs, ProDiff 2-iter + "
+                     "FastDiff 4-iter, LPT shards + RCCL gather"),
+    "C2": dict(batch=1, strong=False, frames=1000, dtype="fp32", vocoder=False, timesteps=2,
+               desc="C2: ProDiff 2-iter mel denoiser (WaveNet 20x256, M=80), B={b}, T={t}, fp32, mel only"),
+}
 
 
-def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
+def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256):
     """Algorithmic FLOPs (2 x MAC) of ONE launch of each tagged kernel.
     Tags used by several block sizes report the mean over their launches in one call."""
     F = B * T
     rows = [F * h for h in hops]
     d_rows = [F * 64, F * 8, F]                       # DBlock output rates (L/4, L/32, L/256)
     dblock = sum(2 * r * 32 * 96 * 2 + 2 * r * 32 * 128 for r in d_rows) / 9.0
+    kp_layers = 4 if dtype == "bf16" else 1           # bf16: one launch computes all 4 layers' kernels
     return {
         "wn_inproj": 2 * F * M * C,
         "wn_gate": 2 * F * 2 * C * (3 * C + H),
@@ -53,7 +82,7 @@ def flops_per_launch(B, T, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_kp_in": 2 * F * 64 * 80 * 5,
         "fd_kp_res": 2 * F * 64 * 64 * 3,
         "fd_kp_bias": 2 * F * 256 * 64 * 3,
-        "fd_kp_kernel": 2 * F * 6144 * 64 * 3,
+        "fd_kp_kernel": kp_layers * 2 * F * 6144 * 64 * 3,
         "fd_upsample": sum(2 * r * 32 * 64 for r in rows) / 3.0,
         "fd_lvc_preconv": sum(2 * r * 32 * 96 for r in rows) / 3.0,
         "fd_lvc": sum(2 * r * 64 * 96 for r in rows) / 3.0,
@@ -80,6 +109,7 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
     rows = [F * h for h in hops]
     per_row_io = 32 * 4
     kf_frame = 6144 * wb + 256 * 4
+    kp_layers = 4 if dtype == "bf16" else 1
     # fused LVC (hop >= 64): x read+write, audio_down read, this layer's kernels+biases
     lvc_f = [r * 3 * per_row_io + F * kf_frame for r in rows[1:]]
     lvc_v = [r * 4 * per_row_io + F * kf_frame for r in rows]          # unfused: x r/w, a, y
@@ -93,7 +123,8 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_first_conv": F * 256 * (1 + 32) * 4,
         # fused DBlock: strided input rows (32 ch) read once + output written once
         "fd_dblock_fused": sum(r * 2 * per_row_io for r in (F * 64, F * 8, F)) / 3.0,
-        "fd_kp_kernel": F * (64 * 4 + 6144 * wb) + 6144 * 192 * wb,
+        # h in (bf16 / fp32), every layer's 6144 kernel values per frame out, weights once
+        "fd_kp_kernel": F * (64 * wb + kp_layers * 6144 * wb) + kp_layers * 6144 * 192 * wb,
         "fd_kp_hidden": F * (80 + 64 + 256) * 4 + (64 * 480 + 6 * 64 * 192 + 256 * 192) * wb,
         "fd_lvc_fused": sum(lvc_f) / 2.0,
         # x in + a in + x out once per block, plus all 4 layers' kernels and biases
@@ -144,46 +175,79 @@ def pmc_traffic(tag, path=None):
     return None, None
 
 
-def step_flops(B, T):
-    """Whole-step algorithmic FLOPs: 2 x 26.43 + 4 x 56.98 MFLOP per frame."""
-    f = flops_per_launch(B, T)
-    per_prodiff_step = f["wn_inproj"] + 20 * (f["wn_gate"] + f["wn_resskip"]) + f["wn_skiphead"] + \
-        f["wn_outproj_posterior"]
-    per_fd_call = f["fd_first_conv"] + 9 * f["fd_dblock"] + 3 * (f["fd_kp_in"] + 6 * f["fd_kp_res"] +
-                                                             f["fd_kp_bias"] + 4 * f["fd_kp_kernel"] +
-                                                             f["fd_upsample"] + 4 * f["fd_lvc_preconv"] +
-                                                             4 * f["fd_lvc"]) + f["fd_final_update"]
-    return 2 * per_prodiff_step + 4 * per_fd_call
+def prodiff_step_flops(B, T, M=80, C=256, H=256):
+    """One denoiser call: 26.43 MFLOP per frame at M=80."""
+    f = flops_per_launch(B, T, M=M, C=C, H=H)
+    return f["wn_inproj"] + 20 * (f["wn_gate"] + f["wn_resskip"]) + f["wn_skiphead"] + f["wn_outproj_posterior"]
 
 
-def cpu_baseline(frames=200):
-    """The numpy oracle (a CPU port of the reference math, float64) on a bounded
-    sample: ONE utterance of `frames` mel frames through the same 2+4-iter pipeline."""
-    from oracle import oracle_fastdiff as OF
-    from oracle import oracle_prodiff as OP
-    from prodiff_amd import schedules as S
+def fastdiff_step_flops(B, T):
+    """One FastDiff eps-network call: 56.98 MFLOP per frame."""
+    f = flops_per_launch(B, T, dtype="fp32")          # per-layer kernel_conv entry
+    return (f["fd_first_conv"] + 9 * f["fd_dblock"] + f["fd_final_update"] +
+            3 * (f["fd_kp_in"] + 6 * f["fd_kp_res"] + f["fd_kp_bias"] + 4 * f["fd_kp_kernel"] +
+                 f["fd_upsample"] + 4 * f["fd_lvc_preconv"] + 4 * f["fd_lvc"]))
+
+
+def ref_cpu_baseline(config):
+    """The reference's own CPU path, timed by tools/ref_cpu_bench.py where
+    /root/reference exists (profiles/r02_ref_cpu.json; the GPU box has no reference)."""
+    path = os.path.join(ROOT, "profiles", "r02_ref_cpu.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    key = "C2" if config == "C2" else "C3"
+    e = d.get("configs", {}).get(key)
+    if not e:
+        return None
+    return {"value": e["mel_frames_per_s"], "unit": "mel-frames/s", "cores": d["threads"], "kind": "reference",
+            "sample": e["sample"], "rtf": e.get("rtf"), "host": d["host"],
+            "timing": f"median of {d['repeats']} after 1 warm-up, fp32, torch.no_grad", "source": os.path.relpath(path, ROOT)}
+
+
+def port_cpu_baseline(frames, vocoder=True):
+    """The torch-fp32 CPU restatement (oracle/oracle_torch.py, a port of the
+    reference math) timed on THIS host's cores on a bounded sample: one utterance
+    of `frames` mel frames through the same 2-iter ProDiff (+ 4-iter FastDiff)."""
+    from oracle import oracle_torch as OT
     from prodiff_amd import synth
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
-    except Exception:
-        cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    p = synth.synth_params(synth.wavenet_param_shapes(80, 256, 20, 256), 0)
-    bufs = OP.diffusion_buffers(OP.vpsde_betas(2, 40.0))
-    bufs["timesteps"] = 2
-    fp = OF.fold_weight_norm(synth.synth_params(synth.fastdiff_param_shapes(), 1))
-    b, a, s, st = S.fastdiff_infer_params(S.fastdiff_reverse_schedule(4), S.fastdiff_train_alpha())
-    cond = synth.synth_inputs(0, (1, frames, 256))
-    t0 = time.perf_counter()
-    mel = OP.prodiff_sample(p, bufs, cond, synth.synth_inputs(1, (1, 1, 80, frames), kind="uniform"),
-                            synth.synth_inputs(2, (2, 1, 1, 80, frames)))
-    OF.fastdiff_sample(fp, np.transpose(mel, (0, 2, 1)), synth.synth_inputs(3, (1, 1, frames * 256)),
-                       synth.synth_inputs(4, (3, 1, 1, frames * 256)), b, a, s, st)
-    dt = time.perf_counter() - t0
-    return {"value": round(frames / dt, 3), "unit": "mel-frames/s", "cores": int(cores), "kind": "port",
-            "sample": f"numpy float64 oracle, 1 utterance x {frames} frames ({frames * 256 / 22050:.2f} s audio), "
-                      f"2-iter ProDiff + 4-iter FastDiff, {dt:.1f} s wall",
-            "rtf": round(dt / (frames * 256 / 22050), 4)}
+    threads = torch.get_num_threads()
+    model = OT.PortModels(synth, seed=0)
+    cond = torch.from_numpy(synth.synth_inputs(0, (1, frames, 256)))
+
+    def run():
+        mel = model.prodiff(cond, seed=1)
+        if vocoder:
+            model.fastdiff(mel, seed=2)
+
+    run()                                     # warm-up
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        run()
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts))
+    audio_s = frames * HOP / SAMPLE_RATE
+    return {"value": round(frames / dt, 2), "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "sample": f"torch fp32 CPU restatement (oracle/oracle_torch.py), 1 utterance x {frames} frames "
+                      f"({audio_s:.2f} s audio), 2-iter ProDiff" + (" + 4-iter FastDiff" if vocoder else "") +
+                      f", median of 3 after 1 warm-up: {dt:.2f} s",
+            "rtf": round(dt / audio_s, 4)}
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def stub_synth(cond, seed):
+    """--dry-run stand-in for the Synthesizer (CPU, no compute worth timing)."""
+    B, T, _ = cond.shape
+    return cond[..., :80].clone(), torch.zeros(B, T * HOP)
 
 
 def main():
@@ -191,49 +255,97 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=8, help="utterances per GPU (C3: 8)")
-    ap.add_argument("--frames", type=int, default=861, help="mel frames per utterance (10 s @ 22.05 kHz/256)")
-    ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline sample length (0 = skip)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
-                    help="compute dtype (C3 is specified in bf16; fp32 is the exact parity path)")
+    ap.add_argument("--config", default="auto", choices=["auto"] + list(CONFIGS),
+                    help="auto: C3 at N=1, C4 (32 utterances per GPU) at N>1")
+    ap.add_argument("--batch", type=int, default=None, help="utterances per GPU (global for C4S)")
+    ap.add_argument("--frames", type=int, default=None, help="mel frames per utterance")
+    ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline_port sample length (0 = skip)")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
+                    help="compute dtype (default: the config's; fp32 is the exact parity path)")
+    ap.add_argument("--no-graph", action="store_true", help="C2: launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=2,
                     help="untimed steps with every launch bracketed by HIP events (the `kernels` table)")
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default: newest profiles/r*_v*_traffic.json)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo launcher + sharding + gather check, no GPU")
     args = ap.parse_args()
+
+    # ---- N ranks: re-launch under torch.distributed.run BEFORE anything touches the GPU
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    cfg_name = args.config if args.config != "auto" else ("C3" if world == 1 else "C4")
+    cfg = CONFIGS[cfg_name]
+    dtype = args.dtype or cfg["dtype"]
+    nb = args.batch or cfg["batch"]
+    T = args.frames or cfg["frames"]
+    dry = args.dry_run
+    if cfg_name == "C2" and world > 1:
+        raise SystemExit("C2 is a single-GPU latency config")
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group("gloo" if dry else "nccl", init_method="env://")
+        assert dist.get_world_size() == args.gpus
+    if dry:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
 
-    from prodiff_amd import _lib
-    from prodiff_amd.pipeline import HOP, SAMPLE_RATE, Synthesizer, gather_to_root
+    from prodiff_amd.pipeline import distributed_synthesize, lpt_shards
 
-    B, T = args.batch, args.frames
-    syn = Synthesizer.synthetic(dev, seed=0, dtype=args.dtype)
-    cond = torch.from_numpy(np.random.default_rng(1000 + rank).standard_normal((B, T, 256), dtype=np.float32)).to(dev)
+    # utterance list (all ranks know every length; only the own shard is resident)
+    n_total = nb if cfg["strong"] else nb * world
+    lengths = [T] * n_total
+    shards = lpt_shards(lengths, world)
+    mine = shards[rank]
+    B = len(mine)                                           # utterances this rank runs per step
+    rng = np.random.default_rng(1000 + rank)
+    conds = [(T, None)] * n_total
+    for i in mine:
+        conds[i] = torch.from_numpy(rng.standard_normal((T, 256), dtype=np.float32)).to(dev)
 
-    def step(i):
-        mel, wav = syn(cond, seed=10_000 * rank + i)
-        if world > 1:
-            gather_to_root(mel)
-            gather_to_root(wav)
-        return mel, wav
+    _lib = None
+    if dry:
+        synth_fn = stub_synth
+    else:
+        from prodiff_amd import _lib
+        from prodiff_amd.pipeline import Synthesizer
+        syn = Synthesizer.synthetic(dev, seed=0, dtype=dtype)
+        synth_fn = syn
 
-    fl = flops_per_launch(B, T)
-    by = bytes_per_launch(B, T, args.dtype)
+    if cfg["vocoder"]:
+        def step(i):
+            return distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev)
+    else:
+        # C2: the ProDiff sampler alone on one utterance (B=1), mel only
+        gd = syn.diffusion
+        cond_b = torch.stack([conds[i] for i in mine])
+        graph = None
+        if not args.no_graph:
+            graph = gd.capture(cond_b, seed=1)             # hipGraph of the whole 2-step sampler
+
+        def step(i):
+            if graph is not None:
+                return graph.replay()
+            return gd.sample(cond_b, seed=10_000 * i)
+
+    fl = flops_per_launch(B, T, dtype)
+    by = bytes_per_launch(B, T, dtype)
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
-    # Kernel timing.  An event pair costs GPU time at every launch it brackets (about
-    # 0.7 ms per step over all ~100 launches), so the per-kernel table comes from an
-    # untimed pass with every launch recorded, and the timed region records only the
-    # dominant kernel (the roofline's `avg_launch_us`, measured live in the timed steps).
-    timing = not args.no_kernel_timing
+    if not dry:
+        torch.cuda.synchronize()
+    # Kernel timing.  An event pair costs GPU time at every launch it brackets, so the
+    # per-kernel table comes from an untimed pass with every launch recorded, and the
+    # timed region records only the dominant kernel (the roofline's avg_launch_us).
+    timing = not (args.no_kernel_timing or dry or (cfg_name == "C2" and not args.no_graph))
     kern_all, dom, nprof = {}, None, 0
     if timing:
         nprof = max(1, args.prof_steps)
@@ -248,30 +360,40 @@ def main():
         dom = max(known.items(), key=lambda kv: kv[1][1])[0]
         _lib.profile_filter([dom])
         _lib.profile_enable(True)
-    torch.cuda.synchronize()
+    if not dry:
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    if not dry:
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        mel, wav = step(args.warmup + nprof + i)
-    torch.cuda.synchronize()
+        out = step(args.warmup + nprof + i)
+    if not dry:
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     kern = _lib.profile_summary() if timing else {}
-    _lib.profile_enable(False)
-    _lib.profile_filter(None)
+    if timing:
+        _lib.profile_enable(False)
+        _lib.profile_filter(None)
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    assert torch.isfinite(wav).all() and torch.isfinite(mel).all()
+    if rank == 0 and not dry:
+        if cfg["vocoder"]:
+            mels, wavs = out
+            assert len(mels) == n_total and all(torch.isfinite(m).all() for m in mels)
+            assert all(torch.isfinite(w).all() for w in wavs)
+        else:
+            assert torch.isfinite(out).all()
 
-    frames = B * T * world * args.steps
+    frames = n_total * T * args.steps
     audio_s = frames * HOP / SAMPLE_RATE
     ms_step = dt / args.steps * 1e3
-    peak_tf = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
+    peak_tf = BF16_PEAK_TFLOPS if dtype == "bf16" else FP32_PEAK_TFLOPS
     ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)          # FLOP/B where MFMA and HBM bounds meet
     roofline, kernels = None, {}
     if kern:
@@ -292,12 +414,14 @@ def main():
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
                         "frac": round(ach / peak_tf, 4)}
         traffic, tsrc = pmc_traffic(dom, args.traffic)
-        roofline.update({"traffic": round(traffic) if traffic else None, "traffic_source": tsrc, "kernel": dom, "flop_per_launch": fl[dom],
-                         "bytes_per_launch": by.get(dom), "intensity_flop_per_byte": round(intensity, 1),
-                         "ridge_flop_per_byte": round(ridge, 1), "avg_launch_us": round(ms / cnt * 1e3, 2),
-                         "launches": cnt, "share_of_step": round(ms / (dt * 1e3), 3),
+        roofline.update({"traffic": round(traffic) if traffic else None, "traffic_source": tsrc, "kernel": dom,
+                         "flop_per_launch": fl[dom], "bytes_per_launch": by.get(dom),
+                         "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(ridge, 1),
+                         "avg_launch_us": round(ms / cnt * 1e3, 2), "launches": cnt,
+                         "share_of_step": round(ms / (dt * 1e3), 3),
                          "timing": "HIP events around this kernel only, over the timed steps"})
-    out = {
+    step_fl = 2 * prodiff_step_flops(n_total, T) + (4 * fastdiff_step_flops(n_total, T) if cfg["vocoder"] else 0)
+    out_line = {
         "metric": METRIC,
         "value": round(frames / dt, 1),
         "unit": "mel-frames/s",
@@ -306,26 +430,31 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if cfg["strong"] else "weak",
         "vs_baseline": None,
-        "dtype": args.dtype,
+        "dtype": dtype,
         "data": "synthetic (cond ~ N(0,1)); random-init weights of the reference architectures; on-device Philox draws",
-        "config": {"workload": f"C3: ProDiff 2-iter (WaveNet 20x256, M=80, vpsde max_beta 40) + FastDiff 4-iter "
-                               f"(base.yaml, hop 256), {B} x {T}-frame utterances per GPU",
-                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world} (utterance shards, "
-                                                                           f"RCCL gather to rank 0)"},
+        "config": {"workload": cfg["desc"].format(b=nb, t=T), "name": cfg_name, "global_batch": n_total,
+                   "per_gpu_batch": B, "seq_len": T,
+                   "parallelism": f"dp{world} (utterance shards, RCCL gather to rank 0)" if cfg["vocoder"]
+                   else "single GPU" + ("" if args.no_graph else ", hipGraph replay")},
         "rtf": round(dt / audio_s, 6),
         "x_realtime": round(audio_s / dt, 1),
-        "model_tflops": round(step_flops(B, T) * world * args.steps / dt / 1e12, 2),
+        "model_tflops": round(step_fl * args.steps / dt / 1e12, 2),
         "roofline": roofline,
         "kernels": kernels,
-        "kernels_source": f"untimed pass of {nprof} steps, every launch bracketed by HIP events",
+        "kernels_source": f"untimed pass of {nprof} steps, every launch bracketed by HIP events" if kernels else None,
         "cpu_baseline": None,
+        "cpu_baseline_port": None,
+        "dry_run": dry,
     }
-    if rank == 0 and world == 1 and args.cpu_frames > 0:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_frames)
+    if rank == 0 and world == 1 and not dry:
+        out_line["cpu_baseline"] = ref_cpu_baseline(cfg_name)
+        if args.cpu_frames > 0:
+            out_line["cpu_baseline_port"] = port_cpu_baseline(args.cpu_frames if cfg["vocoder"] else T,
+                                                              vocoder=cfg["vocoder"])
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out_line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

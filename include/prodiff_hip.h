@@ -175,7 +175,20 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
               fd_model** out);
 void fd_destroy(fd_model* m);
 int fd_hop(const fd_model* m);   /* prod(upsample_ratios) = samples per mel frame */
+/* Workspace of fd_forward (S = 1) or fd_sample (S = N steps; bounded: steps run in chunks of
+ * 16, so the 200- and 1000-step schedules of fastdiff.py:58-61 need the 16-step size). */
 size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
+
+/* Kernel-variant options of a handle (bf16 LVC-block tiling and fusions).  The defaults are
+ * the measured production configuration; the tests select each variant.
+ * Set them before the handle's first forward/sample call; not thread-safe against calls. */
+#define FD_OPT_LVC_TS 0       /* whole-block LVC tile, hop >= 32: 384 (default), 256, 128; 0 = per-layer launches */
+#define FD_OPT_LVC_TS_SUB 1   /* whole-block LVC tile of the hop < 32 block: 128 (default), 256, 384 */
+#define FD_OPT_LVC_FUSE 2     /* 1: upsample / first conv / sampler update fused into the LVC blocks */
+#define FD_OPT_LVC_PF 3       /* 1: next-layer kernel fragments prefetched into registers (tile 384) */
+#define FD_OPT_LVC_SUB 4      /* 1: the hop < 32 block on the whole-block kernel too */
+#define FD_OPT_KP_SIDE 5      /* 1: kernel-predictor GEMMs of fd_sample on a low-priority side stream */
+int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */
 int fd_fold_weight_norm(float* w, const float* g, const float* v, int cout, int per_row,
@@ -234,6 +247,10 @@ int nsf_create(const nsf_dims* dims, const float* const* params, int dtype, void
 void nsf_destroy(nsf_model* m);
 int nsf_hop(const nsf_model* m);   /* prod(upsample_rates) */
 size_t nsf_workspace_size(const nsf_model* m, int B, int T);
+/* NSF_OPT_SMALL_MAX: ResBlock convs with at most this many channels run on the LDS/VALU small-channel
+ * kernel (default 16, measured; 0 = never).  Set before the first forward call. */
+#define NSF_OPT_SMALL_MAX 0
+int nsf_set_option(nsf_model* m, int option, int value);
 
 /* spec2wav_torch(mel, f0=f0) for a batch of independent utterances:
  *   mel [B,T,num_mels] time-major, scaled by mel_scale on load: 2.30259 turns the log10

@@ -14,6 +14,9 @@ LIB_PATH = os.environ.get("PRODIFF_HIP_LIB", os.path.join(_HERE, "libprodiff_hip
 PD_DTYPE_F32 = 0
 PD_DTYPE_BF16 = 1
 PD_REFLOW = {"euler": 0, "rk2": 1, "rk4": 2, "rk5": 3}
+# fd_set_option / nsf_set_option ids (include/prodiff_hip.h)
+FD_OPTIONS = {"lvc_ts": 0, "lvc_ts_sub": 1, "lvc_fuse": 2, "lvc_pf": 3, "lvc_sub": 4, "kp_side": 5}
+NSF_OPTIONS = {"small_max": 0}
 
 
 class HipError(RuntimeError):
@@ -65,6 +68,7 @@ _SIGS = {
     "fd_destroy": (None, [_VP]),
     "fd_hop": (C.c_int, [_VP]),
     "fd_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
+    "fd_set_option": (C.c_int, [_VP, C.c_int, C.c_int]),
     "fd_fold_weight_norm": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, _VP]),
     "fd_forward": (C.c_int, [_VP, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "fd_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
@@ -75,6 +79,7 @@ _SIGS = {
     "nsf_destroy": (None, [_VP]),
     "nsf_hop": (C.c_int, [_VP]),
     "nsf_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int]),
+    "nsf_set_option": (C.c_int, [_VP, C.c_int, C.c_int]),
     "nsf_forward": (C.c_int, [_VP, _VP, C.c_float, _VP, _VP, _VP, C.c_ulonglong, _VP, C.c_int, C.c_int, _VP, C.c_size_t,
                               _VP]),
 }

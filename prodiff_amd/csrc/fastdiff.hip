@@ -23,6 +23,7 @@ constexpr int HK = 64;   // kpnet hidden
 constexpr int NLY = 4;   // lvc layers per block
 constexpr int KPERLAYER = 2 * CI * CI * 3;   // 6144 kernel values per frame per layer
 constexpr int EMB_IN = 128, EMB_MID = 512, EMB_OUT = 512;
+constexpr int FD_STEP_CHUNK = 16;   // sampler steps whose embeddings / KP stacks are batched
 
 // Frame-major LVC kernel layout is MFMA-fragment order.  Within each tap the 32 input
 // channels are stored in the permuted order pos = lvc_pos(ci): position 16h + reg holds
@@ -54,15 +55,16 @@ struct fd_model {
   // Whole-block LVC tile per block kind (measured, r01_ab4): 384 output samples with the
   // next-layer kernel prefetch (8 waves, 1 block/CU, 256 VGPRs) for hop >= 32; 128 for the
   // hop-8 block, whose tiles span several frames (no prefetch).  lvc_ts = 0 selects one
-  // fused launch per layer (PRODIFF_LVC_TS, PRODIFF_LVC_TS_SUB, PRODIFF_LVC_PF).
+  // fused launch per layer.  Every field below is an fd_set_option (FD_OPT_*) with these
+  // measured defaults; the tests use the options to cover each variant.
   int lvc_ts = 384;
   int lvc_ts_sub = 128;
-  bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (PRODIFF_LVC_FUSE)
-  bool lvc_pf = true;          // next-layer kernel fragments prefetched into registers (PRODIFF_LVC_PF)
-  bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (PRODIFF_LVC_SUB)
+  bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (FD_OPT_LVC_FUSE)
+  bool lvc_pf = true;          // next-layer kernel fragments prefetched into registers (FD_OPT_LVC_PF)
+  bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (FD_OPT_LVC_SUB)
   // fd_sample (bf16): the kernel-predictor GEMMs run on a second, low-priority stream into a
   // ring of one K buffer per block, so step j+1's kernels for block n are written while
-  // step j's later blocks run (PRODIFF_KP_SIDE=1).  Created on first use.  Off by default:
+  // step j's later blocks run (FD_OPT_KP_SIDE).  Created on first use.  Off by default:
   // the two streams share the CUs, so each kernel slows down by about the time the overlap
   // saves (r01 ab_v16b: 7.41 vs 7.33 ms/step).
   bool kp_side = false;
@@ -1832,15 +1834,6 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   fd_model* m = new fd_model();
   m->nblocks = dims->num_blocks;
   m->dtype = dtype;
-  if (const char* e = getenv("PRODIFF_LVC_TS")) {   // A/B switches (bench/tests)
-    m->lvc_ts = atoi(e);
-    m->lvc_pf = m->lvc_ts >= 384;
-  }
-  if (const char* e = getenv("PRODIFF_LVC_TS_SUB")) m->lvc_ts_sub = atoi(e);
-  if (const char* e = getenv("PRODIFF_LVC_FUSE")) m->lvc_fuse = atoi(e) != 0;
-  if (const char* e = getenv("PRODIFF_LVC_PF")) m->lvc_pf = atoi(e) != 0;
-  if (const char* e = getenv("PRODIFF_LVC_SUB")) m->lvc_sub = atoi(e) != 0;
-  if (const char* e = getenv("PRODIFF_KP_SIDE")) m->kp_side = atoi(e) != 0;
   int hop = 1;
   for (int n = 0; n < m->nblocks; ++n) {
     m->ratios[n] = dims->upsample_ratios[n];
@@ -1989,7 +1982,29 @@ int fd_hop(const fd_model* m) { return m ? m->hops[m->nblocks - 1] : 0; }
 
 size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S) {
   if (!m || B < 0 || Tc < 0 || S < 1) return 0;
-  return fd_layout(m, B, Tc, S).total;
+  return fd_layout(m, B, Tc, S < FD_STEP_CHUNK ? S : FD_STEP_CHUNK).total;
+}
+
+int fd_set_option(fd_model* m, int option, int value) {
+  PD_CHECK_ARG(m, "null pointer");
+  switch (option) {
+    case FD_OPT_LVC_TS:
+      PD_CHECK_ARG(value == 0 || value == 128 || value == 256 || value == 384, "FD_OPT_LVC_TS in {0,128,256,384}");
+      m->lvc_ts = value;
+      m->lvc_pf = value >= 384;   // the register prefetch is tuned for the 384 tile
+      return PD_OK;
+    case FD_OPT_LVC_TS_SUB:
+      PD_CHECK_ARG(value == 128 || value == 256 || value == 384, "FD_OPT_LVC_TS_SUB in {128,256,384}");
+      m->lvc_ts_sub = value;
+      return PD_OK;
+    case FD_OPT_LVC_FUSE: m->lvc_fuse = value != 0; return PD_OK;
+    case FD_OPT_LVC_PF: m->lvc_pf = value != 0; return PD_OK;
+    case FD_OPT_LVC_SUB: m->lvc_sub = value != 0; return PD_OK;
+    case FD_OPT_KP_SIDE: m->kp_side = value != 0; return PD_OK;
+    default: break;
+  }
+  set_error("fd_set_option: unknown option " + std::to_string(option));
+  return PD_ERR_ARG;
 }
 
 int fd_forward(const fd_model* m, const float* audio, const float* cond, const float* steps, float* eps,
@@ -2017,8 +2032,12 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
               const float* steps, int N, const float* x_T, const float* noise, unsigned long long seed,
               float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream) {
   PD_CHECK_ARG(m && mel && beta && alpha && sigma && steps && wav && workspace, "null pointer");
-  PD_CHECK_ARG(B > 0 && Tc > 0 && N >= 1 && N <= 16, "bad B/T'/N");
-  FdWs W = fd_layout(m, B, Tc, N);
+  PD_CHECK_ARG(B > 0 && Tc > 0 && N >= 1, "bad B/T'/N");
+  // Long schedules (the 200- and 1000-step ones, fastdiff.py:58-61) run in chunks of
+  // FD_STEP_CHUNK steps: each chunk's step embeddings and kernel-predictor hidden stacks
+  // are computed in one batched launch, so the workspace is bounded by the chunk.
+  const int CH = N < FD_STEP_CHUNK ? N : FD_STEP_CHUNK;
+  FdWs W = fd_layout(m, B, Tc, CH);
   if (ws_bytes < W.total) { set_error("workspace too small"); return PD_ERR_WORKSPACE; }
   hipStream_t st = (hipStream_t)stream;
   float* ws = (float*)workspace;
@@ -2035,12 +2054,6 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
   } else {
     PD_TRY(fill_normal(cur, B * L, seed, 0xFFFF0001u, st));
   }
-  // every step's embedding at once: pass j uses n = N-1-j
-  std::vector<float> sv(N);
-  for (int j = 0; j < N; ++j) sv[j] = steps[N - 1 - j];
-  PD_TRY(fill_steps(ws + W.steps, sv.data(), N, B, st));
-  PD_TRY(fd_step_mlp(m, ws, W, N * B, st));
-  if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, mel, ws + W.nz, N, B, Tc, st));
   const bool side = fd_kp_side(m);
   if (side && !m->side) {
     int lo = 0, hi = 0;
@@ -2052,42 +2065,51 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
       PD_HIP(hipEventCreateWithFlags(&m->ev_lvc[b], hipEventDisableTiming));
     }
   }
-  if (side) {
-    PD_HIP(hipEventRecord(m->ev_hidden, st));
-    PD_HIP(hipStreamWaitEvent(m->side, m->ev_hidden, 0));
-  }
   const int nb = m->nblocks, rows = B * Tc;
-  for (int j = 0; j < N; ++j) {
-    const int n = N - 1 - j;
+  for (int j0 = 0; j0 < N; j0 += CH) {
+    const int nc = N - j0 < CH ? N - j0 : CH;
+    // the chunk's step embeddings at once: pass j uses n = N-1-j
+    std::vector<float> sv(nc);
+    for (int j = 0; j < nc; ++j) sv[j] = steps[N - 1 - (j0 + j)];
+    PD_TRY(fill_steps(ws + W.steps, sv.data(), nc, B, st));
+    PD_TRY(fd_step_mlp(m, ws, W, nc * B, st));
+    if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, mel, ws + W.nz, nc, B, Tc, st));
     if (side) {
-      // step j's kernels for every block; slot b is rewritten once step j-1's block b has run
-      for (int b = 0; b < nb; ++b) {
-        if (j > 0) PD_HIP(hipStreamWaitEvent(m->side, m->ev_lvc[b], 0));
-        const __bf16* hkb = reinterpret_cast<const __bf16*>(ws + W.hall) + ((size_t)j * nb + b) * rows * HK;
-        __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf) + (size_t)b * rows * NLY * KPERLAYER;
-        PD_TRY(kp_kernels_all(m->blk[b], hkb, Kb, B, Tc, m->side, true));
-        PD_HIP(hipEventRecord(m->ev_kp[b], m->side));
+      PD_HIP(hipEventRecord(m->ev_hidden, st));
+      PD_HIP(hipStreamWaitEvent(m->side, m->ev_hidden, 0));
+    }
+    for (int jl = 0; jl < nc; ++jl) {
+      const int j = j0 + jl, n = N - 1 - j;
+      if (side) {
+        // step j's kernels for every block; slot b is rewritten once step j-1's block b has run
+        for (int b = 0; b < nb; ++b) {
+          if (j > 0) PD_HIP(hipStreamWaitEvent(m->side, m->ev_lvc[b], 0));
+          const __bf16* hkb = reinterpret_cast<const __bf16*>(ws + W.hall) + ((size_t)jl * nb + b) * rows * HK;
+          __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf) + (size_t)b * rows * NLY * KPERLAYER;
+          PD_TRY(kp_kernels_all(m->blk[b], hkb, Kb, B, Tc, m->side, true));
+          PD_HIP(hipEventRecord(m->ev_kp[b], m->side));
+        }
       }
+      float* x = nullptr;
+      // x = (x - beta/sqrt(1-alpha^2) eps) / sqrt(1-beta) + [n>0] sigma z   (util.py:222-226)
+      const float ce = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
+      const float den = sqrtf(1.f - beta[n]);
+      const float sg = n > 0 ? sigma[n] : 0.f;
+      const FdFinal fin{other, noise ? noise + (size_t)j * B * L : (const float*)nullptr, ce, den, sg, seed,
+                        0x10000u + j};
+      PD_TRY(fd_net(m, ws, W, cur, mel, ws + W.nz + (size_t)jl * B * nb * CC, jl, B, Tc, &x, st,
+                    fused ? &fin : nullptr, side));
+      if (x == nullptr) {   // updated inside the last LVC block
+        std::swap(cur, other);
+        continue;
+      }
+      {
+        ProfScope ps("fd_final_update", st);
+        hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w,
+                           m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + j, L);
+      }
+      PD_LAUNCH_CHECK();
     }
-    float* x = nullptr;
-    // x = (x - beta/sqrt(1-alpha^2) eps) / sqrt(1-beta) + [n>0] sigma z   (util.py:222-226)
-    const float ce = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
-    const float den = sqrtf(1.f - beta[n]);
-    const float sg = n > 0 ? sigma[n] : 0.f;
-    const FdFinal fin{other, noise ? noise + (size_t)j * B * L : (const float*)nullptr, ce, den, sg, seed,
-                      0x10000u + j};
-    PD_TRY(fd_net(m, ws, W, cur, mel, ws + W.nz + (size_t)j * B * m->nblocks * CC, j, B, Tc, &x, st,
-                  fused ? &fin : nullptr, side));
-    if (x == nullptr) {   // updated inside the last LVC block
-      std::swap(cur, other);
-      continue;
-    }
-    {
-    ProfScope ps("fd_final_update", st);
-    hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w,
-                       m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + j, L);
-    }
-    PD_LAUNCH_CHECK();
   }
   if (cur != wav) PD_HIP(hipMemcpyAsync(wav, cur, sizeof(float) * B * L, hipMemcpyDeviceToDevice, st));
   return PD_OK;

@@ -32,6 +32,9 @@ struct NsfConv {
   const float* w = nullptr;   // packed [cout][taps * kpad]
   const float* b = nullptr;
   int taps = 0, dil = 1, cin = 0, cout = 0, kpad = 0;
+  // ResBlock convs with at most this many channels use nsf_conv_small_kernel (NSF_OPT_SMALL_MAX;
+  // measured: 32 channels run faster on the bf16 GEMM)
+  int small_max = 16;
 };
 
 struct NsfUps {
@@ -303,20 +306,11 @@ NsfWs nsf_layout(const nsf_model* m, int B, int T) {
   return W;
 }
 
-// Channel counts up to this use nsf_conv_small_kernel (env PRODIFF_NSF_SMALL_MAX, default 16; 0 = off).
-int nsf_small_max() {
-  static int v = [] {
-    const char* e = getenv("PRODIFF_NSF_SMALL_MAX");
-    return e ? atoi(e) : 16;   // measured: 32 channels run faster on the bf16 GEMM
-  }();
-  return v;
-}
-
 // conv over time-major `in` [B][Tl][cin] (taps with dilation, zero padding (taps-1)*dil/2),
 // pre-activation leaky_relu(alpha) * in_scale on load; out = act(conv + b) (+ res).
 int nsf_conv(const NsfConv& c, const float* in, float in_alpha, float in_scale, int B, int Tl, float* out,
              const float* res, int act, hipStream_t st, int use) {
-  if (use == U_NSF_RES && c.cin == c.cout && c.cout <= nsf_small_max() && in_alpha >= 0.f) {
+  if (use == U_NSF_RES && c.cin == c.cout && c.cout <= c.small_max && in_alpha >= 0.f) {
     switch (c.cout) {
       case 4: return launch_conv_small<4>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
       case 8: return launch_conv_small<8>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
@@ -528,6 +522,17 @@ void nsf_destroy(nsf_model* m) {
 }
 
 int nsf_hop(const nsf_model* m) { return m ? m->upp : 0; }
+
+int nsf_set_option(nsf_model* m, int option, int value) {
+  PD_CHECK_ARG(m, "null pointer");
+  if (option == NSF_OPT_SMALL_MAX) {
+    PD_CHECK_ARG(value >= 0, "NSF_OPT_SMALL_MAX >= 0");
+    for (auto& c : m->res) c.small_max = value;
+    return PD_OK;
+  }
+  set_error("nsf_set_option: unknown option " + std::to_string(option));
+  return PD_ERR_ARG;
+}
 
 size_t nsf_workspace_size(const nsf_model* m, int B, int T) {
   if (!m || B < 0 || T < 0) return 0;

@@ -133,6 +133,7 @@ class FastDiff(nn.Module):
         if use_weight_norm:
             self.apply_weight_norm()
         self.compute_dtype = "fp32"
+        self._options = {}
         self._h = None
         self._sig = None
         self._ws = _lib.Workspace()
@@ -142,6 +143,15 @@ class FastDiff(nn.Module):
         if dtype not in ("fp32", "bf16"):
             raise ValueError(dtype)
         self.compute_dtype = dtype
+        return self
+
+    def set_options(self, **opts):
+        """Kernel-variant options (fd_set_option, include/prodiff_hip.h FD_OPT_*): lvc_ts,
+        lvc_ts_sub, lvc_fuse, lvc_pf, lvc_sub, kp_side.  Unset ones keep the measured defaults."""
+        for k, v in opts.items():
+            if k not in _lib.FD_OPTIONS:
+                raise ValueError(f"unknown FastDiff option {k!r}")
+            self._options[k] = int(v)
         return self
 
     # ------------------------------------------------------- weight norm
@@ -175,7 +185,8 @@ class FastDiff(nn.Module):
         return seq
 
     def _param_sig(self):
-        return (self.compute_dtype,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+        return (self.compute_dtype, tuple(sorted(self._options.items()))) + \
+            tuple((p.data_ptr(), p._version) for p in self.parameters())
 
     def handle(self):
         sig = self._param_sig()
@@ -209,6 +220,11 @@ class FastDiff(nn.Module):
         h = _lib.C.c_void_p()
         dt = _lib.PD_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.PD_DTYPE_F32
         _lib.check(L.fd_create(_lib.C.byref(dims), arr, dt, st, _lib.C.byref(h)))
+        for k, v in self._options.items():
+            rc = L.fd_set_option(h, _lib.FD_OPTIONS[k], v)
+            if rc != 0:
+                L.fd_destroy(h)
+                _lib.check(rc)
         self._release()
         self._h, self._sig, self._keep = h, sig, keep
         return h

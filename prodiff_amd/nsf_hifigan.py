@@ -91,6 +91,16 @@ class Generator(nn.Module):
         self._sig = None
         self._ws = _lib.Workspace()
         self.compute_dtype = "fp32"
+        self._options = {}
+
+    def set_options(self, **opts):
+        """Kernel-variant options (nsf_set_option, include/prodiff_hip.h NSF_OPT_*): small_max."""
+        for k, v in opts.items():
+            if k not in _lib.NSF_OPTIONS:
+                raise ValueError(f"unknown NSF-HiFiGAN option {k!r}")
+            self._options[k] = int(v)
+        self._release()
+        return self
 
     def set_compute_dtype(self, dtype):
         """"fp32" (exact parity path) or "bf16" (bf16 MFMA GEMMs, fp32 accumulate)."""
@@ -168,6 +178,11 @@ class Generator(nn.Module):
         h = _lib.C.c_void_p()
         dt = _lib.PD_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.PD_DTYPE_F32
         _lib.check(L.nsf_create(C_byref(dims), arr, dt, _lib.stream_ptr(dev), _lib.C.byref(h)))
+        for k, v in self._options.items():
+            rc = L.nsf_set_option(h, _lib.NSF_OPTIONS[k], v)
+            if rc != 0:
+                L.nsf_destroy(h)
+                _lib.check(rc)
         self._h, self._sig = h, sig
         return h
 

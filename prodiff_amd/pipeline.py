@@ -77,16 +77,120 @@ def lpt_shards(lengths, world):
     return [sorted(s) for s in shards]
 
 
-def gather_to_root(t, root=0):
-    """Point-to-point gather of equally shaped per-rank tensors to `root`
-    (torch NCCL/RCCL implements gather as sends to the root).  Returns the
-    stacked tensor on root, None elsewhere."""
+def _numel(shape):
+    return int(np.prod(shape)) if len(shape) else 1
+
+
+def gather_to_root(t, root=0, shapes=None):
+    """Point-to-point gather of per-rank tensors of DIFFERENT shapes to `root`
+    (torch's NCCL backend -- RCCL on ROCm -- implements gather as sends to the
+    root; gloo on CPU).  Every rank passes a tensor of the same ndim and dtype.
+
+    The per-rank shapes are exchanged with one small all_gather unless the caller
+    already knows them (``shapes``: one tuple per rank, e.g. from the shard plan,
+    which saves that round trip).  Each rank's tensor is flattened and padded to
+    the largest size, gathered, and trimmed on the root.  Returns the list of
+    per-rank tensors (rank order) on the root, None elsewhere."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
-        return t[None]
-    world = dist.get_world_size()
-    if dist.get_rank() == root:
-        bufs = [torch.empty_like(t) for _ in range(world)]
-        dist.gather(t.contiguous(), gather_list=bufs, dst=root)
-        return torch.stack(bufs)
-    dist.gather(t.contiguous(), dst=root)
+        return [t]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = t.contiguous()
+    if shapes is None:
+        nd = t.dim()
+        mine = torch.zeros(1 + nd, dtype=torch.int64, device=t.device)
+        mine[0] = nd
+        if nd:
+            mine[1:] = torch.tensor(t.shape, dtype=torch.int64)
+        allv = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        shapes = []
+        for v in allv:
+            v = v.cpu().tolist()
+            if v[0] != nd:
+                raise ValueError("gather_to_root: ranks passed tensors of different ndim")
+            shapes.append(tuple(v[1:]))
+    shapes = [tuple(int(d) for d in s) for s in shapes]
+    if tuple(t.shape) != shapes[rank]:
+        raise ValueError(f"gather_to_root: rank {rank} tensor {tuple(t.shape)} != planned {shapes[rank]}")
+    n = max(_numel(s) for s in shapes)
+    flat = t.reshape(-1)
+    if flat.numel() < n:
+        flat = torch.cat([flat, flat.new_zeros(n - flat.numel())])
+    if rank == root:
+        bufs = [torch.empty(n, dtype=t.dtype, device=t.device) for _ in range(world)]
+        dist.gather(flat, gather_list=bufs, dst=root)
+        return [b[:_numel(s)].reshape(s) for b, s in zip(bufs, shapes)]
+    dist.gather(flat, dst=root)
     return None
+
+
+def length_groups(lengths, idx):
+    """Utterances `idx` grouped by exact length (a batch must share T: the
+    denoiser has no frame mask, so padding would change results near utterance
+    ends).  Returns [(T, [indices])] in descending T."""
+    groups = {}
+    for i in idx:
+        groups.setdefault(int(lengths[i]), []).append(int(i))
+    return sorted(groups.items(), key=lambda kv: -kv[0])
+
+
+def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None):
+    """Synthesize utterances sharded over the ranks of the default process group
+    (SURVEY §8(e)); the reference runs them one by one, B=1 per segment
+    (handler/infer/handler.py:373-388).
+
+    synth_fn(cond [B,T,H], seed) -> (mel [B,T,M], wav [B,T*hop]): one rank's
+      batched synthesis (a ``Synthesizer``).
+    conds: list over ALL utterances (same order on every rank) of [T_i,H] tensors
+      on this rank's device, or (T_i, callable returning one) pairs, so that only
+      this rank's shard is materialized.
+    Utterances are LPT-partitioned by length (``lpt_shards``); each rank runs its
+    shard in equal-length batches, flattens its outputs, and one ragged gather
+    per output kind brings them to the root, which un-permutes them.  The plan is
+    deterministic, so no shape exchange is needed.  Returns on the root the lists
+    [mel_i [T_i,M]], [wav_i [T_i*hop]] in input order; (None, None) elsewhere."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    lengths = [int(c.shape[0]) if torch.is_tensor(c) else int(c[0]) for c in conds]
+    shards = lpt_shards(lengths, world)
+    mel_parts, wav_parts, order = [], [], []
+    M = None
+    for g, (T, idx) in enumerate(length_groups(lengths, shards[rank])):
+        cb = torch.stack([conds[i] if torch.is_tensor(conds[i]) else conds[i][1]() for i in idx])
+        mel, wav = synth_fn(cb, seed + 7919 * g + 104729 * rank)
+        M = mel.shape[-1]
+        mel_parts.append(mel.reshape(-1))
+        wav_parts.append(wav.reshape(-1))
+        order += idx
+    dev = device
+    if dev is None:
+        dev = next((c.device for c in conds if torch.is_tensor(c)), torch.device("cpu"))
+    if M is None:     # an empty shard still takes part in the collectives
+        M = 0
+        mel_flat = torch.zeros(0, device=dev)
+        wav_flat = torch.zeros(0, device=dev)
+    else:
+        mel_flat, wav_flat = torch.cat(mel_parts), torch.cat(wav_parts)
+    if world == 1:
+        mels_all, wavs_all = [mel_flat], [wav_flat]
+    else:
+        # mel bins: known to every rank with a non-empty shard
+        mt = torch.tensor([M], device=mel_flat.device)
+        dist.all_reduce(mt, op=dist.ReduceOp.MAX)
+        M = int(mt.item())
+        mel_shapes = [(sum(lengths[i] for i in s) * M,) for s in shards]
+        wav_shapes = [(sum(lengths[i] for i in s) * hop,) for s in shards]
+        mels_all = gather_to_root(mel_flat, root, mel_shapes)
+        wavs_all = gather_to_root(wav_flat, root, wav_shapes)
+    if rank != root:
+        return None, None
+    mels, wavs = [None] * len(lengths), [None] * len(lengths)
+    for r, s in enumerate(shards):
+        mo, wo = 0, 0
+        for T, idx in length_groups(lengths, s):
+            for i in idx:
+                mels[i] = mels_all[r][mo:mo + T * M].reshape(T, M)
+                wavs[i] = wavs_all[r][wo:wo + T * hop]
+                mo += T * M
+                wo += T * hop
+    return mels, wavs

@@ -137,6 +137,18 @@ class WaveNet(nn.Module):
         return out
 
 
+class SampleGraph:
+    """A captured sampler (``GaussianDiffusion.capture``): static input, static output."""
+
+    def __init__(self, graph, cond, mel, keep=()):
+        self.graph, self.cond, self.mel = graph, cond, mel
+        self._keep = keep        # captured draw buffers stay alive with the graph
+
+    def replay(self):
+        self.graph.replay()
+        return self.mel
+
+
 class GaussianDiffusion(nn.Module):
     """x0-predict DDPM sampler (prodiff.py:48-159), fused on the GPU.
 
@@ -215,6 +227,29 @@ class GaussianDiffusion(nn.Module):
                                        _lib.fptr(xT), _lib.fptr(nz), seed, _lib.fptr(mel), B, T, ws, wsb,
                                        _lib.stream_ptr(dev)))
         return mel
+
+    @torch.no_grad()
+    def capture(self, cond, infer_step=4, seed=0, x_T=None, noise=None):
+        """Record the whole reverse process for cond's shape as ONE hipGraph.
+
+        The library's calls are stream-ordered and allocation-free, so
+        torch.cuda.CUDAGraph (hipGraph on ROCm) captures every launch of
+        ``pd_prodiff_sample``; a replay costs one graph launch instead of one
+        host launch per kernel -- the B=1 regime of the reference's per-step
+        loop (prodiff.py:148-150).  The draws are keyed by the captured ``seed``
+        (fixed across replays), or explicit ``x_T``/``noise`` draws are captured
+        by address (parity mode).  Returns a ``SampleGraph``: copy new conditions
+        into ``.cond`` and ``.replay()`` returns the static mel [B,T,M]."""
+        cond = cond.float().contiguous()
+        xT = None if x_T is None else x_T.float().contiguous().clone()
+        nz = None if noise is None else noise.float().contiguous().clone()
+        self.sample(cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz)   # packs weights, sizes the workspace
+        torch.cuda.synchronize()
+        static_cond = cond.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            mel = self.sample(static_cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz)
+        return SampleGraph(g, static_cond, mel, keep=(xT, nz))
 
     def forward(self, cond, src_spec=None, gt_spec=None, infer_step=4, infer=False):
         if not infer:

@@ -317,6 +317,59 @@ def gen_reflow():
              infer_step=S, cond=cond, x_T=x_T, x=x, out=out)
 
 
+# --------------------------------------------------------------------------
+# Full-size fixtures (SURVEY §8(c) fixture (vi)): C2 (ProDiff 2-iter, B=1, T=1000)
+# and a C3 slice (B=2 x 861 frames: ProDiff 2-iter -> FastDiff 4-iter).  Every
+# input and draw is regenerated from its seed by prodiff_amd.synth (see
+# FULLSIZE_CASES), so only outputs are stored: the full mel, the waveform at every
+# 8th sample, and per-utterance statistics of the whole waveform.
+# --------------------------------------------------------------------------
+FULLSIZE_CASES = {
+    # name: (B, T, prodiff weight seed, fastdiff weight seed or None, draw seed for FastDiff)
+    "fullsize_c2": (1, 1000, 61, None, None),
+    "fullsize_c3_b2": (2, 861, 62, 63, 64),
+}
+WAV_STRIDE = 8
+
+
+def gen_fullsize():
+    for name, (B, T, ps, fs, ds) in FULLSIZE_CASES.items():
+        M, H, L, C = 80, 256, 20, 256
+        net = WaveNet(M, H, L, C, 1)
+        gd = GaussianDiffusion(out_dims=M, denoise_fn=net, timesteps=2, time_scale=1000,
+                               schedule_type="vpsde", max_beta=40.0, spec_min=[-12], spec_max=[0]).eval()
+        load_synth(net, synth.wavenet_param_shapes(M, H, L, C), ps)
+        cond = synth.synth_inputs(ps + 300, (B, T, H))
+        with torch.no_grad(), Recorder(ps) as rec:
+            mel = gd(torch.from_numpy(cond), infer=True).numpy()
+        assert len(rec.rand) == 1 and len(rec.randn) == 2
+        out = dict(B=B, T=T, prodiff_seed=ps, mel=mel)
+        if fs is not None:
+            m, _ = build_fastdiff(fs)
+            dh = fd_util.compute_hyperparams_given_schedule(torch.linspace(1e-6, 0.01, 1000))
+            cnt = [0]
+
+            def std_normal(size):
+                a = synth.synth_inputs(ds * 1000 + cnt[0], tuple(size))
+                cnt[0] += 1
+                return torch.from_numpy(a)
+
+            orig = fd_util.std_normal
+            fd_util.std_normal = std_normal
+            try:
+                with torch.no_grad():
+                    wav = fd_util.sampling_given_noise_schedule(
+                        m, (B, 1, T * 256), dh, torch.FloatTensor(FASTDIFF_SCHEDULES[4]),
+                        condition=torch.from_numpy(mel).transpose(1, 2).contiguous()).numpy()[:, 0]
+            finally:
+                fd_util.std_normal = orig
+            assert cnt[0] == 4
+            w64 = wav.astype(np.float64)
+            out.update(fastdiff_seed=fs, draw_seed=ds, wav_stride=WAV_STRIDE, wav_sub=wav[:, ::WAV_STRIDE],
+                       wav_l2=np.linalg.norm(w64, axis=1), wav_mean=w64.mean(1), wav_absmax=np.abs(w64).max(1))
+        save(name, **out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:          # e.g. `gen_golden.py reflow` regenerates one family
         globals()["gen_" + sys.argv[1]]()
@@ -326,3 +379,4 @@ if __name__ == "__main__":
     gen_prodiff()
     gen_fastdiff()
     gen_reflow()
+    gen_fullsize()

@@ -1,0 +1,137 @@
+"""Parity at the sizes bench.py times (SURVEY §8(c) fixture (vi)).
+
+* C2 (ProDiff 2-iter, B=1, T=1000, fp32) against the reference's output, eager
+  and as a replayed hipGraph: |d| <= 1e-4.
+* A C3 slice (B=2 x 861 frames: ProDiff 2-iter -> FastDiff 4-iter, fp32) against
+  the reference: mel |d| <= 1e-4; waveform |d| <= 1e-4 at every 8th sample plus
+  the whole-waveform statistics (L2 norm, mean, max) to 1e-5 relative.
+* Full C3 (B=8 x 861) in bf16 against the fp32 HIP path with the SAME explicit
+  draws (the fp32 path is pinned to the reference above): mel and waveform within
+  the bf16 bar of tests/test_gpu_bf16.py.  This runs the grid-scale code the
+  bench times: thousands of 384-row LVC tiles, the XCD block remap with a block
+  count not divisible by 8, the kernel-predictor grouping, the 1.2 GB workspace.
+Every input and draw is regenerated from its seed (tests/golden/gen_golden.py,
+FULLSIZE_CASES), so only outputs are committed.
+"""
+import numpy as np
+import pytest
+import torch
+
+from prodiff_amd import FastDiff, GaussianDiffusion, WaveNet, synth
+from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
+from tests import golden_io as G
+from tests.bf16_bar import assert_bf16_close
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+ABS = 1e-4
+
+
+def tt(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def prodiff(seed, dtype="fp32"):
+    net = WaveNet(80, 256, 20, 256, 1)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in
+                         synth.synth_params(synth.wavenet_param_shapes(80, 256, 20, 256), seed).items()})
+    gd = GaussianDiffusion(80, net, timesteps=2, time_scale=1000, max_beta=40.0).to(DEV)
+    return gd.set_compute_dtype(dtype)
+
+
+def fastdiff(seed, dtype="fp32"):
+    m = FastDiff()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_params(synth.fastdiff_param_shapes(),
+                                                                             seed).items()})
+    return m.to(DEV).set_compute_dtype(dtype)
+
+
+def prodiff_draws(seed, B, T):
+    """The reference's torch.rand (x_T) then 2 x torch.randn, as gen_golden.Recorder drew them."""
+    xT = synth.synth_inputs(seed * 1000, (B, 1, 80, T), kind="uniform")
+    nz = np.stack([synth.synth_inputs(seed * 1000 + 1 + j, (B, 1, 80, T)) for j in range(2)])
+    return xT, nz
+
+
+def fastdiff_draws(seed, B, L):
+    xT = synth.synth_inputs(seed * 1000, (B, 1, L))
+    nz = np.stack([synth.synth_inputs(seed * 1000 + 1 + j, (B, 1, L)) for j in range(3)])
+    return xT, nz
+
+
+SCHED = fastdiff_infer_params(fastdiff_reverse_schedule(4), fastdiff_train_alpha())
+
+
+def test_c2_prodiff_fullsize_fp32():
+    d = G.load("fullsize_c2")
+    B, T, ps = int(d["B"]), int(d["T"]), int(d["prodiff_seed"])
+    gd = prodiff(ps)
+    cond = tt(synth.synth_inputs(ps + 300, (B, T, 256)))
+    xT, nz = prodiff_draws(ps, B, T)
+    mel = gd.sample(cond, x_T=tt(xT), noise=tt(nz)).cpu().numpy()
+    err = float(np.abs(mel - d["mel"]).max())
+    print(f"C2 fp32 max|d| = {err:.3e}")
+    assert err <= ABS
+    # the same sampler captured once and replayed as a hipGraph (bench.py --config C2)
+    g = gd.capture(cond, x_T=tt(xT), noise=tt(nz))
+    for _ in range(2):
+        out = g.replay()
+    torch.cuda.synchronize()
+    err_g = float(np.abs(out.cpu().numpy() - d["mel"]).max())
+    print(f"C2 fp32 hipGraph replay max|d| = {err_g:.3e}")
+    assert err_g <= ABS
+    # a new condition copied into the static input is picked up by the replay
+    g.cond.copy_(cond * 0.5)
+    ref2 = gd.sample(cond * 0.5, x_T=tt(xT), noise=tt(nz))
+    np.testing.assert_allclose(g.replay().cpu().numpy(), ref2.cpu().numpy(), rtol=0, atol=1e-6)
+
+
+@pytest.fixture(scope="module")
+def c3():
+    return G.load("fullsize_c3_b2")
+
+
+def test_c3_slice_prodiff_fp32(c3):
+    B, T, ps = int(c3["B"]), int(c3["T"]), int(c3["prodiff_seed"])
+    gd = prodiff(ps)
+    xT, nz = prodiff_draws(ps, B, T)
+    mel = gd.sample(tt(synth.synth_inputs(ps + 300, (B, T, 256))), x_T=tt(xT), noise=tt(nz)).cpu().numpy()
+    err = float(np.abs(mel - c3["mel"]).max())
+    print(f"C3-slice ProDiff fp32 max|d| = {err:.3e}")
+    assert err <= ABS
+
+
+def test_c3_slice_fastdiff_fp32(c3):
+    """The reference's own mel in, the reference's waveform out (4-iter, B=2, L=220416)."""
+    B, T = int(c3["B"]), int(c3["T"])
+    L = T * 256
+    m = fastdiff(int(c3["fastdiff_seed"]))
+    xT, nz = fastdiff_draws(int(c3["draw_seed"]), B, L)
+    b, a, s, st = SCHED
+    wav = m.sample(tt(c3["mel"]), b, a, s, st, x_T=tt(xT), noise=tt(nz))[:, 0].cpu().numpy().astype(np.float64)
+    sub = wav[:, ::int(c3["wav_stride"])]
+    err = float(np.abs(sub - c3["wav_sub"]).max())
+    print(f"C3-slice FastDiff fp32 max|d| (every 8th sample) = {err:.3e}, max|ref| = {np.abs(c3['wav_sub']).max():.2f}")
+    assert err <= ABS
+    np.testing.assert_allclose(np.linalg.norm(wav, axis=1), c3["wav_l2"], rtol=1e-5)
+    np.testing.assert_allclose(np.abs(wav).max(1), c3["wav_absmax"], rtol=1e-5)
+    np.testing.assert_allclose(wav.mean(1), c3["wav_mean"], rtol=0, atol=1e-6)
+
+
+def test_c3_full_bf16_vs_fp32():
+    """B=8 x 861 (the bench's C3 batch): bf16 sampler chain vs the fp32 HIP chain, same draws."""
+    B, T = 8, 861
+    L = T * 256
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    cond = torch.randn(B, T, 256, device=DEV, generator=gen)
+    xT = torch.rand(B, 1, 80, T, device=DEV, generator=gen)
+    nz = torch.randn(2, B, 1, 80, T, device=DEV, generator=gen)
+    mel32 = prodiff(0).sample(cond, x_T=xT, noise=nz)
+    mel16 = prodiff(0, "bf16").sample(cond, x_T=xT, noise=nz)
+    assert_bf16_close(mel16.cpu().numpy(), mel32.cpu().numpy(), "C3 ProDiff bf16 vs fp32, B=8x861")
+    wT = torch.randn(B, 1, L, device=DEV, generator=gen)
+    wn = torch.randn(3, B, 1, L, device=DEV, generator=gen)
+    b, a, s, st = SCHED
+    wav32 = fastdiff(1).sample(mel32, b, a, s, st, x_T=wT, noise=wn).cpu().numpy()
+    wav16 = fastdiff(1, "bf16").sample(mel32, b, a, s, st, x_T=wT, noise=wn).cpu().numpy()
+    assert_bf16_close(wav16, wav32, "C3 FastDiff bf16 vs fp32, B=8x861")

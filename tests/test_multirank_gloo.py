@@ -1,14 +1,24 @@
-"""N>1 path on CPU: utterance sharding (LPT) and the point-to-point gather to the
-root, world_size 2 over gloo (the GPU run uses the same code over RCCL)."""
+"""N>1 path on CPU: utterance sharding (LPT), the ragged point-to-point gather to
+the root and the un-permute back to input order, world sizes 2 and 3 over gloo
+(the GPU run uses the same code over RCCL); and bench.py's own N-rank launcher
+in its CPU dry-run mode."""
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from prodiff_amd.pipeline import gather_to_root, lpt_shards
+from prodiff_amd.pipeline import distributed_synthesize, gather_to_root, length_groups, lpt_shards
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOP = 4          # stub vocoder hop (keeps the test tensors small)
+M = 3
 
 
 def test_lpt_shards_balance_and_cover():
@@ -22,6 +32,22 @@ def test_lpt_shards_balance_and_cover():
     # equal lengths (C4): equal counts
     sh = lpt_shards([861] * 256, 8)
     assert all(len(s) == 32 for s in sh)
+    # more ranks than utterances: empty shards are allowed
+    sh = lpt_shards([5, 3], 4)
+    assert sorted(len(s) for s in sh) == [0, 0, 1, 1]
+
+
+def test_length_groups_exact():
+    g = length_groups([5, 9, 3, 7, 7, 2], [0, 3, 4, 5])
+    assert g == [(7, [3, 4]), (5, [0]), (2, [5])]
+
+
+def stub_synth(cond, seed):
+    """A deterministic stand-in for Synthesizer: per-utterance (independent of the
+    batch it runs in and of the seed), mel [B,T,M], wav [B,T*HOP]."""
+    mel = cond[..., :M] * 2.0 + 1.0
+    wav = torch.repeat_interleave(cond[..., 0], HOP, dim=1) - cond[..., 1].sum(1, keepdim=True)
+    return mel, wav
 
 
 def _free_port():
@@ -32,35 +58,68 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _conds(lengths):
+    g = torch.Generator().manual_seed(1234)
+    return [torch.randn(T, 8, generator=g) for T in lengths]
+
+
+def _worker(rank, world, port, q, lengths):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    lengths = [5, 9, 3, 7, 7, 2]
-    shards = lpt_shards(lengths, world)
-    mine = shards[rank]
-    # each rank "synthesises" its utterances: here a deterministic function of the index
-    out = torch.zeros(len(shards[0]) + 2, 4)
-    for j, i in enumerate(mine):
-        out[j] = float(i) + torch.arange(4, dtype=torch.float32) / 10
-    g = gather_to_root(out)
-    if rank == 0:
-        q.put((shards, g.numpy()))
-    dist.barrier()
-    dist.destroy_process_group()
+    try:
+        conds = _conds(lengths)
+        # only this rank's shard is materialized: the rest are (length, callable) stubs
+        mine = set(lpt_shards(lengths, world)[rank])
+        arg = [c if i in mine else (c.shape[0], None) for i, c in enumerate(conds)]
+        mels, wavs = distributed_synthesize(stub_synth, arg, hop=HOP)
+        # ragged gather with the shape exchange (no plan given)
+        t = torch.full((rank + 1, 2 + rank), float(rank))
+        g = gather_to_root(t)
+        if rank == 0:
+            q.put(([m.numpy() for m in mels], [w.numpy() for w in wavs], [x.numpy() for x in g]))
+        else:
+            assert mels is None and wavs is None and g is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
 
 
-def test_gather_to_root_world2():
+@pytest.mark.parametrize("world,lengths", [(2, [5, 9, 3, 7, 7, 2]), (3, [4, 11, 6, 6]), (2, [6])])
+def test_distributed_synthesize_ragged(world, lengths):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, lengths)) for r in range(world)]
     for p in procs:
         p.start()
-    shards, g = q.get(timeout=120)
+    mels, wavs, g = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert g.shape[0] == 2
-    for r, s in enumerate(shards):
-        for j, i in enumerate(s):
-            np.testing.assert_allclose(g[r, j], i + np.arange(4) / 10, rtol=0, atol=1e-6)
+    # every utterance back in input order, equal to running it alone
+    conds = _conds(lengths)
+    assert len(mels) == len(lengths) == len(wavs)
+    for i, c in enumerate(conds):
+        em, ew = stub_synth(c[None], 0)
+        np.testing.assert_array_equal(mels[i], em[0].numpy())
+        np.testing.assert_array_equal(wavs[i], ew[0].numpy())
+        assert mels[i].shape == (lengths[i], M) and wavs[i].shape == (lengths[i] * HOP,)
+    for r in range(world):
+        np.testing.assert_array_equal(g[r], np.full((r + 1, 2 + r), float(r)))
+
+
+def test_bench_self_launches_n_ranks_dry_run():
+    """`bench.py --gpus 2` without torchrun spawns 2 ranks itself (CPU dry run: gloo,
+    stub synthesis, no GPU) and rank 0 reports n_gpus 2."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                          "--warmup", "1", "--dry-run"], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["dry_run"] is True
+    assert d["config"]["global_batch"] == 2 * d["config"]["per_gpu_batch"]

@@ -116,3 +116,42 @@ def test_reflow_oracle(name):
     else:
         out = OR.denorm_spec(x, [-12.0], [0.0])
     assert np.abs(out - d["out"]).max() < 2e-5
+
+
+# ---------------------------------------------------------------- torch fp32 port
+# oracle_torch.py is the CPU line bench.py times on the GPU box (cpu_baseline_port);
+# pin it to the same reference goldens.
+def _tt(a):
+    import torch
+    return torch.as_tensor(np.asarray(a), dtype=torch.float32)
+
+
+def test_torch_port_prodiff_sample():
+    from oracle import oracle_torch as OT
+    d = G.load("prodiff_t2_m80")
+    p = {k: _tt(v) for k, v in G.prodiff_params("prodiff_t2_m80").items()}
+    mel = OT.prodiff_sample(p, G.prodiff_buffers(d), _tt(d["cond"]), _tt(d["x_T"]),
+                            [_tt(n) for n in d["noise"]]).numpy()
+    assert np.abs(mel - d["mel"]).max() < 1e-4
+
+
+def test_torch_port_fastdiff_sample():
+    from oracle import oracle_torch as OT
+    d = G.load("fastdiff_sample_n4")
+    s = G.load("schedules")
+    p = OT.fold_weight_norm(G.fastdiff_params(31))
+    b, a, sg, st = OF.infer_schedule(s["fd_n4_beta"], s["fd_train_alpha"])
+    wav = OT.fastdiff_sample(p, _tt(d["c"]), _tt(d["x_T"]), [_tt(n) for n in d["noise"]], b, a, sg, st).numpy()
+    assert np.abs(wav - d["wav"]).max() < 1e-4
+
+
+def test_torch_port_lvc_matches_numpy():
+    import torch
+    from oracle import oracle_torch as OT
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((2, 32, 5 * 8))
+    k = rng.standard_normal((2, 32, 64, 3, 5))
+    b = rng.standard_normal((2, 64, 5))
+    ref = OF.lvc(x, k, b, 8)
+    out = OT.lvc(_tt(x), _tt(k), _tt(b), 8).numpy()
+    assert np.abs(out - ref).max() < 1e-4

@@ -1,0 +1,143 @@
+"""Time the REFERENCE's own CPU path (SURVEY §8(d) CPU-baseline procedure).
+
+Runs only where /root/reference exists (this container; the GPU box has no reference):
+
+    PYTHONDONTWRITEBYTECODE=1 python tools/ref_cpu_bench.py [--threads N] [--repeats 5]
+
+Imports the reference modules read-only with the SURVEY §8(c) shims (lower-case
+``modules.fastdiff`` alias for FastDiff_model.py:4-5; ``Tensor.cuda`` as identity
+for the hard-coded ``.cuda()`` in util.py:68,214,424), loads the shared seeded
+synthetic weights (prodiff_amd.synth) and times, fp32 under torch.no_grad():
+
+  C3: ProDiff 2-iter (GaussianDiffusion + WaveNet 20x256, M=80, vpsde max_beta 40,
+      prodiff.py:136-153) on cond [8,861,256], then FastDiff 4-iter
+      (util.py:158-232 with the fastdiff.py:72-73 schedule) on the mel -> wav [8,1,220416]
+  C2: ProDiff 2-iter alone, B=1, T=1000
+
+1 warm-up + median of N timed runs.  Writes profiles/r02_ref_cpu.json, which
+bench.py reports as ``cpu_baseline`` (kind "reference").
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+sys.path.insert(0, REF)
+
+from prodiff_amd import synth  # noqa: E402
+
+torch.Tensor.cuda = lambda self, *a, **k: self          # shim (util.py:68,214,424)
+
+from modules.decoder.wavenet import WaveNet            # noqa: E402
+from modules.diffusion.prodiff import GaussianDiffusion  # noqa: E402
+import modules.FastDiff                                # noqa: E402
+import modules.FastDiff.module                         # noqa: E402
+import modules.FastDiff.module.modules as fd_modules   # noqa: E402
+import modules.FastDiff.module.util as fd_util         # noqa: E402
+sys.modules["modules.fastdiff"] = modules.FastDiff
+sys.modules["modules.fastdiff.module"] = modules.FastDiff.module
+sys.modules["modules.fastdiff.module.modules"] = fd_modules
+sys.modules["modules.fastdiff.module.util"] = fd_util
+from modules.FastDiff.module.FastDiff_model import FastDiff  # noqa: E402
+
+HOP, SR = 256, 22050
+SCHED4 = [3.2176e-04, 2.5743e-03, 2.5376e-02, 7.0414e-01]   # component/vocoder/fastdiff.py:72-73
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def build(seed=0):
+    net = WaveNet(80, 256, 20, 256, 1)
+    gd = GaussianDiffusion(out_dims=80, denoise_fn=net, timesteps=2, time_scale=1000, schedule_type="vpsde",
+                           max_beta=40.0, spec_min=[-12], spec_max=[0]).eval()
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in
+                         synth.synth_params(synth.wavenet_param_shapes(80, 256, 20, 256), seed).items()})
+    fd = FastDiff()
+    fd.load_state_dict({k: torch.from_numpy(v) for k, v in
+                        synth.synth_params(synth.fastdiff_param_shapes(), seed + 1).items()})
+    fd.remove_weight_norm()
+    dh = fd_util.compute_hyperparams_given_schedule(torch.linspace(1e-6, 0.01, 1000))
+    return gd, fd.eval(), dh
+
+
+def timed(fn, repeats):
+    fn()                                   # warm-up
+    ts = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", type=int, default=os.cpu_count())
+    ap.add_argument("--repeats", type=int, default=5)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02_ref_cpu.json"))
+    args = ap.parse_args()
+    torch.set_num_threads(args.threads)
+    gd, fd, dh = build()
+    res = {}
+
+    # C3: 8 x 10 s, ProDiff 2-iter + FastDiff 4-iter
+    B, T = 8, 861
+    cond = torch.from_numpy(synth.synth_inputs(0, (B, T, 256)))
+    split = {}
+
+    @torch.no_grad()
+    def c3():
+        t0 = time.perf_counter()
+        mel = gd(cond, infer=True)                                   # [B,T,80]
+        t1 = time.perf_counter()
+        fd_util.sampling_given_noise_schedule(fd, (B, 1, T * HOP), dh, torch.FloatTensor(SCHED4),
+                                              condition=mel.transpose(1, 2).contiguous())
+        split.setdefault("prodiff", []).append(t1 - t0)
+        split.setdefault("fastdiff", []).append(time.perf_counter() - t1)
+
+    med, ts = timed(c3, args.repeats)
+    audio = B * T * HOP / SR
+    res["C3"] = {"mel_frames_per_s": round(B * T / med, 2), "seconds_median": round(med, 3),
+                 "seconds_all": [round(t, 3) for t in ts], "rtf": round(med / audio, 4),
+                 "x_realtime": round(audio / med, 3),
+                 "prodiff_s_median": round(float(np.median(split["prodiff"][1:])), 3),
+                 "fastdiff_s_median": round(float(np.median(split["fastdiff"][1:])), 3),
+                 "sample": f"reference modules, B={B} x {T} frames ({audio:.1f} s audio), ProDiff 2-iter + "
+                           f"FastDiff 4-iter, fp32"}
+    print("C3", res["C3"], flush=True)
+
+    # C2: ProDiff 2-iter, B=1, T=1000
+    cond2 = torch.from_numpy(synth.synth_inputs(0, (1, 1000, 256)))
+    med2, ts2 = timed(torch.no_grad()(lambda: gd(cond2, infer=True)), args.repeats)
+    res["C2"] = {"mel_frames_per_s": round(1000 / med2, 2), "seconds_median": round(med2, 4),
+                 "seconds_all": [round(t, 4) for t in ts2], "rtf": round(med2 / (1000 * 512 / 44100), 4),
+                 "sample": "reference modules, ProDiff 2-iter, B=1 x 1000 frames, M=80, fp32, mel only"}
+    print("C2", res["C2"], flush=True)
+
+    out = {"host": f"{cpu_model()}, {os.cpu_count()} vCPUs (survey container, no GPU)",
+           "threads": args.threads, "repeats": args.repeats, "torch": torch.__version__,
+           "reference": REF, "script": "tools/ref_cpu_bench.py", "configs": res}
+    with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", args.out)
+
+
+if __name__ == "__main__":
+    main()
