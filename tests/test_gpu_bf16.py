@@ -12,7 +12,7 @@ from prodiff_amd import FastDiff, GaussianDiffusion, WaveNet, synth
 from prodiff_amd.fastdiff import sampling_given_noise_schedule
 from tests import golden_io as G
 
-from tests.bf16_bar import assert_bf16_close
+from tests.bf16_bar import EPS_REL_L2, EPS_REL_MAX, assert_bf16_close
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -60,7 +60,7 @@ def test_fastdiff_forward_bf16(fd16):
     m, _ = fd16
     d = G.load("fastdiff_fwd")
     eps = m((tt(d["audio"]), tt(d["c"]), tt(d["steps"]))).cpu().numpy()
-    assert_bf16_close(eps, d["eps"], "fastdiff_fwd")
+    assert_bf16_close(eps, d["eps"], "fastdiff_fwd", EPS_REL_L2, EPS_REL_MAX)
 
 
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5)])
@@ -71,7 +71,8 @@ def test_fastdiff_forward_bf16_oracle(fd16, B, Tc):
     c = synth.synth_inputs(B + 50 * Tc + 1, (B, 80, Tc), loc=-5.0, scale=2.0)
     st = np.full((B, 1), 23.4676, np.float32)
     eps = m((tt(audio), tt(c), tt(st))).cpu().numpy()
-    assert_bf16_close(eps, OF.fastdiff_forward(pf, audio, c, st), f"fastdiff_fwd B={B} Tc={Tc}")
+    assert_bf16_close(eps, OF.fastdiff_forward(pf, audio, c, st), f"fastdiff_fwd B={B} Tc={Tc}", EPS_REL_L2,
+                      EPS_REL_MAX)
 
 
 def test_fastdiff_sample_bf16(fd16):
@@ -99,7 +100,7 @@ def test_fastdiff_lvc_block_bf16(ts, B, Tc):
     st = np.full((B, 1), 41.5, np.float32)
     eps = m((tt(audio), tt(c), tt(st))).cpu().numpy()
     assert_bf16_close(eps, OF.fastdiff_forward(OF.fold_weight_norm(p), audio, c, st),
-                      f"lvc_block ts={ts} B={B} Tc={Tc}")
+                      f"lvc_block ts={ts} B={B} Tc={Tc}", EPS_REL_L2, EPS_REL_MAX)
 
 
 @pytest.mark.parametrize("fuse", [0, 1])
