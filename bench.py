@@ -268,6 +268,8 @@ def main():
                     help="untimed steps with every launch bracketed by HIP events (the `kernels` table)")
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default: newest profiles/r*_v*_traffic.json)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo launcher + sharding + gather check, no GPU")
+    ap.add_argument("--fd-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="FastDiff kernel-variant option for A/B runs (fd_set_option, e.g. lvc_stream=0)")
     args = ap.parse_args()
 
     # ---- N ranks: re-launch under torch.distributed.run BEFORE anything touches the GPU
@@ -318,6 +320,8 @@ def main():
         from prodiff_amd import _lib
         from prodiff_amd.pipeline import Synthesizer
         syn = Synthesizer.synthetic(dev, seed=0, dtype=dtype)
+        if args.fd_opt:
+            syn.vocoder.model.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.fd_opt)})
         synth_fn = syn
 
     if cfg["vocoder"]:

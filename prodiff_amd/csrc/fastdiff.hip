@@ -62,6 +62,7 @@ struct fd_model {
   bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (FD_OPT_LVC_FUSE)
   bool lvc_pf = true;          // next-layer kernel fragments prefetched into registers (FD_OPT_LVC_PF)
   bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (FD_OPT_LVC_SUB)
+  bool lvc_stream = true;      // hop % 32 == 0 blocks with a fused upsample on the streaming kernel (FD_OPT_LVC_STREAM)
   // fd_sample (bf16): the kernel-predictor GEMMs run on a second, low-priority stream into a
   // ring of one K buffer per block, so step j+1's kernels for block n are written while
   // step j's later blocks run (FD_OPT_KP_SIDE).  Created on first use.  Off by default:
@@ -965,6 +966,410 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
 #undef TILE
 }
 
+// ------------------------------------------------------------------ streaming LVC block (bf16)
+// All 4 layers of one TimeAware_LVCBlock (modules.py:205-217) for hop % 32 == 0, with the
+// ConvTranspose upsample in front (UPS always), audio_down recomputed from the audio (AUD)
+// and the final conv + sampler update behind (FIN), as ONE streaming pipeline per workgroup.
+//
+// Why streaming: the whole-block kernel (lvc_block_bf16_kernel) recomputes a 64-row halo
+// on each side of every 384-row tile and runs its 8 waves through the same barrier-
+// separated phases (all waves in the gate at once, then all in the MFMAs), so a SIMD's
+// vector and matrix pipes rarely work together.  Here a workgroup walks ONE long time
+// range [R0, R1) of an utterance tile by tile (32 rows), with 2 halo tiles per side
+// (reach 47 rows < 64) for the whole range instead of per tile, and every wave keeps one
+// kind of work:
+//   * 4 "owner" waves (V): wave w owns the tiles j = w (mod 4).  Each step it runs the
+//     location-variable conv + gate of one layer on one of its tiles, and keeps the
+//     tiles' fp32 state z = x + a in registers across the 4 layers (a 4-deep queue).
+//   * 4 "pre-conv" waves (P): wave 4 + l computes layer l's dilated pre-conv
+//     y = lrelu(W_l . [u(t-d); u(t); u(t+d)] + b), u = lrelu(z), for one tile per step.
+//     Wave 5 also runs the input stage S (upsample + audio_down -> u_0), wave 7 the final
+//     conv + sampler update F.
+// The waves of a step touch different tiles, so a SIMD hosts one V and one P wave with
+// MFMA work and gate work interleaved.  Tiles meet through LDS rings (one per layer) and
+// ONE workgroup barrier per step.  Stage schedule (a stage at step s sees everything done
+// at steps < s):  S(j) at j;  P_l(j) at j + Q_l, Q = 2, 6, 11, 16;  V_l(j) at j + 5l + 4;
+// F(j) at j + 21.  P_l(j) reads u_l of tiles j-1..j+1 (written by V_{l-1} or S), V_l(j)
+// reads y_l of tiles j-1..j+1.  Owner w runs layer (s - w) mod 4 at step s, so inside its
+// unrolled 4-step cycle the layer is a compile-time constant.
+//
+// LDS (bytes): u rings 4 x 4 slots, y rings 4 + 3 x 5 slots (32 rows x 80 B), x_0 ring 5
+// slots and x_4 ring 4 slots (32 rows x 144 B) = 132 KB: one workgroup (8 waves) per CU.
+namespace lsk {
+constexpr int LD = 40, XLD = 36;
+constexpr int TROW = 32 * LD;                  // bf16 per ring slot
+constexpr int XROW = 32 * XLD;                 // fp32 per ring slot
+constexpr int NU = 4, NY0 = 4, NY = 5, NX0 = 5, NX4 = 4;
+constexpr int U_OFF = 0;                                   // bf16 units
+constexpr int Y_OFF = U_OFF + 4 * NU * TROW;
+constexpr int BF_END = Y_OFF + (NY0 + 3 * NY) * TROW;
+constexpr int X0_OFF = BF_END / 2;                         // fp32 units (BF_END is even)
+constexpr int X4_OFF = X0_OFF + NX0 * XROW;
+constexpr int SMEM = (X4_OFF + NX4 * XROW) * 4;
+constexpr int HALO = 2;                                    // halo tiles per side
+constexpr int LAG_F = 21, LAG_V3 = 19;
+__device__ __forceinline__ int qlag(int l) { return l == 0 ? 2 : l == 1 ? 6 : l == 2 ? 11 : 16; }
+__device__ __forceinline__ int ymod(int l) { return l == 0 ? 32 * NY0 : 32 * NY; }
+__device__ __forceinline__ int yslot0(int l) { return l == 0 ? 0 : NY0 + (l - 1) * NY; }
+__device__ __forceinline__ int pmod(int x, int m) { x %= m; return x < 0 ? x + m : x; }
+}  // namespace lsk
+
+template <bool AUD, bool FIN>
+__global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockArgs P, int seg) {
+  using namespace lsk;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ __attribute__((aligned(16))) float FWF[FIN ? 7 * 32 : 4];
+  __bf16* const BS = reinterpret_cast<__bf16*>(smem);
+  float* const FS = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, h = lane >> 5;
+  const int b = blockIdx.y;
+  const int Tc = P.Tc, hop = P.hop, Lh = Tc * hop;
+  const int R0 = blockIdx.x * seg, R1 = min(R0 + seg, Lh);
+  const int tg = R0 - 32 * HALO;                                // time of tile 0, row 0
+  const int NT = (R1 - R0 + 31) / 32 + 2 * HALO;
+  const int NSTEP = NT + (FIN ? LAG_F : LAG_V3) + 1;
+  const long long base = (long long)b * Lh;
+
+  // zero the rings: halo tiles read slots nobody wrote (rows outside [0, Lh) are written
+  // as zeros, the reference convs' zero padding)
+  for (int i = tid; i < SMEM / 16; i += 512) reinterpret_cast<uint4*>(smem)[i] = uint4{0u, 0u, 0u, 0u};
+  if constexpr (FIN) {
+    if (tid < 224) FWF[tid] = P.wfin[tid];                      // [tap][c]
+  }
+  __syncthreads();
+
+  // audio_down = first_conv(audio) (FastDiff_model.py:90) of one 32-row tile, in the MFMA C
+  // layout (lane = time tt + n, channels (reg&3) + 8(reg>>2) + 4h), as 2 bf16 MFMAs on a
+  // hi/lo split of weights and audio (|error| ~ 2^-16 relative):  A1 = [W_hi, b_hi | W_lo,
+  // b_lo], B1 = [x_hi(t-3..t+3), 1 | same];  A2 = [W_hi, 0 | 0], B2 = [x_lo(t-3..t+3), 0 | *].
+  bf16x8 fa1 = {}, fa2 = {};
+  if constexpr (AUD) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const float w = P.fw[n * 7 + k];                          // fw is [c][tap]
+      const __bf16 whi = (__bf16)w, wlo = (__bf16)(w - (float)whi);
+      fa1[k] = h ? wlo : whi;
+      fa2[k] = h ? (__bf16)0.f : whi;
+    }
+    const float bb = P.fb[n];
+    const __bf16 bhi = (__bf16)bb;
+    fa1[7] = h ? (__bf16)(bb - (float)bhi) : bhi;
+    fa2[7] = (__bf16)0.f;
+  }
+  auto audio_down = [&](int tt) -> f32x16 {
+    f32x16 acc;
+    if constexpr (AUD) {
+      const int t = tt + n;
+      float xv[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const int ta = t + k - 3;
+        const float v = P.audio[base + min(max(ta, 0), Lh - 1)];
+        xv[k] = (ta >= 0 && ta < Lh) ? v : 0.f;
+      }
+      bf16x8 bh, bl;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        bh[k] = (__bf16)xv[k];
+        bl[k] = (__bf16)(xv[k] - (float)bh[k]);
+      }
+      bh[7] = (__bf16)1.f;
+      bl[7] = (__bf16)0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa2, bl, acc, 0, 0, 0);
+    } else {
+      const int t = tt + n;
+      const bool ok = t >= 0 && t < Lh;
+      const float* ap = P.a + (base + min(max(t, 0), Lh - 1)) * CI + 4 * h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 v = *reinterpret_cast<const float4*>(ap + 8 * i);
+        acc[4 * i] = ok ? v.x : 0.f; acc[4 * i + 1] = ok ? v.y : 0.f;
+        acc[4 * i + 2] = ok ? v.z : 0.f; acc[4 * i + 3] = ok ? v.w : 0.f;
+      }
+    }
+    return acc;
+  };
+  // u = bf16 lrelu(z) of one tile row into a ring slot (positions 16h + reg: kernel k-order)
+  auto store_u = [&](__bf16* row, const f32x2* z, bool in) {
+    bf16x8 u0, u1;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const f32x2 v0 = in ? lrelu2(z[p]) : f32x2{0.f, 0.f}, v1 = in ? lrelu2(z[4 + p]) : f32x2{0.f, 0.f};
+      u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
+      u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
+    }
+    *reinterpret_cast<bf16x8*>(row + 16 * h) = u0;
+    *reinterpret_cast<bf16x8*>(row + 16 * h + 8) = u1;
+  };
+
+  if (wave < 4) {
+    // ============================ owner waves: V_l(j), l = (s - w) mod 4
+    const int w = wave;
+    f32x2 z[4][8];                                   // z of the tiles at layers 0..3 (queue)
+    bf16x8 kn[12];                                   // prefetched kernel fragments of the next V stage
+    float4 bn[8];                                    // and its frame's LVC biases (4 gate, 4 filter)
+    auto prefetch = [&](int l, int j) {
+      const int fr = min(max((tg + 32 * j) / hop, 0), Tc - 1);
+      const long long row = (long long)b * Tc + fr;
+      const __bf16* kq = P.Kf[l] + row * KPERLAYER;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) kn[kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+      const float* bq = P.Bf + row * (2 * CI * NLY) + l * 2 * CI + 4 * h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bn[i] = *reinterpret_cast<const float4*>(bq + 8 * i);
+        bn[4 + i] = *reinterpret_cast<const float4*>(bq + 32 + 8 * i);
+      }
+    };
+    prefetch(0, 0);
+    for (int s = 0; s < w; ++s) __syncthreads();
+    for (int c = 0; 4 * c + w < NSTEP; ++c) {
+      // queue shift: the tile at layer l last cycle is at layer l + 1 now
+#pragma unroll
+      for (int q = 3; q > 0; --q)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) z[q][p] = z[q - 1][p];
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        const int s = 4 * c + w + l;
+        if (s >= NSTEP) break;
+        const int j = s - 5 * l - 4;
+        if (j >= 0 && j < NT) {
+          const int tt = tg + 32 * j, t = tt + n;
+          const bool in = t >= 0 && t < Lh;
+          f32x16 av;
+          if (l < 3) av = audio_down(tt);
+          if (l == 0) {      // z_0 = x_0 (from the input stage) + a
+            const float* xr = FS + X0_OFF + pmod(32 * j + n, 32 * NX0) * XLD + 4 * h;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float4 v = *reinterpret_cast<const float4*>(xr + 8 * i);
+              z[0][2 * i] = f32x2{v.x + av[4 * i], v.y + av[4 * i + 1]};
+              z[0][2 * i + 1] = f32x2{v.z + av[4 * i + 2], v.w + av[4 * i + 3]};
+            }
+          }
+          // o^T = K . [y(t-1); y(t); y(t+1)]^T + Bf, pre-scaled for exp2 (kp_kernels_all prescale)
+          f32x16 g, f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            g[4 * i] = -LOG2E * bn[i].x; g[4 * i + 1] = -LOG2E * bn[i].y;
+            g[4 * i + 2] = -LOG2E * bn[i].z; g[4 * i + 3] = -LOG2E * bn[i].w;
+            f[4 * i] = 2.f * LOG2E * bn[4 + i].x; f[4 * i + 1] = 2.f * LOG2E * bn[4 + i].y;
+            f[4 * i + 2] = 2.f * LOG2E * bn[4 + i].z; f[4 * i + 3] = 2.f * LOG2E * bn[4 + i].w;
+          }
+          const __bf16* Yl = BS + Y_OFF + yslot0(l) * TROW;
+          const int ym = ymod(l);
+#pragma unroll
+          for (int kk = 0; kk < 6; ++kk) {
+            const bf16x8 yb = *reinterpret_cast<const bf16x8*>(
+                Yl + pmod(32 * j + n + (kk >> 1) - 1, ym) * LD + 16 * (kk & 1) + 8 * h);
+            g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g, 0, 0, 0);
+            f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f, 0, 0, 0);
+          }
+          {   // the next step's V stage: layer (l + 1) mod 4
+            const int l2 = (l + 1) & 3, j2 = s + 1 - 5 * l2 - 4;
+            prefetch(l2, min(max(j2, 0), NT - 1));
+          }
+          // x_{l+1} = z_l + sigmoid(o_g) tanh(o_f); z_{l+1} = x_{l+1} + a (l < 3)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const f32x2 o0 = gate2s(f32x2{g[4 * i], g[4 * i + 1]}, f32x2{f[4 * i], f[4 * i + 1]});
+            const f32x2 o1 = gate2s(f32x2{g[4 * i + 2], g[4 * i + 3]}, f32x2{f[4 * i + 2], f[4 * i + 3]});
+            if (l < 3) {
+              z[l][2 * i] += o0 + f32x2{av[4 * i], av[4 * i + 1]};
+              z[l][2 * i + 1] += o1 + f32x2{av[4 * i + 2], av[4 * i + 3]};
+            } else {
+              z[l][2 * i] += o0;
+              z[l][2 * i + 1] += o1;
+            }
+          }
+          if (l < 3) {
+            store_u(BS + U_OFF + ((l + 1) * NU * 32 + ((32 * j + n) & (32 * NU - 1))) * LD, z[l], in);
+          } else if constexpr (FIN) {
+            float* xr = FS + X4_OFF + ((32 * j + n) & (32 * NX4 - 1)) * XLD + 4 * h;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              *reinterpret_cast<float4*>(xr + 8 * i) =
+                  in ? make_float4(z[3][2 * i].x, z[3][2 * i].y, z[3][2 * i + 1].x, z[3][2 * i + 1].y)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+          } else {
+            if (t >= R0 && t < R1) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<float4*>(P.xout + (base + t) * CI + 8 * i + 4 * h) =
+                    make_float4(z[3][2 * i].x, z[3][2 * i].y, z[3][2 * i + 1].x, z[3][2 * i + 1].y);
+            }
+          }
+        } else {    // no tile this step: still fetch the next step's fragments
+          const int l2 = (l + 1) & 3, j2 = s + 1 - 5 * l2 - 4;
+          prefetch(l2, min(max(j2, 0), NT - 1));
+        }
+        __syncthreads();
+      }
+    }
+  } else {
+    // ============================ pre-conv waves: P_l(j), l = wave - 4 (+ S on wave 5, F on wave 7)
+    const int l = wave - 4;
+    const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
+    bf16x8 wf[6];
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      const __bf16* wq = P.Wc[l] + n * 96 + (kk >> 1) * 32 + 16 * h + 4 * (kk & 1);
+      const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(wq), w1 = *reinterpret_cast<const bf16x4*>(wq + 8);
+      wf[kk] = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+    }
+    f32x2 bias[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 bv = *reinterpret_cast<const float4*>(P.bc[l] + 8 * i + 4 * h);
+      bias[2 * i] = f32x2{bv.x, bv.y}; bias[2 * i + 1] = f32x2{bv.z, bv.w};
+    }
+    const __bf16* Ul = BS + U_OFF + l * NU * 32 * LD;
+    __bf16* Yl = BS + Y_OFF + yslot0(l) * TROW;
+    const int ym = ymod(l), ql = qlag(l);
+    // input stage (wave 5): ConvTranspose upsample (modules.py:205-206) from x_prev as r phase
+    // GEMMs on 16x16x32 MFMAs.  Output t = r m + k - p takes taps k (input m) and k + r (input
+    // m - 1): C[co][m] = [W_k^T | W_{k+r}^T] . [lrelu(x_prev(m)); lrelu(x_prev(m - 1))].
+    const int r = P.r, pp = P.p, Tin = Lh / r;
+    const int l16 = lane & 15, kg = lane >> 4;
+    float bup[8] = {};
+    if (wave == 5) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bup[4 * ct + e] = P.bup[16 * ct + 4 * kg + e];
+    }
+    for (int s = 0; s < NSTEP; ++s) {
+      // ---- P_l(j): y = lrelu(W . [u(t-d); u(t); u(t+d)] + b), rows outside the utterance zero
+      {
+        const int j = s - ql;
+        if (j >= 0 && j < NT) {
+          f32x16 acc;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+          for (int kk = 0; kk < 6; ++kk) {
+            const int tap = kk >> 1;
+            const bf16x8 bu = *reinterpret_cast<const bf16x8*>(
+                Ul + ((32 * j + n + (tap - 1) * d) & (32 * NU - 1)) * LD + 16 * (kk & 1) + 8 * h);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc, 0, 0, 0);
+          }
+          const int t = tg + 32 * j + n;
+          const bool in = t >= 0 && t < Lh;
+          f32x2 v[8];
+#pragma unroll
+          for (int p = 0; p < 8; ++p) {
+            const f32x2 y = lrelu2(f32x2{acc[2 * p], acc[2 * p + 1]} + bias[p]);
+            v[p] = in ? y : f32x2{0.f, 0.f};
+          }
+          bf16x8 y0, y1;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            y0[2 * p] = (__bf16)v[p].x; y0[2 * p + 1] = (__bf16)v[p].y;
+            y1[2 * p] = (__bf16)v[4 + p].x; y1[2 * p + 1] = (__bf16)v[4 + p].y;
+          }
+          __bf16* dst = Yl + pmod(32 * j + n, ym) * LD + 16 * h;
+          *reinterpret_cast<bf16x8*>(dst) = y0;
+          *reinterpret_cast<bf16x8*>(dst + 8) = y1;
+        }
+      }
+      // ---- S(j = s) (wave 5): x_0 = upsample(lrelu(x_prev)) -> x_0 ring; u_0 = lrelu(x_0 + a)
+      if (wave == 5 && s < NT) {
+        const int j = s, tt = tg + 32 * j;
+        // input positions m of this tile: m in [mb, mb + 16), mb = floor((tt + p) / r) - 1
+        const int mb = floordiv(tt + pp, r) - 1;
+        bf16x8 xb[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {        // ks 0: x_prev(m), ks 1: x_prev(m - 1)
+          const int m = mb + l16 - ks;
+          const bool ok = m >= 0 && m < Tin;
+          const float* xp = P.xin + ((long long)b * Tin + min(max(m, 0), Tin - 1)) * CI + 8 * kg;
+          const float4 v0 = *reinterpret_cast<const float4*>(xp), v1 = *reinterpret_cast<const float4*>(xp + 4);
+          const float e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float u = ok ? e[q] : 0.f;
+            xb[ks][q] = (__bf16)(u >= 0.f ? u : 0.2f * u);
+          }
+        }
+        float* X0 = FS + X0_OFF;
+        for (int k = 0; k < r; ++k) {
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct) {
+            typedef float f32x4_ __attribute__((ext_vector_type(4)));
+            f32x4_ acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+              const bf16x8 wa = *reinterpret_cast<const bf16x8*>(
+                  P.Wup + ((long long)(k * 32 + 16 * ct + l16)) * 64 + 32 * ks + 8 * kg);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xb[ks], acc, 0, 0, 0);
+            }
+            // C[co = 16 ct + 4 kg + e][m = mb + l16] -> time r m + k - p
+            const int row = r * (mb + l16) + k - pp - tt;
+            if (row >= 0 && row < 32)
+              *reinterpret_cast<float4*>(X0 + pmod(32 * j + row, 32 * NX0) * XLD + 16 * ct + 4 * kg) =
+                  make_float4(acc[0] + bup[4 * ct], acc[1] + bup[4 * ct + 1], acc[2] + bup[4 * ct + 2],
+                              acc[3] + bup[4 * ct + 3]);
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's x_0 rows are in LDS
+        __builtin_amdgcn_wave_barrier();
+        const f32x16 av = audio_down(tt);
+        const float* xr = X0 + pmod(32 * j + n, 32 * NX0) * XLD + 4 * h;
+        f32x2 zz[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 v = *reinterpret_cast<const float4*>(xr + 8 * i);
+          zz[2 * i] = f32x2{v.x + av[4 * i], v.y + av[4 * i + 1]};
+          zz[2 * i + 1] = f32x2{v.z + av[4 * i + 2], v.w + av[4 * i + 3]};
+        }
+        const int t = tt + n;
+        store_u(BS + U_OFF + ((32 * j + n) & (32 * NU - 1)) * LD, zz, t >= 0 && t < Lh);
+      }
+      // ---- F(j) (wave 7): eps = final_conv(x_4), audio_out = (x_t - ce eps) / den + sig z
+      if constexpr (FIN) {
+        const int j = s - LAG_F;
+        if (wave == 7 && j >= 0 && j < NT) {
+          const int sm = lane >> 1, c0 = (lane & 1) * 16, t = tg + 32 * j + sm;
+          const float* X4 = FS + X4_OFF;
+          float e = 0.f;
+#pragma unroll
+          for (int tap = 0; tap < 7; ++tap) {
+            const float* xrow = X4 + ((32 * j + sm + tap - 3) & (32 * NX4 - 1)) * XLD + c0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 v = *reinterpret_cast<const float4*>(xrow + 4 * q);
+              const float4 w4 = *reinterpret_cast<const float4*>(&FWF[tap * 32 + c0 + 4 * q]);
+              e = fmaf(w4.x, v.x, fmaf(w4.y, v.y, fmaf(w4.z, v.z, fmaf(w4.w, v.w, e))));
+            }
+          }
+          e += __shfl_xor(e, 1);
+          if ((lane & 1) == 0 && t >= R0 && t < R1) {
+            e += P.bfin[0];
+            float v = (P.audio[base + t] - P.ce * e) / P.den;
+            if (P.sig != 0.f)
+              v += P.sig * (P.noise ? P.noise[base + t] : philox_normal(P.seed, (unsigned long long)(base + t), P.stream));
+            P.audio_out[base + t] = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Rows per workgroup: one wave of about 256 workgroups over the chip (one per CU), whole
+// tiles, at least 16 tiles so the 4 halo tiles and the 21-step pipeline fill stay small.
+int lvc_stream_seg(int Lh, int B) {
+  const long long rows = (long long)Lh * B;
+  int seg = (int)((rows + 256LL * 32 - 1) / (256LL * 32)) * 32;
+  return seg < 512 ? 512 : seg;
+}
+
 // ------------------------------------------------------------------ DiffusionDBlock (bf16)
 // modules.py:131-138 in one launch:
 //   xs = x[f i];  h1 = lrelu(conv_d1(lrelu(xs)));  h2 = lrelu(conv_d2(h1));
@@ -1740,7 +2145,19 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         la.audio_out = fin->audio_out; la.noise = fin->noise; la.ce = fin->ce; la.den = fin->den;
         la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream;
       }
-      {
+      if (m->lvc_stream && ups && hop % 32 == 0 && r >= 4) {
+        // streaming pipeline: one long time range per workgroup (lvc_stream_bf16_kernel)
+        ProfScope ps(fuse_fin ? "fd_lvc_block_final" : "fd_lvc_block_ups", st);
+        const int Lh = (int)Tout, seg = lvc_stream_seg(Lh, B);
+        const dim3 grid(cdiv(Lh, seg), B);
+        if (last && aud && fuse_fin)
+          hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, true>), grid, dim3(512), 0, st, la, seg);
+        else if (last && aud)
+          hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, false>), grid, dim3(512), 0, st, la, seg);
+        else
+          hipLaunchKernelGGL((lvc_stream_bf16_kernel<false, false>), grid, dim3(512), 0, st, la, seg);
+        PD_LAUNCH_CHECK();
+      } else {
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : hop < 32 ? "fd_lvc_block_sub" : ups ? "fd_lvc_block_ups"
                                                                                    : "fd_lvc_block", st);
         const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
@@ -2001,6 +2418,7 @@ int fd_set_option(fd_model* m, int option, int value) {
     case FD_OPT_LVC_PF: m->lvc_pf = value != 0; return PD_OK;
     case FD_OPT_LVC_SUB: m->lvc_sub = value != 0; return PD_OK;
     case FD_OPT_KP_SIDE: m->kp_side = value != 0; return PD_OK;
+    case FD_OPT_LVC_STREAM: m->lvc_stream = value != 0; return PD_OK;
     default: break;
   }
   set_error("fd_set_option: unknown option " + std::to_string(option));

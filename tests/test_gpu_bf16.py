@@ -86,15 +86,18 @@ def test_fastdiff_sample_bf16(fd16):
     assert_bf16_close(wav, d["wav"], "fastdiff_sample_n4")
 
 
-@pytest.mark.parametrize("ts", [0, 128, 256, 384])
-@pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
+@pytest.mark.parametrize("ts", ["stream", 0, 128, 256, 384])
+@pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9), (1, 40)])
 def test_fastdiff_lvc_block_bf16(ts, B, Tc):
-    """LVC modes (FD_OPT_LVC_TS: 0 = one fused launch per layer, 128/256/384 = whole block) against
-    the oracle, including utterances shorter than one block and the grid/halo edges."""
+    """LVC modes against the oracle, including utterances shorter than one block and the
+    grid/halo edges: the streaming pipeline kernel (FD_OPT_LVC_STREAM, default; T'=40 gives
+    several workgroups per utterance at hop 64 and 256) and the whole-block kernel
+    (FD_OPT_LVC_TS: 0 = one fused launch per layer, 128/256/384 = whole block)."""
     p = G.fastdiff_params(31)
     m = FastDiff()
     m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
-    m = m.to(DEV).set_compute_dtype("bf16").set_options(lvc_ts=ts)
+    opts = dict(lvc_stream=1) if ts == "stream" else dict(lvc_ts=ts, lvc_stream=0)
+    m = m.to(DEV).set_compute_dtype("bf16").set_options(**opts)
     audio = synth.synth_inputs(7 * B + Tc, (B, 1, Tc * 256))
     c = synth.synth_inputs(7 * B + Tc + 1, (B, 80, Tc), loc=-5.0, scale=2.0)
     st = np.full((B, 1), 41.5, np.float32)
@@ -103,8 +106,7 @@ def test_fastdiff_lvc_block_bf16(ts, B, Tc):
                       f"lvc_block ts={ts} B={B} Tc={Tc}", EPS_REL_L2, EPS_REL_MAX)
 
 
-@pytest.mark.parametrize("fuse", [0, 1])
-@pytest.mark.parametrize("ts", [128, 256, 384])
+@pytest.mark.parametrize("fuse,ts", [(0, 128), (0, 256), (0, 384), (1, 128), (1, 256), (1, 384), (1, "stream")])
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
 def test_fastdiff_sample_bf16_oracle(fuse, ts, B, Tc):
     """The 4-step sampler with the upsample / first conv / final update fused into the LVC
@@ -116,7 +118,8 @@ def test_fastdiff_sample_bf16_oracle(fuse, ts, B, Tc):
     p = G.fastdiff_params(31)
     m = FastDiff()
     m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
-    m = m.to(DEV).set_compute_dtype("bf16").set_options(lvc_ts=ts, lvc_fuse=fuse, lvc_sub=fuse)
+    opts = dict(lvc_stream=1) if ts == "stream" else dict(lvc_ts=ts, lvc_stream=0)
+    m = m.to(DEV).set_compute_dtype("bf16").set_options(lvc_fuse=fuse, lvc_sub=fuse, **opts)
     b, a, s, st = fastdiff_infer_params(fastdiff_reverse_schedule(4), fastdiff_train_alpha())
     mel = synth.synth_inputs(40 + B, (B, Tc, 80), loc=-5.0, scale=2.0)
     xT = synth.synth_inputs(41 + B, (B, 1, Tc * 256))
