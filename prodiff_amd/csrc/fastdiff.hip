@@ -62,7 +62,10 @@ struct fd_model {
   bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (FD_OPT_LVC_FUSE)
   bool lvc_pf = true;          // next-layer kernel fragments prefetched into registers (FD_OPT_LVC_PF)
   bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (FD_OPT_LVC_SUB)
-  bool lvc_stream = true;      // hop % 32 == 0 blocks with a fused upsample on the streaming kernel (FD_OPT_LVC_STREAM)
+  // hop % 32 == 0 blocks with a fused upsample on the streaming kernel (FD_OPT_LVC_STREAM).  Off:
+  // measured slower than the whole-block kernel (r02: 688 vs 454 us on the hop-256 block,
+  // DESIGN.md §4), kept as a tested variant.
+  bool lvc_stream = false;
   // fd_sample (bf16): the kernel-predictor GEMMs run on a second, low-priority stream into a
   // ring of one K buffer per block, so step j+1's kernels for block n are written while
   // step j's later blocks run (FD_OPT_KP_SIDE).  Created on first use.  Off by default:
@@ -994,7 +997,14 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
 // unrolled 4-step cycle the layer is a compile-time constant.
 //
 // LDS (bytes): u rings 4 x 4 slots, y rings 4 + 3 x 5 slots (32 rows x 80 B), x_0 ring 5
-// slots and x_4 ring 4 slots (32 rows x 144 B) = 132 KB: one workgroup (8 waves) per CU.
+// slots and x_4 ring 4 slots (32 rows x 144 B), the audio samples of 32 tiles (AUD, FIN) =
+// 136 KB: one workgroup (8 waves) per CU.
+// Latency: the only global loads a V wave waits on are its kernel/bias fragments, loaded into
+// registers one step ahead, and the input stage's x_prev / audio_down / audio rows are loaded
+// two steps ahead (a barrier per step makes every step as slow as its slowest wave, so no
+// wave may wait on a cold load).  Every global pointer a wave indexes by a run-time layer is
+// read once before the step loop: a pointer load inside it would wait for all the wave's
+// outstanding prefetches (vmcnt retires in order).
 namespace lsk {
 constexpr int LD = 40, XLD = 36;
 constexpr int TROW = 32 * LD;                  // bf16 per ring slot
@@ -1005,7 +1015,14 @@ constexpr int Y_OFF = U_OFF + 4 * NU * TROW;
 constexpr int BF_END = Y_OFF + (NY0 + 3 * NY) * TROW;
 constexpr int X0_OFF = BF_END / 2;                         // fp32 units (BF_END is even)
 constexpr int X4_OFF = X0_OFF + NX0 * XROW;
-constexpr int SMEM = (X4_OFF + NX4 * XROW) * 4;
+constexpr int NAU = 1024;                                  // audio ring: 32 tiles of samples
+constexpr int WLD = 72;                                    // bf16 per upsample weight row (64 + 8 pad)
+// the x_4 ring (FIN), audio ring (AUD) and upsample weights (ratio <= RMAX) exist per variant
+template <bool AUD, bool FIN, int RMAX> struct Geo {
+  static constexpr int AU_OFF = X4_OFF + (FIN ? NX4 * XROW : 0);
+  static constexpr int WU_OFF = AU_OFF + (AUD ? NAU : 0);               // fp32 units
+  static constexpr int SMEM = (WU_OFF + RMAX * 32 * WLD / 2) * 4;
+};
 constexpr int HALO = 2;                                    // halo tiles per side
 constexpr int LAG_F = 21, LAG_V3 = 19;
 __device__ __forceinline__ int qlag(int l) { return l == 0 ? 2 : l == 1 ? 6 : l == 2 ? 11 : 16; }
@@ -1013,11 +1030,25 @@ __device__ __forceinline__ int ymod(int l) { return l == 0 ? 32 * NY0 : 32 * NY;
 __device__ __forceinline__ int yslot0(int l) { return l == 0 ? 0 : NY0 + (l - 1) * NY; }
 __device__ __forceinline__ int pmod(int x, int m) { x %= m; return x < 0 ? x + m : x; }
 }  // namespace lsk
+#ifdef LB_TRACE
+// tools/stream_probe.hip: s_memtime stamps of workgroup (5, 0), steps 100..107, [step][wave][8]
+#define LS_STAMP(s, i)                                                                         \
+  do {                                                                                         \
+    if (lane == 0 && blockIdx.x == 5 && blockIdx.y == 0 && (s) >= 100 && (s) < 108)            \
+      P.trace[(((s) - 100) * 8 + wave) * 8 + (i)] = __builtin_readcyclecounter();             \
+  } while (0)
+#else
+#define LS_STAMP(s, i) \
+  do {                 \
+  } while (0)
+#endif
 
-template <bool AUD, bool FIN>
+template <bool AUD, bool FIN, int RMAX>
 __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockArgs P, int seg) {
   using namespace lsk;
-  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  using GG = Geo<AUD, FIN, RMAX>;
+  constexpr int SMEM = GG::SMEM, AU_OFF = GG::AU_OFF, WU_OFF = GG::WU_OFF;
+  static_assert(SMEM + (FIN ? 7 * 32 * 4 : 16) <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   __shared__ __attribute__((aligned(16))) float FWF[FIN ? 7 * 32 : 4];
   __bf16* const BS = reinterpret_cast<__bf16*>(smem);
@@ -1036,6 +1067,20 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
   for (int i = tid; i < SMEM / 16; i += 512) reinterpret_cast<uint4*>(smem)[i] = uint4{0u, 0u, 0u, 0u};
   if constexpr (FIN) {
     if (tid < 224) FWF[tid] = P.wfin[tid];                      // [tap][c]
+  }
+  {   // upsample phase weights [r][32 co][64] -> LDS rows of WLD (conflict-free A-fragment reads)
+    __bf16* WU = BS + 2 * WU_OFF;
+    for (int i = tid; i < P.r * 32 * 8; i += 512) {
+      const int row = i >> 3, c = (i & 7) * 8;
+      *reinterpret_cast<bf16x8*>(WU + row * WLD + c) = *reinterpret_cast<const bf16x8*>(P.Wup + row * 64 + c);
+    }
+  }
+  __syncthreads();
+  if constexpr (AUD) {     // audio samples of tile 0 (the input stage writes tile s + 1 at step s)
+    if (tid < 32) {
+      const int t = tg + tid;
+      FS[AU_OFF + tid] = (t >= 0 && t < Lh) ? P.audio[base + t] : 0.f;
+    }
   }
   __syncthreads();
 
@@ -1060,14 +1105,12 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
   auto audio_down = [&](int tt) -> f32x16 {
     f32x16 acc;
     if constexpr (AUD) {
-      const int t = tt + n;
+      // samples from the LDS ring (zero outside the utterance: the first conv's padding)
+      const float* ar = FS + AU_OFF;
+      const int i0 = tt - tg + n - 3;
       float xv[7];
 #pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        const int ta = t + k - 3;
-        const float v = P.audio[base + min(max(ta, 0), Lh - 1)];
-        xv[k] = (ta >= 0 && ta < Lh) ? v : 0.f;
-      }
+      for (int k = 0; k < 7; ++k) xv[k] = ar[(i0 + k) & (NAU - 1)];
       bf16x8 bh, bl;
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
@@ -1138,6 +1181,7 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
         const int s = 4 * c + w + l;
         if (s >= NSTEP) break;
         const int j = s - 5 * l - 4;
+        LS_STAMP(s, 0);
         if (j >= 0 && j < NT) {
           const int tt = tg + 32 * j, t = tt + n;
           const bool in = t >= 0 && t < Lh;
@@ -1152,6 +1196,7 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
               z[0][2 * i + 1] = f32x2{v.z + av[4 * i + 2], v.w + av[4 * i + 3]};
             }
           }
+          LS_STAMP(s, 1);
           // o^T = K . [y(t-1); y(t); y(t+1)]^T + Bf, pre-scaled for exp2 (kp_kernels_all prescale)
           f32x16 g, f;
 #pragma unroll
@@ -1170,10 +1215,12 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
             g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g, 0, 0, 0);
             f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f, 0, 0, 0);
           }
+          LS_STAMP(s, 2);
           {   // the next step's V stage: layer (l + 1) mod 4
             const int l2 = (l + 1) & 3, j2 = s + 1 - 5 * l2 - 4;
             prefetch(l2, min(max(j2, 0), NT - 1));
           }
+          LS_STAMP(s, 3);
           // x_{l+1} = z_l + sigmoid(o_g) tanh(o_f); z_{l+1} = x_{l+1} + a (l < 3)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -1187,6 +1234,7 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
               z[l][2 * i + 1] += o1;
             }
           }
+          LS_STAMP(s, 4);
           if (l < 3) {
             store_u(BS + U_OFF + ((l + 1) * NU * 32 + ((32 * j + n) & (32 * NU - 1))) * LD, z[l], in);
           } else if constexpr (FIN) {
@@ -1208,6 +1256,7 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
           const int l2 = (l + 1) & 3, j2 = s + 1 - 5 * l2 - 4;
           prefetch(l2, min(max(j2, 0), NT - 1));
         }
+        LS_STAMP(s, 6);
         __syncthreads();
       }
     }
@@ -1243,21 +1292,51 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
 #pragma unroll
         for (int e = 0; e < 4; ++e) bup[4 * ct + e] = P.bup[16 * ct + 4 * kg + e];
     }
-    for (int s = 0; s < NSTEP; ++s) {
+    // input-stage operands of tile j, loaded two steps ahead (buffer j & 1)
+    struct SIn {
+      float4 xv[2][2];    // x_prev rows m = mb + l16 - ks, channels 8 kg .. 8 kg + 7
+      float4 av[4];       // audio_down rows (!AUD): a[tt + n][8 i + 4 h ..]
+      float au;           // AUD/FIN: audio sample of tile j + 1, row n
+    };
+    auto s_load = [&](SIn& q, int j) {
+      if (wave != 5 || j >= NT) return;
+      const int tt = tg + 32 * j, mb = floordiv(tt + pp, r) - 1;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int m = min(max(mb + l16 - ks, 0), Tin - 1);
+        const float* xp = P.xin + ((long long)b * Tin + m) * CI + 8 * kg;
+        q.xv[ks][0] = *reinterpret_cast<const float4*>(xp);
+        q.xv[ks][1] = *reinterpret_cast<const float4*>(xp + 4);
+      }
+      if constexpr (AUD) {
+        q.au = P.audio[base + min(max(tt + 32 + n, 0), Lh - 1)];
+      } else {
+        const float* ap = P.a + (base + min(max(tt + n, 0), Lh - 1)) * CI + 4 * h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q.av[i] = *reinterpret_cast<const float4*>(ap + 8 * i);
+      }
+    };
+    SIn sq[2];
+    s_load(sq[0], 0);
+    s_load(sq[1], 1);
+    auto step = [&](int s, SIn& cur) {
+      LS_STAMP(s, 0);
       // ---- P_l(j): y = lrelu(W . [u(t-d); u(t); u(t+d)] + b), rows outside the utterance zero
       {
         const int j = s - ql;
         if (j >= 0 && j < NT) {
-          f32x16 acc;
+          f32x16 acc, acc1;     // two accumulation chains (even / odd k-steps) halve the MFMA latency chain
 #pragma unroll
-          for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+          for (int q = 0; q < 16; ++q) { acc[q] = 0.f; acc1[q] = 0.f; }
 #pragma unroll
           for (int kk = 0; kk < 6; ++kk) {
             const int tap = kk >> 1;
             const bf16x8 bu = *reinterpret_cast<const bf16x8*>(
                 Ul + ((32 * j + n + (tap - 1) * d) & (32 * NU - 1)) * LD + 16 * (kk & 1) + 8 * h);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc, 0, 0, 0);
+            if (kk & 1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc1, 0, 0, 0);
+            else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc, 0, 0, 0);
           }
+          acc += acc1;
           const int t = tg + 32 * j + n;
           const bool in = t >= 0 && t < Lh;
           f32x2 v[8];
@@ -1277,9 +1356,17 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
           *reinterpret_cast<bf16x8*>(dst + 8) = y1;
         }
       }
+      LS_STAMP(s, 1);
       // ---- S(j = s) (wave 5): x_0 = upsample(lrelu(x_prev)) -> x_0 ring; u_0 = lrelu(x_0 + a)
       if (wave == 5 && s < NT) {
         const int j = s, tt = tg + 32 * j;
+        if constexpr (AUD) {   // the audio samples of tile j + 1 (tile j's own were written last step)
+          if (lane < 32) {
+            const int t = tt + 32 + n;
+            FS[AU_OFF + ((32 * j + 32 + n) & (NAU - 1))] = (t >= 0 && t < Lh) ? cur.au : 0.f;
+          }
+        }
+        LS_STAMP(s, 3);
         // input positions m of this tile: m in [mb, mb + 16), mb = floor((tt + p) / r) - 1
         const int mb = floordiv(tt + pp, r) - 1;
         bf16x8 xb[2];
@@ -1287,9 +1374,8 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
         for (int ks = 0; ks < 2; ++ks) {        // ks 0: x_prev(m), ks 1: x_prev(m - 1)
           const int m = mb + l16 - ks;
           const bool ok = m >= 0 && m < Tin;
-          const float* xp = P.xin + ((long long)b * Tin + min(max(m, 0), Tin - 1)) * CI + 8 * kg;
-          const float4 v0 = *reinterpret_cast<const float4*>(xp), v1 = *reinterpret_cast<const float4*>(xp + 4);
-          const float e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          const float e[8] = {cur.xv[ks][0].x, cur.xv[ks][0].y, cur.xv[ks][0].z, cur.xv[ks][0].w,
+                              cur.xv[ks][1].x, cur.xv[ks][1].y, cur.xv[ks][1].z, cur.xv[ks][1].w};
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float u = ok ? e[q] : 0.f;
@@ -1297,28 +1383,55 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
           }
         }
         float* X0 = FS + X0_OFF;
-        for (int k = 0; k < r; ++k) {
+        // all r x 2 phase-tile products issued back to back (independent accumulators), then stored
+        typedef float f32x4_ __attribute__((ext_vector_type(4)));
+        f32x4_ pacc[RMAX][2];
+#pragma unroll
+        for (int k = 0; k < RMAX; ++k) {
 #pragma unroll
           for (int ct = 0; ct < 2; ++ct) {
-            typedef float f32x4_ __attribute__((ext_vector_type(4)));
-            f32x4_ acc = {0.f, 0.f, 0.f, 0.f};
+            pacc[k][ct] = f32x4_{0.f, 0.f, 0.f, 0.f};
+            if (k < r) {
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-              const bf16x8 wa = *reinterpret_cast<const bf16x8*>(
-                  P.Wup + ((long long)(k * 32 + 16 * ct + l16)) * 64 + 32 * ks + 8 * kg);
-              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xb[ks], acc, 0, 0, 0);
+              for (int ks = 0; ks < 2; ++ks) {
+                const bf16x8 wa = *reinterpret_cast<const bf16x8*>(
+                    BS + 2 * WU_OFF + (k * 32 + 16 * ct + l16) * WLD + 32 * ks + 8 * kg);
+                pacc[k][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xb[ks], pacc[k][ct], 0, 0, 0);
+              }
             }
-            // C[co = 16 ct + 4 kg + e][m = mb + l16] -> time r m + k - p
-            const int row = r * (mb + l16) + k - pp - tt;
-            if (row >= 0 && row < 32)
-              *reinterpret_cast<float4*>(X0 + pmod(32 * j + row, 32 * NX0) * XLD + 16 * ct + 4 * kg) =
-                  make_float4(acc[0] + bup[4 * ct], acc[1] + bup[4 * ct + 1], acc[2] + bup[4 * ct + 2],
-                              acc[3] + bup[4 * ct + 3]);
           }
         }
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's x_0 rows are in LDS
+        LS_STAMP(s, 4);
+        const int x0base = 32 * j - tt;
+#pragma unroll
+        for (int k = 0; k < RMAX; ++k) {
+          // C[co = 16 ct + 4 kg + e][m = mb + l16] -> time r m + k - p
+          const int row = r * (mb + l16) + k - pp - tt;
+          if (k < r && row >= 0 && row < 32) {
+            float* xrow = X0 + pmod(x0base + tt + row, 32 * NX0) * XLD + 4 * kg;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+              *reinterpret_cast<float4*>(xrow + 16 * ct) =
+                  make_float4(pacc[k][ct][0] + bup[4 * ct], pacc[k][ct][1] + bup[4 * ct + 1],
+                              pacc[k][ct][2] + bup[4 * ct + 2], pacc[k][ct][3] + bup[4 * ct + 3]);
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's x_0 rows / audio are in LDS
         __builtin_amdgcn_wave_barrier();
-        const f32x16 av = audio_down(tt);
+        LS_STAMP(s, 5);
+        const int t = tt + n;
+        const bool in = t >= 0 && t < Lh;
+        f32x16 av;
+        if constexpr (AUD) {
+          av = audio_down(tt);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            av[4 * i] = in ? cur.av[i].x : 0.f; av[4 * i + 1] = in ? cur.av[i].y : 0.f;
+            av[4 * i + 2] = in ? cur.av[i].z : 0.f; av[4 * i + 3] = in ? cur.av[i].w : 0.f;
+          }
+        }
+        LS_STAMP(s, 7);
         const float* xr = X0 + pmod(32 * j + n, 32 * NX0) * XLD + 4 * h;
         f32x2 zz[8];
 #pragma unroll
@@ -1327,16 +1440,17 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
           zz[2 * i] = f32x2{v.x + av[4 * i], v.y + av[4 * i + 1]};
           zz[2 * i + 1] = f32x2{v.z + av[4 * i + 2], v.w + av[4 * i + 3]};
         }
-        const int t = tt + n;
-        store_u(BS + U_OFF + ((32 * j + n) & (32 * NU - 1)) * LD, zz, t >= 0 && t < Lh);
+        store_u(BS + U_OFF + ((32 * j + n) & (32 * NU - 1)) * LD, zz, in);
       }
+      LS_STAMP(s, 2);
+      s_load(cur, s + 2);
       // ---- F(j) (wave 7): eps = final_conv(x_4), audio_out = (x_t - ce eps) / den + sig z
       if constexpr (FIN) {
         const int j = s - LAG_F;
         if (wave == 7 && j >= 0 && j < NT) {
           const int sm = lane >> 1, c0 = (lane & 1) * 16, t = tg + 32 * j + sm;
           const float* X4 = FS + X4_OFF;
-          float e = 0.f;
+          f32x2 ea[4] = {};     // independent accumulators: the LDS reads pipeline under the FMAs
 #pragma unroll
           for (int tap = 0; tap < 7; ++tap) {
             const float* xrow = X4 + ((32 * j + sm + tap - 3) & (32 * NX4 - 1)) * XLD + c0;
@@ -1344,20 +1458,28 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
             for (int q = 0; q < 4; ++q) {
               const float4 v = *reinterpret_cast<const float4*>(xrow + 4 * q);
               const float4 w4 = *reinterpret_cast<const float4*>(&FWF[tap * 32 + c0 + 4 * q]);
-              e = fmaf(w4.x, v.x, fmaf(w4.y, v.y, fmaf(w4.z, v.z, fmaf(w4.w, v.w, e))));
+              ea[q] = __builtin_elementwise_fma(f32x2{w4.x, w4.y}, f32x2{v.x, v.y}, ea[q]);
+              ea[q] = __builtin_elementwise_fma(f32x2{w4.z, w4.w}, f32x2{v.z, v.w}, ea[q]);
             }
           }
+          const f32x2 e2 = (ea[0] + ea[1]) + (ea[2] + ea[3]);
+          float e = e2.x + e2.y;
           e += __shfl_xor(e, 1);
           if ((lane & 1) == 0 && t >= R0 && t < R1) {
             e += P.bfin[0];
-            float v = (P.audio[base + t] - P.ce * e) / P.den;
+            float v = (FS[AU_OFF + ((32 * j + sm) & (NAU - 1))] - P.ce * e) / P.den;
             if (P.sig != 0.f)
               v += P.sig * (P.noise ? P.noise[base + t] : philox_normal(P.seed, (unsigned long long)(base + t), P.stream));
             P.audio_out[base + t] = v;
           }
         }
       }
+      LS_STAMP(s, 6);
       __syncthreads();
+    };
+    for (int s = 0; s < NSTEP; s += 2) {
+      step(s, sq[0]);
+      if (s + 1 < NSTEP) step(s + 1, sq[1]);
     }
   }
 }
@@ -2145,17 +2267,20 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         la.audio_out = fin->audio_out; la.noise = fin->noise; la.ce = fin->ce; la.den = fin->den;
         la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream;
       }
-      if (m->lvc_stream && ups && hop % 32 == 0 && r >= 4) {
+      // (the LDS image holds upsample weights for r <= 4 with the audio fusions, r <= 8 without)
+      if (m->lvc_stream && ups && hop % 32 == 0 && r >= 4 && (last && aud ? r <= 4 : r <= 8)) {
         // streaming pipeline: one long time range per workgroup (lvc_stream_bf16_kernel)
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : "fd_lvc_block_ups", st);
         const int Lh = (int)Tout, seg = lvc_stream_seg(Lh, B);
         const dim3 grid(cdiv(Lh, seg), B);
         if (last && aud && fuse_fin)
-          hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, true>), grid, dim3(512), 0, st, la, seg);
+          hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, true, 4>), grid, dim3(512), 0, st, la, seg);
         else if (last && aud)
-          hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, false>), grid, dim3(512), 0, st, la, seg);
+          hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, false, 4>), grid, dim3(512), 0, st, la, seg);
+        else if (r <= 4)
+          hipLaunchKernelGGL((lvc_stream_bf16_kernel<false, false, 4>), grid, dim3(512), 0, st, la, seg);
         else
-          hipLaunchKernelGGL((lvc_stream_bf16_kernel<false, false>), grid, dim3(512), 0, st, la, seg);
+          hipLaunchKernelGGL((lvc_stream_bf16_kernel<false, false, 8>), grid, dim3(512), 0, st, la, seg);
         PD_LAUNCH_CHECK();
       } else {
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : hop < 32 ? "fd_lvc_block_sub" : ups ? "fd_lvc_block_ups"
