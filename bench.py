@@ -74,6 +74,8 @@ def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256):
         "wn_gate": 2 * F * 2 * C * (3 * C + H),
         "wn_resskip": 2 * F * 2 * C * C,
         "wn_layer": 2 * F * 2 * C * (3 * C + H) + 2 * F * 2 * C * C,     # fused gate + res/skip (bf16)
+        "wn_gate2": 2 * F * 2 * C * (3 * C + H),                            # two-GEMM layer (bf16)
+        "wn_resskip2": 2 * F * 2 * C * C * 39 / 40,                          # last of 20 layers: skip half only
         "wn_skiphead": 2 * F * C * C,
         "wn_outproj_posterior": 2 * F * M * C,
         "fd_first_conv": 2 * F * 256 * 32 * 7,
@@ -118,6 +120,10 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         "wn_gate": F * (C + H + C) * 4 + 2 * C * (3 * C + H) * wb,
         "wn_resskip": F * (C + 2 * C + 2 * C) * 4 + 2 * C * C * wb,
         "wn_layer": F * (C + H + C + 2 * C) * 4 + 2 * C * (4 * C + H) * wb,
+        # bf16 activations in (xa = x + dp, cond), g out, weights once
+        "wn_gate2": F * (C + H + C) * 2 + 2 * C * (3 * C + H) * wb,
+        # g in; x read + written, skip read + written (fp32), xa' written
+        "wn_resskip2": F * (C * 2 + C * 4 * 2 + C * 4 * 2 + C * 2) + 2 * C * C * wb,
         "wn_skiphead": F * 2 * C * 4 + C * C * wb,
         "wn_outproj_posterior": F * (C + 3 * M) * 4 + M * C * wb,
         "fd_first_conv": F * 256 * (1 + 32) * 4,
@@ -269,7 +275,9 @@ def main():
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default: newest profiles/r*_v*_traffic.json)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo launcher + sharding + gather check, no GPU")
     ap.add_argument("--fd-opt", action="append", default=[], metavar="NAME=VALUE",
-                    help="FastDiff kernel-variant option for A/B runs (fd_set_option, e.g. lvc_stream=0)")
+                    help="FastDiff kernel-variant option for A/B runs (fd_set_option, e.g. lvc_stream=1)")
+    ap.add_argument("--wn-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="WaveNet kernel-variant option for A/B runs (pd_wavenet_set_option, e.g. layer=0)")
     args = ap.parse_args()
 
     # ---- N ranks: re-launch under torch.distributed.run BEFORE anything touches the GPU
@@ -322,6 +330,8 @@ def main():
         syn = Synthesizer.synthetic(dev, seed=0, dtype=dtype)
         if args.fd_opt:
             syn.vocoder.model.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.fd_opt)})
+        if args.wn_opt:
+            syn.diffusion.denoise_fn.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.wn_opt)})
         synth_fn = syn
 
     if cfg["vocoder"]:

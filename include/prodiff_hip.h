@@ -82,6 +82,13 @@ typedef struct {
 int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, int dtype,
                       void* stream, pd_wavenet** out);
 void pd_wavenet_destroy(pd_wavenet* h);
+/* Kernel-variant option of a handle; set before its first call.  PD_WN_OPT_LAYER selects the
+ * bf16 residual-layer implementation: 0 the fused kernel with 32-frame blocks, 3 the fused
+ * kernel with 64-frame blocks, 2 (default) 64-frame blocks when they still give every CU a
+ * block (B*T >= 16384 frames) else 32, 1 two GEMM launches per layer with 128 x 128 tiles
+ * (DESIGN.md §4). */
+#define PD_WN_OPT_LAYER 0
+int pd_wavenet_set_option(pd_wavenet* h, int option, int value);
 /* S = number of reverse steps the workspace must serve (1 for pd_wavenet_forward). */
 size_t pd_wavenet_workspace_size(const pd_wavenet* h, int B, int T, int S);
 

@@ -17,6 +17,7 @@ PD_REFLOW = {"euler": 0, "rk2": 1, "rk4": 2, "rk5": 3}
 # fd_set_option / nsf_set_option ids (include/prodiff_hip.h)
 FD_OPTIONS = {"lvc_ts": 0, "lvc_ts_sub": 1, "lvc_fuse": 2, "lvc_pf": 3, "lvc_sub": 4, "kp_side": 5, "lvc_stream": 6}
 NSF_OPTIONS = {"small_max": 0}
+WN_OPTIONS = {"layer": 0}
 
 
 class HipError(RuntimeError):
@@ -54,6 +55,7 @@ _SIGS = {
     "pd_profile_filter": (C.c_int, [C.c_char_p]),
     "pd_wavenet_create": (C.c_int, [C.POINTER(pd_wavenet_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
     "pd_wavenet_destroy": (None, [_VP]),
+    "pd_wavenet_set_option": (C.c_int, [_VP, C.c_int, C.c_int]),
     "pd_wavenet_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
     "pd_wavenet_forward": (C.c_int, [_VP, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "pd_prodiff_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),

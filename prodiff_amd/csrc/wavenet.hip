@@ -30,6 +30,9 @@ struct pd_wavenet {
   __bf16* frag = nullptr;
   __bf16* W1f = nullptr;   // [L][2C/32 tiles][K/16 steps][64 lanes][8]
   __bf16* W2f = nullptr;
+  // bf16 residual layer (PD_WN_OPT_LAYER): 0 = fused kernel, 32 frames per block; 3 = fused, 64
+  // frames per block; 2 = auto between the two by grid size; 1 = two 128x128-tile GEMMs
+  int layer_mode = 2;
 };
 
 namespace {
@@ -69,14 +72,21 @@ struct WnLayerArgs {
   int B, T, H, dil, first;
 };
 
-template <int K1>
+// RT row tiles (32 frames each) per block: every weight fragment streamed from L2 feeds RT
+// MFMAs, so RT = 2 halves the L2 -> CU weight bytes per frame (the port, about 64 B/clk/CU,
+// is what bounds RT = 1 at a quarter of the MFMA rate).  RT = 2 keeps the K = 1024 input
+// rows of 64 frames in LDS (132 KB, one block per CU); the gated g tile reuses that space.
+template <int K1, int RT>
 __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P) {
   constexpr int C = WNF_C;
   constexpr int LDA = K1 + 8, LDG = C + 8;       // 16-B-offset rows: conflict-free b128 fragment reads
-  __shared__ __attribute__((aligned(16))) __bf16 As[32 * LDA];
-  __shared__ __attribute__((aligned(16))) __bf16 Gs[32 * LDG];
+  constexpr int AS_BYTES = 32 * RT * LDA * 2, GS_BYTES = 32 * RT * LDG * 2;
+  constexpr int SM = RT == 1 ? AS_BYTES + GS_BYTES : (AS_BYTES > GS_BYTES ? AS_BYTES : GS_BYTES);
+  __shared__ __attribute__((aligned(16))) char smem[SM];
+  __bf16* As = reinterpret_cast<__bf16*>(smem);
+  __bf16* Gs = reinterpret_cast<__bf16*>(smem + (RT == 1 ? AS_BYTES : 0));   // RT = 2: aliases As
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
-  const int H = K1 - 3 * C, rows = P.B * P.T, R0 = blockIdx.x * 32;
+  const int H = K1 - 3 * C, rows = P.B * P.T, R0 = blockIdx.x * 32 * RT;
   // GEMM1: gate tile nt = wave, filter tile nt = 8 + wave.  Weight fragments stream from
   // L2 through a register ring WD k-steps deep (the loop is fully unrolled, so every
   // wait is a partial vmcnt): the L2 latency hides behind WD steps of MFMAs.  The ring
@@ -93,45 +103,52 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
   for (int i = 0; i < WD0; ++i) { rg[i] = wg[i * 64]; rf[i] = wf[i * 64]; }
   // stage [x(t-d)+dp; x(t)+dp; x(t+d)+dp; cond] as bf16 (zero outside each row's utterance).
   // Thread tid always owns column group g = 4 (tid % 256) (so its tap/channel is fixed)
-  // and rows tid/256 + 2 it; all 16 loads are issued before any is used (clamped
-  // addresses, masked afterwards) instead of one branch-guarded round trip each.
+  // and rows tid/256 + 2 it; all 16 loads of a 32-row half are issued before any is used
+  // (clamped addresses, masked afterwards) instead of one branch-guarded round trip each.
   constexpr int NGR = K1 / 4, IT = 32 * NGR / 512;
   static_assert(NGR == 256 && IT == 16, "staging map assumes K1 = 1024");
   const int g = (tid & (NGR - 1)) * 4, r0 = tid / NGR;
   const bool isx = g < 3 * C;
   const int tap = g / C, c = isx ? g - tap * C : g - 3 * C, sh = (tap - 1) * P.dil;
-  float4 sv[IT], dv[IT];
-  float ok[IT];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int R = R0 + r0 + 2 * it;
-    const int Rc = R < rows ? R : rows - 1;
-    const int b = Rc / P.T, t = Rc - b * P.T, tt = isx ? t + sh : t;
-    const bool v = R < rows && tt >= 0 && tt < P.T;
-    const int ttc = tt < 0 ? 0 : tt >= P.T ? P.T - 1 : tt;
-    ok[it] = v ? 1.f : 0.f;
-    const float* src = isx ? P.xin + ((long long)b * P.T + ttc) * C + c : P.cond + ((long long)b * P.T + ttc) * H + c;
-    sv[it] = *reinterpret_cast<const float4*>(src);
-    dv[it] = isx ? *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  for (int half = 0; half < RT; ++half) {
+    float4 sv[IT], dv[IT];
+    float ok[IT];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const float m = ok[it];
-    const float4 v = sv[it], d = dv[it];
-    *reinterpret_cast<bf16x4*>(&As[(r0 + 2 * it) * LDA + g]) =
-        bf16x4{(__bf16)((v.x + d.x) * m), (__bf16)((v.y + d.y) * m), (__bf16)((v.z + d.z) * m),
-               (__bf16)((v.w + d.w) * m)};
+    for (int it = 0; it < IT; ++it) {
+      const int R = R0 + 32 * half + r0 + 2 * it;
+      const int Rc = R < rows ? R : rows - 1;
+      const int b = Rc / P.T, t = Rc - b * P.T, tt = isx ? t + sh : t;
+      const bool v = R < rows && tt >= 0 && tt < P.T;
+      const int ttc = tt < 0 ? 0 : tt >= P.T ? P.T - 1 : tt;
+      ok[it] = v ? 1.f : 0.f;
+      const float* src = isx ? P.xin + ((long long)b * P.T + ttc) * C + c : P.cond + ((long long)b * P.T + ttc) * H + c;
+      sv[it] = *reinterpret_cast<const float4*>(src);
+      dv[it] = isx ? *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const float m = ok[it];
+      const float4 v = sv[it], d = dv[it];
+      *reinterpret_cast<bf16x4*>(&As[(32 * half + r0 + 2 * it) * LDA + g]) =
+          bf16x4{(__bf16)((v.x + d.x) * m), (__bf16)((v.y + d.y) * m), (__bf16)((v.z + d.z) * m),
+                 (__bf16)((v.w + d.w) * m)};
+    }
   }
 #pragma unroll
   for (int i = WD0; i < WD; ++i) { rg[i] = wg[i * 64]; rf[i] = wf[i * 64]; }
   __syncthreads();
-  f32x16 ag, af;
+  f32x16 ag[RT], af[RT];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { ag[r] = 0.f; af[r] = 0.f; }
+  for (int q = 0; q < RT; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { ag[q][r] = 0.f; af[q][r] = 0.f; }
   bf16x8 r2a[WD2], r2b[WD2];
 #pragma unroll
   for (int ks = 0; ks < KS1; ++ks) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[r32 * LDA + ks * 16 + h * 8]);
+    bf16x8 a[RT];
+#pragma unroll
+    for (int q = 0; q < RT; ++q) a[q] = *reinterpret_cast<const bf16x8*>(&As[(32 * q + r32) * LDA + ks * 16 + h * 8]);
     const bf16x8 bgt = rg[ks % WD], bft = rf[ks % WD];
     if (ks + WD < KS1) {
       rg[ks % WD] = wg[(ks + WD) * 64];
@@ -141,22 +158,28 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
       r2b[ks + WD - KS1] = wsk[(ks + WD - KS1) * 64];
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the prefetch where it is (the scheduler sinks loads to their use)
-    ag = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bgt, ag, 0, 0, 0);
-    af = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bft, af, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < RT; ++q) {
+      ag[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], bgt, ag[q], 0, 0, 0);
+      af[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], bft, af[q], 0, 0, 0);
+    }
   }
+  if (RT > 1) __syncthreads();          // Gs aliases As: every wave is past its GEMM1 reads
   {
     const int n = wave * 32 + r32;
     const float bgv = P.b1[n], bfv = P.b1[C + n];
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int r = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      Gs[r * LDG + n] = (__bf16)gate_fast(ag[reg] + bgv, af[reg] + bfv);
-    }
+    for (int q = 0; q < RT; ++q)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int r = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        Gs[r * LDG + n] = (__bf16)gate_fast(ag[q][reg] + bgv, af[q][reg] + bfv);
+      }
   }
   __syncthreads();
 
   // GEMM2: residual tile nt = wave, skip tile nt = 8 + wave.  The epilogue's x / skip
-  // reads are issued first so they land under the MFMAs.
+  // reads of the first row tile are issued first so they land under the MFMAs.
   const int n = wave * 32 + r32;
   float xo[16], so[16];
 #pragma unroll
@@ -166,36 +189,219 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
     xo[reg] = P.xin[o];
     so[reg] = P.first ? 0.f : P.skip[o];
   }
-  f32x16 ar, as_;
+  f32x16 ar[RT], as_[RT];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { ar[r] = 0.f; as_[r] = 0.f; }
+  for (int q = 0; q < RT; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { ar[q][r] = 0.f; as_[q][r] = 0.f; }
 #pragma unroll
   for (int ks = 0; ks < KS2; ++ks) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Gs[r32 * LDG + ks * 16 + h * 8]);
+    bf16x8 a[RT];
+#pragma unroll
+    for (int q = 0; q < RT; ++q) a[q] = *reinterpret_cast<const bf16x8*>(&Gs[(32 * q + r32) * LDG + ks * 16 + h * 8]);
     const bf16x8 b0 = r2a[ks % WD2], b1 = r2b[ks % WD2];
     if (ks + WD2 < KS2) {
       r2a[ks % WD2] = wr[(ks + WD2) * 64];
       r2b[ks % WD2] = wsk[(ks + WD2) * 64];
     }
     __builtin_amdgcn_sched_barrier(0);
-    ar = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0, ar, 0, 0, 0);
-    as_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b1, as_, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < RT; ++q) {
+      ar[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b0, ar[q], 0, 0, 0);
+      as_[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b1, as_[q], 0, 0, 0);
+    }
   }
   const float brv = P.b2[n], bsv = P.b2[C + n];
   const float rs2 = 0.70710678118654752440f;
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int R = R0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-    if (R < rows) {
-      const long long o = (long long)R * C + n;      // rows are b*T + t: contiguous [B][T][C]
-      P.xout[o] = (xo[reg] + ar[reg] + brv) * rs2;
-      P.skip[o] = so[reg] + as_[reg] + bsv;
+  for (int q = 0; q < RT; ++q)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int R = R0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (R < rows) {
+        const long long o = (long long)R * C + n;      // rows are b*T + t: contiguous [B][T][C]
+        const float xv = q == 0 ? xo[reg] : P.xin[o];
+        const float sv = q == 0 ? so[reg] : (P.first ? 0.f : P.skip[o]);
+        P.xout[o] = (xv + ar[q][reg] + brv) * rs2;
+        P.skip[o] = sv + as_[q][reg] + bsv;
+      }
+    }
+}
+
+// ------------------------------------------------------------------ two-GEMM residual layer (bf16)
+// The same layer as wn_layer_bf16_kernel as two launches with 128 x 128 tiles
+// (wavenet.py:60-72):
+//   GATE     g = sigmoid(W1_g . a + b_g) * tanh(W1_f . a + b_f),  a = [xa(t-d); xa(t); xa(t+d); cond(t)]
+//   RESSKIP  o = W2 . g + b2;  x = (x + o[:C]) / sqrt2 (and xa' = bf16(x + dp of the next layer));
+//            skip (+)= o[C:]
+// The fused kernel holds 32 frames and streams all 1.3 MB of a layer's weights through
+// every block, so it is bound by the L2 -> CU port (about 64 B/clk/CU; its MFMA needs four
+// times that).  Here a block reuses each 128-row weight tile for 128 frames (A = weights
+// staged in LDS, B = activations; both k-contiguous, double-buffered 64-k stages): about as
+// many bytes per MFMA as the port delivers.  The activations the GATE GEMM reads are bf16
+// copies kept beside the fp32 state: xa = bf16(x + dp_l) (written by the previous RESSKIP
+// epilogue, which knows dp_{l+1}) and condb = bf16(cond) (once per call).  x and skip stay fp32.
+// GATE block (bx, cg): frames [128 bx, +128), gate channels [64 cg, +64) and their filter
+// channels; RESSKIP block (bx, nt): output channels [128 nt, +128) (nt < C/128: residual).
+constexpr int WG_BM = 128, WG_BN = 128, WG_KC = 64, WG_LD = 72;
+enum { WG_GATE = 0, WG_RESSKIP = 1 };
+
+struct WnGemmArgs {
+  const __bf16* W;       // [N][ldw] bf16 weights (rows = output channels, k contiguous)
+  int ldw, K;
+  const float* bias;     // [N]
+  const __bf16* xa;      // GATE: [rows][C] bf16(x + dp_l)
+  const __bf16* condb;   // GATE: [rows][H] bf16(cond)
+  __bf16* g;             // GATE: out / RESSKIP: in, [rows][C] bf16
+  float* x;              // RESSKIP: [rows][C] fp32 residual state, updated in place
+  float* skip;           // RESSKIP: [rows][C] fp32
+  __bf16* xa_next;       // RESSKIP: [rows][C] bf16(x + dp_{l+1}) or null (last layer)
+  const float* dp_next;  // RESSKIP: dp_{l+1}[b * dp_ld + c]
+  int dp_ld, first, nt0;
+  int B, T, C, H, dil;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(512, 2) void wn_gemm_bf16_kernel(const WnGemmArgs P) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][WG_BN * WG_LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][WG_BM * WG_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n32 = lane & 31, h = lane >> 5;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int C = P.C, T = P.T, rows = P.B * P.T, R0 = blockIdx.x * WG_BM;
+  const int cg = blockIdx.y;                          // GATE: channel group; RESSKIP: output tile
+  // weight row of LDS A row i
+  auto wrow = [&](int i) {
+    if (MODE == WG_GATE) return i < 64 ? 64 * cg + i : C + 64 * cg + (i - 64);
+    return WG_BN * (cg + P.nt0) + i;
+  };
+  // this thread's two 16-B pieces of a stage: piece p -> row p >> 3, k offset (p & 7) * 8
+  uint4 ra[2], rb[2];
+  auto load = [&](int kc) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = tid + 512 * q, row = p >> 3, kk = kc * WG_KC + (p & 7) * 8;
+      ra[q] = *reinterpret_cast<const uint4*>(P.W + (long long)wrow(row) * P.ldw + kk);
+      const int R = R0 + row;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (R < rows) {
+        if (MODE == WG_GATE) {
+          const int b = R / T, t = R - b * T;
+          if (kk < 3 * C) {
+            const int tap = kk / C, c = kk - tap * C, tt = t + (tap - 1) * P.dil;
+            if (tt >= 0 && tt < T) v = *reinterpret_cast<const uint4*>(P.xa + ((long long)b * T + tt) * C + c);
+          } else {
+            v = *reinterpret_cast<const uint4*>(P.condb + (long long)R * P.H + (kk - 3 * C));
+          }
+        } else {
+          v = *reinterpret_cast<const uint4*>(P.g + (long long)R * C + kk);
+        }
+      }
+      rb[q] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = tid + 512 * q, row = p >> 3, col = (p & 7) * 8;
+      *reinterpret_cast<uint4*>(&As[buf][row * WG_LD + col]) = ra[q];
+      *reinterpret_cast<uint4*>(&Bs[buf][row * WG_LD + col]) = rb[q];
+    }
+  };
+  // wave (wm, wn): frames 32 wm.., weight tiles t0 = LDS rows [32 wn, +32) and t1 = [64 + 32 wn, +32)
+  // (GATE: the gate and the filter half of the same 32 channels) or [64 wn, +32), [64 wn + 32, +32)
+  const int t0 = MODE == WG_GATE ? 32 * wn : 64 * wn, t1 = MODE == WG_GATE ? 64 + 32 * wn : 64 * wn + 32;
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
+  const int NKC = P.K / WG_KC;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kc = 0; kc < NKC; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < NKC) load(kc + 1);
+#pragma unroll
+    for (int ks = 0; ks < WG_KC / 16; ++ks) {
+      const bf16x8 bx = *reinterpret_cast<const bf16x8*>(&Bs[buf][(32 * wm + n32) * WG_LD + ks * 16 + 8 * h]);
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&As[buf][(t0 + n32) * WG_LD + ks * 16 + 8 * h]);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&As[buf][(t1 + n32) * WG_LD + ks * 16 + 8 * h]);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bx, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bx, acc1, 0, 0, 0);
+    }
+    if (kc + 1 < NKC) store(buf ^ 1);
+    __syncthreads();
+  }
+  // C[n][m]: lane (frame m = 32 wm + n32, h) holds weight rows (reg&3) + 8(reg>>2) + 4h of each tile
+  const int R = R0 + 32 * wm + n32;
+  if (R >= rows) return;
+  if (MODE == WG_GATE) {
+    const int ch0 = 64 * cg + 32 * wn;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = ch0 + 8 * i + 4 * h;
+      const float4 bg = *reinterpret_cast<const float4*>(P.bias + c);
+      const float4 bf = *reinterpret_cast<const float4*>(P.bias + C + c);
+      *reinterpret_cast<bf16x4*>(P.g + (long long)R * C + c) =
+          bf16x4{(__bf16)gate_fast(acc0[4 * i] + bg.x, acc1[4 * i] + bf.x),
+                 (__bf16)gate_fast(acc0[4 * i + 1] + bg.y, acc1[4 * i + 1] + bf.y),
+                 (__bf16)gate_fast(acc0[4 * i + 2] + bg.z, acc1[4 * i + 2] + bf.z),
+                 (__bf16)gate_fast(acc0[4 * i + 3] + bg.w, acc1[4 * i + 3] + bf.w)};
+    }
+  } else {
+    const int b = R / T;
+    const float rs2 = 0.70710678118654752440f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const f32x16& acc = q ? acc1 : acc0;
+      const int n0 = WG_BN * (cg + P.nt0) + (q ? t1 : t0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + 8 * i + 4 * h;
+        const float4 bb = *reinterpret_cast<const float4*>(P.bias + n);
+        const float4 o = make_float4(acc[4 * i] + bb.x, acc[4 * i + 1] + bb.y, acc[4 * i + 2] + bb.z,
+                                     acc[4 * i + 3] + bb.w);
+        if (n < C) {
+          float4* xp = reinterpret_cast<float4*>(P.x + (long long)R * C + n);
+          const float4 xv = *xp;
+          const float4 xn = make_float4((xv.x + o.x) * rs2, (xv.y + o.y) * rs2, (xv.z + o.z) * rs2,
+                                        (xv.w + o.w) * rs2);
+          *xp = xn;
+          if (P.xa_next) {
+            const float4 d = *reinterpret_cast<const float4*>(P.dp_next + (long long)b * P.dp_ld + n);
+            *reinterpret_cast<bf16x4*>(P.xa_next + (long long)R * C + n) =
+                bf16x4{(__bf16)(xn.x + d.x), (__bf16)(xn.y + d.y), (__bf16)(xn.z + d.z), (__bf16)(xn.w + d.w)};
+          }
+        } else {
+          float4* sp = reinterpret_cast<float4*>(P.skip + (long long)R * C + (n - C));
+          const float4 sv = P.first ? make_float4(0.f, 0.f, 0.f, 0.f) : *sp;
+          *sp = make_float4(sv.x + o.x, sv.y + o.y, sv.z + o.z, sv.w + o.w);
+        }
+      }
     }
   }
 }
 
+// xa = bf16(x + dp[b]) (layer 0's GATE input) and, when cond is given, condb = bf16(cond)
+__global__ void wn_xa_kernel(const float* __restrict__ x, const float* __restrict__ dp, int dp_ld,
+                             __bf16* __restrict__ xa, const float* __restrict__ cond, __bf16* __restrict__ condb,
+                             int rows, int T, int C, int H) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i < (long long)rows * C) {
+    const long long R = i / C;
+    const int c = (int)(i - R * C), b = (int)(R / T);
+    const float4 v = *reinterpret_cast<const float4*>(x + i);
+    const float4 d = *reinterpret_cast<const float4*>(dp + (long long)b * dp_ld + c);
+    *reinterpret_cast<bf16x4*>(xa + i) = bf16x4{(__bf16)(v.x + d.x), (__bf16)(v.y + d.y), (__bf16)(v.z + d.z),
+                                                 (__bf16)(v.w + d.w)};
+  }
+  if (cond && i < (long long)rows * H) {
+    const float4 v = *reinterpret_cast<const float4*>(cond + i);
+    *reinterpret_cast<bf16x4*>(condb + i) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+  }
+}
+
 struct WsLayout {
-  size_t x, x2, g, skip, hs, xin, condT, outT, steps, emb, h1, d, dproj, total;
+  size_t x, x2, g, skip, hs, xin, condT, outT, steps, emb, h1, d, dproj, xa, condb, total;
 };
 
 WsLayout ws_layout(const pd_wavenet* h, int B, int T, int S) {
@@ -220,6 +426,8 @@ WsLayout ws_layout(const pd_wavenet* h, int B, int T, int S) {
   w.h1 = take((size_t)S * B * 4 * h->C);
   w.d = take((size_t)S * B * h->C);
   w.dproj = take((size_t)S * B * h->L * h->C);
+  w.xa = take(BT * h->C / 2 + 8);                 // bf16 [B*T][C] (two-GEMM layer path)
+  w.condb = take(BT * h->H / 2 + 8);              // bf16 [B*T][H]
   w.total = off * sizeof(float);
   return w;
 }
@@ -258,7 +466,45 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     a.act = ACT_RELU;
     PD_TRY((launch_small_gemm<EPI_STORE, U_WN_INPROJ>(a, st, "wn_inproj")));
   }
-  if (h->W1f) {
+  if (h->W1f && h->layer_mode == 1 && C % WG_BN == 0 && (3 * C + H) % WG_KC == 0 && H % 8 == 0) {
+    // bf16: two launches per residual layer with 128 x 128 tiles (wn_gemm_bf16_kernel)
+    const int rows = B * T;
+    __bf16* xa = reinterpret_cast<__bf16*>(ws + Lw.xa);
+    __bf16* condb = reinterpret_cast<__bf16*>(ws + Lw.condb);
+    __bf16* gb = reinterpret_cast<__bf16*>(ws + Lw.g);
+    {
+      const long long n4 = ((long long)rows * (C > H ? C : H) + 3) / 4;
+      hipLaunchKernelGGL(wn_xa_kernel, dim3(cdiv(n4, 256)), dim3(256), 0, st, x, dproj, Ly * C, xa, cond, condb,
+                         rows, T, C, H);
+      PD_LAUNCH_CHECK();
+    }
+    const __bf16* W1 = lookup_bf16(h->Wl1);
+    const __bf16* W2 = lookup_bf16(h->Wl2);
+    const int K1 = 3 * C + H;
+    for (int l = 0; l < Ly; ++l) {
+      WnGemmArgs P{};
+      P.B = B; P.T = T; P.C = C; P.H = H; P.dil = 1 << (l % h->cyc);
+      P.W = W1 + (size_t)l * 2 * C * h->ldw1; P.ldw = h->ldw1; P.K = K1; P.bias = h->bl1 + (size_t)l * 2 * C;
+      P.xa = xa; P.condb = condb; P.g = gb;
+      {
+        ProfScope ps("wn_gate2", st);
+        hipLaunchKernelGGL(wn_gemm_bf16_kernel<WG_GATE>, dim3(cdiv(rows, WG_BM), C / 64), dim3(512), 0, st, P);
+        PD_LAUNCH_CHECK();
+      }
+      const bool last = l == Ly - 1;
+      P.W = W2 + (size_t)l * 2 * C * C; P.ldw = C; P.K = C; P.bias = h->bl2 + (size_t)l * 2 * C;
+      P.x = x; P.skip = skip; P.first = l == 0;
+      P.xa_next = last ? nullptr : xa; P.dp_next = last ? nullptr : dproj + (size_t)(l + 1) * C; P.dp_ld = Ly * C;
+      // the last layer's residual half feeds nothing (wavenet.py:115-119 keeps only skip)
+      P.nt0 = last ? C / WG_BN : 0;
+      {
+        ProfScope ps("wn_resskip2", st);
+        hipLaunchKernelGGL(wn_gemm_bf16_kernel<WG_RESSKIP>, dim3(cdiv(rows, WG_BM), (last ? C : 2 * C) / WG_BN),
+                           dim3(512), 0, st, P);
+        PD_LAUNCH_CHECK();
+      }
+    }
+  } else if (h->W1f) {
     // bf16, C == 256: one fused launch per residual layer, x ping-pongs x <-> x2
     float* xb[2] = {x, ws + Lw.x2};
     for (int l = 0; l < Ly; ++l) {
@@ -269,7 +515,14 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       P.W2f = h->W2f + (size_t)l * 2 * C * C; P.b2 = h->bl2 + (size_t)l * 2 * C;
       P.B = B; P.T = T; P.H = H; P.dil = 1 << (l % h->cyc); P.first = (l == 0);
       ProfScope ps("wn_layer", st);
-      hipLaunchKernelGGL(wn_layer_bf16_kernel<1024>, dim3(cdiv((long long)B * T, 32)), dim3(512), 0, st, P);
+      // auto: 64-frame blocks once they still fill every CU (r02: B=32 x 861 frames 73 vs 88 us per
+      // layer), else 32-frame blocks (B=8: 108 blocks of 64 frames leave half the chip idle, 37 vs 27 us)
+      if (h->layer_mode == 2 && cdiv((long long)B * T, 64) >= 256)
+        hipLaunchKernelGGL((wn_layer_bf16_kernel<1024, 2>), dim3(cdiv((long long)B * T, 64)), dim3(512), 0, st, P);
+      else if (h->layer_mode == 3)
+        hipLaunchKernelGGL((wn_layer_bf16_kernel<1024, 2>), dim3(cdiv((long long)B * T, 64)), dim3(512), 0, st, P);
+      else
+        hipLaunchKernelGGL((wn_layer_bf16_kernel<1024, 1>), dim3(cdiv((long long)B * T, 32)), dim3(512), 0, st, P);
       PD_LAUNCH_CHECK();
     }
   } else
@@ -419,6 +672,17 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
   }
   *out = h;
   return PD_OK;
+}
+
+int pd_wavenet_set_option(pd_wavenet* h, int option, int value) {
+  PD_CHECK_ARG(h, "null pointer");
+  if (option == PD_WN_OPT_LAYER) {
+    PD_CHECK_ARG(value >= 0 && value <= 3, "PD_WN_OPT_LAYER is 0, 1, 2 or 3");
+    h->layer_mode = value;
+    return PD_OK;
+  }
+  set_error("pd_wavenet_set_option: unknown option " + std::to_string(option));
+  return PD_ERR_ARG;
 }
 
 void pd_wavenet_destroy(pd_wavenet* h) {

@@ -57,6 +57,7 @@ class WaveNet(nn.Module):
         self.output_projection = nn.Conv1d(C, in_dims, 1)
         nn.init.zeros_(self.output_projection.weight)
         self.compute_dtype = "fp32"
+        self._options = {}
         self._h = None
         self._sig = None
         self._ws = _lib.Workspace()
@@ -66,6 +67,14 @@ class WaveNet(nn.Module):
         if dtype not in ("fp32", "bf16"):
             raise ValueError(dtype)
         self.compute_dtype = dtype
+        return self
+
+    def set_options(self, **opts):
+        """Kernel-variant options (pd_wavenet_set_option, include/prodiff_hip.h PD_WN_OPT_*): layer."""
+        for k, v in opts.items():
+            if k not in _lib.WN_OPTIONS:
+                raise ValueError(f"unknown WaveNet option {k!r}")
+            self._options[k] = int(v)
         return self
 
     # ----------------------------------------------------------- packing
@@ -85,7 +94,7 @@ class WaveNet(nn.Module):
     def handle(self):
         """The packed C handle; re-packed whenever a parameter is replaced or modified."""
         ps = self.ordered_params()
-        sig = (self.compute_dtype,) + tuple((p.data_ptr(), p._version) for p in ps)
+        sig = (self.compute_dtype, tuple(sorted(self._options.items()))) + tuple((p.data_ptr(), p._version) for p in ps)
         if self._h is not None and sig == self._sig:
             return self._h
         L = _lib.lib()
@@ -100,6 +109,11 @@ class WaveNet(nn.Module):
         dt = _lib.PD_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.PD_DTYPE_F32
         _lib.check(L.pd_wavenet_create(_lib.C.byref(dims), arr, dt,
                                        _lib.stream_ptr(dev), _lib.C.byref(h)))
+        for k, v in self._options.items():
+            rc = L.pd_wavenet_set_option(h, _lib.WN_OPTIONS[k], v)
+            if rc != 0:
+                L.pd_wavenet_destroy(h)
+                _lib.check(rc)
         self._release()
         self._h, self._sig = h, sig
         self._keep = tensors   # the pack is stream-ordered; keep sources alive

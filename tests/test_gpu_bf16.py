@@ -22,16 +22,20 @@ def tt(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
+@pytest.mark.parametrize("layer", [3, 0, 1])
 @pytest.mark.parametrize("name", ["wavenet_m80_c256_l20_cyc1", "wavenet_m64_c256_l20_cyc5",
                                   "wavenet_m80_c64_l4_cyc2"])
-def test_wavenet_bf16(name):
+def test_wavenet_bf16(name, layer):
+    """Every bf16 residual-layer kernel (PD_WN_OPT_LAYER: 3 = fused, 64 frames per block; 0 =
+    fused, 32 frames; 1 = two 128x128-tile GEMMs; the default 2 picks 3 or 0 by grid size)
+    against the reference goldens."""
     d = G.load(name)
     M, H, L, C, cyc = [int(v) for v in d["dims"]]
     net = WaveNet(M, H, L, C, cyc)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in G.wavenet_params(d["dims"], d["seed"]).items()})
-    net = net.to(DEV).set_compute_dtype("bf16")
+    net = net.to(DEV).set_compute_dtype("bf16").set_options(layer=layer)
     out = net(tt(d["spec"]), tt(d["steps"]), tt(d["cond"])).cpu().numpy()
-    assert_bf16_close(out, d["out"], name)
+    assert_bf16_close(out, d["out"], f"{name} layer={layer}")
 
 
 @pytest.mark.parametrize("name", ["prodiff_t2_m80", "prodiff_t4_m128"])
