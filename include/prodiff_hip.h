@@ -272,6 +272,71 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
                 const float* noise, unsigned long long seed, float* wav, int B, int T,
                 void* workspace, size_t ws_bytes, void* stream);
 
+/* ============================================================ condition encoder
+ * SVS teacher condition -- replaces ProDiffTeacher.forward_condition
+ * (modules/svs/prodiff_teacher.py:103-146): FastspeechEncoder (modules/fastspeech/
+ * tts_modules.py:232-330: token + position embedding, enc_layers x EncSALayer with 2-head
+ * self-attention and the k=9 conv FFN, final LayerNorm), mel2ph_to_dur (:223-229), the
+ * mel2ph length-regulator gather and the pitch / speaker / gender / voicing / breath sums.
+ */
+typedef struct pd_cond pd_cond;
+
+typedef struct {
+  int vocab_size;            /* len(ph_encoder)                         prodiff_teacher.py:13 */
+  int hidden_size;           /* H: 256 (handler/base_config.yaml:112), multiple of 64       */
+  int enc_layers;            /* 4                                                            */
+  int enc_ffn_kernel_size;   /* 9 (odd, <= 11)                                               */
+  int num_heads;             /* 2; head dim H / num_heads in {64, 128, 256}                  */
+  int num_spk;               /* spk_embed rows                                               */
+  int num_langs;             /* lang_embed rows = len(hparams["languages"]) + 1              */
+  int use_dur_embed, use_spk_id, use_gender_id, use_lang_id, use_voicing_embed, use_breath_embed;
+} pd_cond_dims;
+
+/* Parameter order = the reference state-dict order (buffers and `diffusion.*` skipped), fp32:
+ *   for l < enc_layers: encoder.layers.l.op.{layer_norm1.weight, layer_norm1.bias,
+ *       self_attn.in_proj_weight [3H,H], self_attn.out_proj.weight [H,H], layer_norm2.weight,
+ *       layer_norm2.bias, ffn.ffn_1.weight [4H,H,k], ffn.ffn_1.bias, ffn.ffn_2.weight [H,4H],
+ *       ffn.ffn_2.bias},
+ *   encoder.layer_norm.{weight,bias}, encoder.embed_tokens.weight [V,H],
+ *   [dur_embed.{weight [H,1],bias}], [spk_embed.weight], [gender_embed.weight [2,H]],
+ *   [lang_embed.weight], pitch_embed.{weight,bias}, [voicing_embed.{weight,bias}],
+ *   [breath_embed.{weight,bias}]   ([...] present iff its use_* flag is set).
+ * The reference's add_gender_embed looks gender ids up in lang_embed (prodiff_teacher.py:95);
+ * that is reproduced, so use_gender_id requires use_lang_id. */
+int pd_cond_num_params(const pd_cond_dims* dims);
+int pd_cond_create(const pd_cond_dims* dims, const float* const* params, int dtype, void* stream,
+                   pd_cond** out);
+void pd_cond_destroy(pd_cond* h);
+size_t pd_cond_workspace_size(const pd_cond* h, int B, int T_txt, int T_mel);
+
+/* forward_condition's inputs, all device pointers (int64 = torch.long), NULL when absent:
+ *   txt_tokens [B,T_txt] (0 = padding), mel2ph [B,T_mel] (0 = padding frame, else token
+ *   index + 1, <= T_txt), f0 [B,T_mel] Hz, lang_seq [B,T_txt], spk_embed_id [B] or
+ *   spk_mix_embed [B, spk_mix_frames (1 or T_mel), H], gender_embed_id [B] or
+ *   gender_mix_embed [B, gender_mix_frames, H], voicing [B,T_mel], breath [B,T_mel].
+ * Embedding ids outside their table (an IndexError in the reference) are clamped on the device
+ * and mel2ph values above T_txt give zero frames, so a malformed input cannot fault the GPU. */
+typedef struct {
+  const long long* txt_tokens;
+  const long long* mel2ph;
+  const float* f0;
+  const long long* lang_seq;
+  const long long* spk_embed_id;
+  const float* spk_mix_embed;
+  int spk_mix_frames;
+  const long long* gender_embed_id;
+  const float* gender_mix_embed;
+  int gender_mix_frames;
+  const float* voicing;
+  const float* breath;
+} pd_cond_inputs;
+
+/* cond [B,T_mel,H] time-major (what pd_prodiff_sample / pd_reflow_sample take), and optionally
+ * enc_out [B,T_txt,H] = the FastspeechEncoder output (tts_modules.py:310-317); either may be
+ * NULL (not both).  Every utterance needs at least one non-padding token. */
+int pd_cond_forward(const pd_cond* h, const pd_cond_inputs* in, float* cond, float* enc_out, int B,
+                    int T_txt, int T_mel, void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,160 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+CPU (numpy, float64) restatement of the SVS teacher's condition stage,
+``ProDiffTeacher.forward_condition``, used by ``tests/`` as the checker of
+``pd_cond_forward``.  Nothing in ``prodiff_amd`` imports it.
+
+Pinned against ``tests/golden/cond_*.npz``, which ``tests/golden/gen_golden.py``
+produced by running the reference teacher itself (tests/test_oracle.py).
+
+Follows:
+  * forward_condition   -- modules/svs/prodiff_teacher.py:103-146 (+ add_spk_embed :84-89,
+                           add_gender_embed :91-95 -- ids index lang_embed there, add_pitch :97-100)
+  * mel2ph_to_dur       -- modules/fastspeech/tts_modules.py:223-229
+  * FastspeechEncoder   -- tts_modules.py:291-330 (forward_embedding), FFTBlocks.forward :264-289
+  * positions           -- utils/tts_utils.py:6-18 (make_positions),
+                           modules/commons/common_layers.py:111-149 (SinusoidalPositionalEmbedding)
+  * EncSALayer          -- common_layers.py:625-674; TransformerFFNLayer :542-583;
+                           MultiheadAttention :172-300 (torch multi_head_attention_forward, bias=False)
+  * LayerNorm           -- common_layers.py:76-83 (eps 1e-5); FFTBlocks' final nn.LayerNorm
+"""
+import math
+
+import numpy as np
+
+
+def mel2ph_to_dur(mel2ph, T_txt):
+    """tts_modules.py:223-229: dur[b, t] = #{f : mel2ph[b, f] == t + 1}."""
+    B = mel2ph.shape[0]
+    dur = np.zeros((B, T_txt + 1), np.int64)
+    for b in range(B):
+        np.add.at(dur[b], mel2ph[b], 1)
+    return dur[:, 1:]
+
+
+def sinusoid_table(n, dim, padding_idx=0):
+    """common_layers.py:111-128 (float32 as the reference builds it)."""
+    half = dim // 2
+    e = math.log(10000) / (half - 1)
+    f = np.exp(np.arange(half, dtype=np.float32) * np.float32(-e)).astype(np.float32)
+    a = (np.arange(n, dtype=np.float32)[:, None] * f[None, :]).astype(np.float32)
+    emb = np.concatenate([np.sin(a), np.cos(a)], axis=1).astype(np.float64)
+    if dim % 2 == 1:
+        emb = np.concatenate([emb, np.zeros((n, 1))], axis=1)
+    emb[padding_idx] = 0
+    return emb
+
+
+def make_positions(nonpad):
+    """utils/tts_utils.py:6-18 on ~padding_mask (padding_idx 0)."""
+    m = nonpad.astype(np.int64)
+    return np.cumsum(m, axis=1) * m
+
+
+def layer_norm(x, g, b, eps=1e-5):
+    mu = x.mean(-1, keepdims=True)
+    var = ((x - mu) ** 2).mean(-1, keepdims=True)
+    return (x - mu) / np.sqrt(var + eps) * g + b
+
+
+def gelu(x):
+    from scipy.special import erf
+    return 0.5 * x * (1.0 + erf(x / math.sqrt(2.0)))
+
+
+def self_attention(x, w_in, w_out, key_pad, heads):
+    """MultiheadAttention (bias=False) with key_padding_mask; x [B,T,H]."""
+    B, T, H = x.shape
+    D = H // heads
+    qkv = x @ w_in.T
+    q, k, v = qkv[..., :H], qkv[..., H:2 * H], qkv[..., 2 * H:]
+    q = q * (D ** -0.5)
+    out = np.zeros_like(x)
+    for h in range(heads):
+        sl = slice(h * D, (h + 1) * D)
+        s = np.einsum("btd,bsd->bts", q[..., sl], k[..., sl])
+        s = np.where(key_pad[:, None, :], -np.inf, s)
+        s = s - s.max(-1, keepdims=True)
+        p = np.exp(s)
+        p /= p.sum(-1, keepdims=True)
+        out[..., sl] = np.einsum("bts,bsd->btd", p, v[..., sl])
+    return out @ w_out.T
+
+
+def ffn(x, w1, b1, w2, b2):
+    """TransformerFFNLayer (SAME padding, gelu): conv_k -> * k^-0.5 -> gelu -> linear."""
+    B, T, H = x.shape
+    F, _, k = w1.shape
+    p = k // 2
+    xp = np.pad(x, ((0, 0), (p, p), (0, 0)))
+    y = np.zeros((B, T, F))
+    for j in range(k):
+        y += xp[:, j:j + T, :] @ w1[:, :, j].T
+    y = gelu((y + b1) * k ** -0.5)
+    return y @ w2.T + b2
+
+
+def encoder(P, hp, txt_tokens, extra_embed):
+    """FastspeechEncoder.forward (tts_modules.py:310-317)."""
+    H = hp["hidden_size"]
+    pad = txt_tokens == 0
+    nonpad = (~pad)[..., None].astype(np.float64)
+    x = math.sqrt(H) * P["encoder.embed_tokens.weight"][txt_tokens]
+    if extra_embed is not None:
+        x = x + extra_embed
+    pos = make_positions(~pad)
+    x = x + sinusoid_table(int(pos.max()) + 1, H)[pos]
+    x = x * nonpad
+    for l in range(hp["enc_layers"]):
+        pre = f"encoder.layers.{l}.op."
+        r = x
+        y = layer_norm(x, P[pre + "layer_norm1.weight"], P[pre + "layer_norm1.bias"])
+        y = self_attention(y, P[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.out_proj.weight"],
+                           pad, hp["num_heads"])
+        x = (r + y) * nonpad
+        r = x
+        y = layer_norm(x, P[pre + "layer_norm2.weight"], P[pre + "layer_norm2.bias"])
+        y = ffn(y, P[pre + "ffn.ffn_1.weight"], P[pre + "ffn.ffn_1.bias"],
+                P[pre + "ffn.ffn_2.weight"], P[pre + "ffn.ffn_2.bias"])
+        x = (r + y) * nonpad
+    return layer_norm(x, P["encoder.layer_norm.weight"], P["encoder.layer_norm.bias"]) * nonpad
+
+
+def lin1(P, name, v):
+    """Linear(1, H) applied to v[..., None]."""
+    return v[..., None] * P[name + ".weight"][:, 0] + P[name + ".bias"]
+
+
+def forward_condition(P, hp, txt_tokens, mel2ph, f0, lang_seq=None, spk_embed_id=None, spk_mix_embed=None,
+                      gender_embed_id=None, gender_mix_embed=None, voicing=None, breath=None, return_encoder=False):
+    """prodiff_teacher.py:103-146.  P: {state-dict key: float64 array}; hp: the teacher's hparams."""
+    P = {k: np.asarray(v, np.float64) for k, v in P.items()}
+    txt_tokens = np.asarray(txt_tokens, np.int64)
+    mel2ph = np.asarray(mel2ph, np.int64)
+    extra = None
+    if hp.get("use_dur_embed", True):
+        dur = mel2ph_to_dur(mel2ph, txt_tokens.shape[1]).astype(np.float64)
+        extra = lin1(P, "dur_embed", dur)
+    if hp.get("use_lang_id", True):
+        assert lang_seq is not None, "use_lang_embed is True, lang_seq is required"
+        extra = extra + P["lang_embed.weight"][np.asarray(lang_seq, np.int64)]
+    enc = encoder(P, hp, txt_tokens, extra)
+    B, T, H = enc.shape
+    padded = np.concatenate([np.zeros((B, 1, H)), enc], axis=1)
+    cond = np.take_along_axis(padded, mel2ph[..., None].repeat(H, -1), axis=1)
+    cond = cond + lin1(P, "pitch_embed", np.log(1 + np.asarray(f0, np.float64) / 700))
+    if hp.get("use_spk_id", True):
+        cond = cond + (np.asarray(spk_mix_embed, np.float64) if spk_mix_embed is not None
+                       else P["spk_embed.weight"][np.asarray(spk_embed_id, np.int64)][:, None, :])
+    if hp.get("use_gender_id", False):
+        cond = cond + (np.asarray(gender_mix_embed, np.float64) if gender_mix_embed is not None
+                       else P["lang_embed.weight"][np.asarray(gender_embed_id, np.int64)][:, None, :])
+    var = []
+    if hp.get("use_voicing_embed", False):
+        var.append(lin1(P, "voicing_embed", np.asarray(voicing, np.float64)))
+    if hp.get("use_breath_embed", False):
+        var.append(lin1(P, "breath_embed", np.asarray(breath, np.float64)))
+    if var:
+        cond = cond + sum(var)
+    cond = cond * (mel2ph > 0)[..., None]
+    return (cond, enc) if return_encoder else cond

@@ -46,6 +46,21 @@ class nsf_dims(C.Structure):
                 ("harmonic_num", C.c_int)]
 
 
+class pd_cond_dims(C.Structure):
+    _fields_ = [("vocab_size", C.c_int), ("hidden_size", C.c_int), ("enc_layers", C.c_int),
+                ("enc_ffn_kernel_size", C.c_int), ("num_heads", C.c_int), ("num_spk", C.c_int),
+                ("num_langs", C.c_int), ("use_dur_embed", C.c_int), ("use_spk_id", C.c_int),
+                ("use_gender_id", C.c_int), ("use_lang_id", C.c_int), ("use_voicing_embed", C.c_int),
+                ("use_breath_embed", C.c_int)]
+
+
+class pd_cond_inputs(C.Structure):
+    _fields_ = [("txt_tokens", C.c_void_p), ("mel2ph", C.c_void_p), ("f0", C.c_void_p), ("lang_seq", C.c_void_p),
+                ("spk_embed_id", C.c_void_p), ("spk_mix_embed", C.c_void_p), ("spk_mix_frames", C.c_int),
+                ("gender_embed_id", C.c_void_p), ("gender_mix_embed", C.c_void_p), ("gender_mix_frames", C.c_int),
+                ("voicing", C.c_void_p), ("breath", C.c_void_p)]
+
+
 _VP = C.c_void_p
 _SIGS = {
     "pd_last_error": (C.c_char_p, []),
@@ -76,6 +91,12 @@ _SIGS = {
     "fd_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                             C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, C.c_int,
                             C.c_int, _VP, C.c_size_t, _VP]),
+    "pd_cond_num_params": (C.c_int, [C.POINTER(pd_cond_dims)]),
+    "pd_cond_create": (C.c_int, [C.POINTER(pd_cond_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
+    "pd_cond_destroy": (None, [_VP]),
+    "pd_cond_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
+    "pd_cond_forward": (C.c_int, [_VP, C.POINTER(pd_cond_inputs), _VP, _VP, C.c_int, C.c_int, C.c_int, _VP,
+                                  C.c_size_t, _VP]),
     "nsf_num_params": (C.c_int, [C.POINTER(nsf_dims)]),
     "nsf_create": (C.c_int, [C.POINTER(nsf_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
     "nsf_destroy": (None, [_VP]),
@@ -121,6 +142,18 @@ def fptr(t):
         raise HipError("libprodiff_hip needs device tensors (got a CPU tensor)")
     if t.dtype != torch.float32 or not t.is_contiguous():
         raise HipError(f"expected contiguous float32 tensor, got {t.dtype} contiguous={t.is_contiguous()}")
+    return C.c_void_p(t.data_ptr())
+
+
+def lptr(t):
+    """Device pointer of a contiguous int64 (torch.long) CUDA tensor, or None."""
+    if t is None:
+        return None
+    import torch
+    if not t.is_cuda:
+        raise HipError("libprodiff_hip needs device tensors (got a CPU tensor)")
+    if t.dtype != torch.int64 or not t.is_contiguous():
+        raise HipError(f"expected contiguous int64 tensor, got {t.dtype} contiguous={t.is_contiguous()}")
     return C.c_void_p(t.data_ptr())
 
 

@@ -52,7 +52,7 @@ const char* get_error();
 
 namespace pd {
 
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_MISH = 3, ACT_SWISH = 4, ACT_TANH = 5 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_MISH = 3, ACT_SWISH = 4, ACT_TANH = 5, ACT_GELU = 6 };
 
 __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
   switch (act) {
@@ -65,6 +65,12 @@ __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
     }
     case ACT_SWISH: return v / (1.f + expf(-v));
     case ACT_TANH: return tanhf(v);
+    case ACT_GELU: {
+      // exact (erf) GELU of alpha * v: the FFT-encoder FFN scales its conv output by
+      // kernel_size^-0.5 BEFORE the activation (common_layers.py:570-576)
+      const float x = v * alpha;
+      return 0.5f * x * (1.f + erff(x * 0.70710678118654752440f));
+    }
     default: return v;
   }
 }

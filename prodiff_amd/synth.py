@@ -129,6 +129,9 @@ def _gain(name):
     # NSF-HiFiGAN output conv feeds a tanh: keep it out of saturation
     if name.startswith("conv_post"):
         return 0.3
+    # durations reach tens of frames; keep dur * w at the embedding scale
+    if name.startswith("dur_embed"):
+        return 0.1
     return 1.0
 
 
@@ -142,6 +145,8 @@ def synth_tensor(name, shape, seed):
         return (_gain(name) * (1.0 + 0.1 * z)).astype(np.float32)
     if name.endswith(".weight_v"):
         return z
+    if "layer_norm" in name and name.endswith(".weight"):   # LayerNorm gamma ~ 1
+        return (1.0 + 0.1 * z).astype(np.float32)
     if "upsample" in name or name.startswith("ups."):   # ConvTranspose1d [Cin, Cout, k]: 2 taps hit each output
         fan_in = shape[0] * 2
     else:
@@ -207,3 +212,90 @@ def nsf_param_shapes(num_mels=128, upsample_initial_channel=512, upsample_rates=
     s["conv_post.weight"] = (1, ch0 // 2 ** len(upsample_rates), 7)
     s["conv_post.bias"] = (1,)
     return s
+
+
+# --------------------------------------------------------------------------
+# SVS teacher condition stage (modules/svs/prodiff_teacher.py:10-47, encoder
+# modules/fastspeech/tts_modules.py:291-308, layers common_layers.py:625-648)
+# --------------------------------------------------------------------------
+COND_DEFAULTS = dict(hidden_size=256, enc_layers=4, enc_ffn_kernel_size=9, num_heads=2, num_spk=1, num_langs=3,
+                     use_dur_embed=True, use_spk_id=True, use_gender_id=False, use_lang_id=True,
+                     use_voicing_embed=True, use_breath_embed=True)
+
+
+def cond_param_shapes(vocab_size, hidden_size=256, enc_layers=4, enc_ffn_kernel_size=9, num_spk=1, num_langs=3,
+                      use_dur_embed=True, use_spk_id=True, use_gender_id=False, use_lang_id=True,
+                      use_voicing_embed=True, use_breath_embed=True, **_):
+    """Ordered ``{state-dict key: shape}`` of the teacher minus ``diffusion.*`` and buffers."""
+    H, k = hidden_size, enc_ffn_kernel_size
+    s = OrderedDict()
+    for l in range(enc_layers):
+        p = f"encoder.layers.{l}.op."
+        s[p + "layer_norm1.weight"] = (H,)
+        s[p + "layer_norm1.bias"] = (H,)
+        s[p + "self_attn.in_proj_weight"] = (3 * H, H)
+        s[p + "self_attn.out_proj.weight"] = (H, H)
+        s[p + "layer_norm2.weight"] = (H,)
+        s[p + "layer_norm2.bias"] = (H,)
+        s[p + "ffn.ffn_1.weight"] = (4 * H, H, k)
+        s[p + "ffn.ffn_1.bias"] = (4 * H,)
+        s[p + "ffn.ffn_2.weight"] = (H, 4 * H)
+        s[p + "ffn.ffn_2.bias"] = (H,)
+    s["encoder.layer_norm.weight"] = (H,)
+    s["encoder.layer_norm.bias"] = (H,)
+    s["encoder.embed_tokens.weight"] = (vocab_size, H)
+    if use_dur_embed:
+        s["dur_embed.weight"] = (H, 1)
+        s["dur_embed.bias"] = (H,)
+    if use_spk_id:
+        s["spk_embed.weight"] = (num_spk, H)
+    if use_gender_id:
+        s["gender_embed.weight"] = (2, H)
+    if use_lang_id:
+        s["lang_embed.weight"] = (num_langs, H)
+    s["pitch_embed.weight"] = (H, 1)
+    s["pitch_embed.bias"] = (H,)
+    if use_voicing_embed:
+        s["voicing_embed.weight"] = (H, 1)
+        s["voicing_embed.bias"] = (H,)
+    if use_breath_embed:
+        s["breath_embed.weight"] = (H, 1)
+        s["breath_embed.bias"] = (H,)
+    return s
+
+
+def synth_cond_params(shapes, seed):
+    """synth_params + the padding rows Embedding(..., padding_idx=0) keeps at zero
+    (common_layers.py:63-68: initialised to 0 and never updated)."""
+    P = synth_params(shapes, seed)
+    for k in ("encoder.embed_tokens.weight", "lang_embed.weight"):
+        if k in P:
+            P[k][0] = 0.0
+    return P
+
+
+def synth_cond_inputs(seed, lengths, vocab_size, num_spk=1, num_langs=3, max_dur=12, pad_tokens=0):
+    """Ragged batch of phoneme sequences with durations: ``lengths[b]`` tokens (ids >= 1) then
+    zero padding to max(lengths) + pad_tokens; mel2ph repeats token i+1 dur[i] times, then
+    0-padding to the longest utterance (the binarizer's layout, tts_modules.py:135-171)."""
+    rng = np.random.default_rng([int(seed), 0xC0D])
+    B = len(lengths)
+    Tt = max(lengths) + pad_tokens
+    tok = np.zeros((B, Tt), np.int64)
+    lang = np.zeros((B, Tt), np.int64)
+    durs = []
+    for b, n in enumerate(lengths):
+        tok[b, :n] = rng.integers(1, vocab_size, n)
+        lang[b, :n] = rng.integers(1, max(num_langs, 2), n)
+        durs.append(rng.integers(1, max_dur + 1, n))
+    Tm = max(int(d.sum()) for d in durs)
+    mel2ph = np.zeros((B, Tm), np.int64)
+    for b, d in enumerate(durs):
+        mel2ph[b, :int(d.sum())] = np.repeat(np.arange(1, len(d) + 1), d)
+    f0 = rng.uniform(80.0, 800.0, (B, Tm)).astype(np.float32)
+    f0[rng.random((B, Tm)) < 0.15] = 0.0        # unvoiced frames
+    voicing = rng.uniform(-1.5, 1.0, (B, Tm)).astype(np.float32)
+    breath = rng.uniform(-1.5, 1.0, (B, Tm)).astype(np.float32)
+    spk = rng.integers(0, num_spk, B).astype(np.int64)
+    return dict(txt_tokens=tok, mel2ph=mel2ph, f0=f0, lang_seq=lang, spk_embed_id=spk,
+                voicing=voicing, breath=breath)

@@ -29,6 +29,7 @@ sys.path.insert(0, REF)
 from prodiff_amd import synth  # noqa: E402
 
 torch.Tensor.cuda = lambda self, *a, **k: self          # shim (util.py:68,214,424)
+sys.modules.setdefault("chardet", types.ModuleType("chardet"))   # utils/__init__.py:6
 torch.set_num_threads(8)
 
 from modules.decoder.wavenet import WaveNet            # noqa: E402
@@ -368,6 +369,75 @@ def gen_fullsize():
             out.update(fastdiff_seed=fs, draw_seed=ds, wav_stride=WAV_STRIDE, wav_sub=wav[:, ::WAV_STRIDE],
                        wav_l2=np.linalg.norm(w64, axis=1), wav_mean=w64.mean(1), wav_absmax=np.abs(w64).max(1))
         save(name, **out)
+
+
+# --------------------------------------------------------------------------
+# SVS teacher condition stage (modules/svs/prodiff_teacher.py:103-146)
+# --------------------------------------------------------------------------
+COND_CASES = {
+    # name: (hparam overrides, vocab, lengths, pad_tokens, param seed, input seed, spk mode)
+    "cond_small": (dict(num_spk=3, num_langs=3), 40, [17, 9, 23], 2, 41, 141, "id"),
+    # handler/config.yaml flags: single speaker, voicing/breath embeds off
+    "cond_handler": (dict(num_spk=1, num_langs=2, use_voicing_embed=False, use_breath_embed=False),
+                     64, [120], 0, 42, 142, "id"),
+    # 4 heads (head dim 64), 2 layers, time-varying speaker mix, gender ids (looked up in lang_embed)
+    "cond_mix_gender": (dict(num_spk=4, num_langs=4, num_heads=4, enc_layers=2, use_gender_id=True),
+                        50, [30, 11], 1, 43, 143, "mix_t"),
+    # 1 head (head dim 256), long utterances: many query / key blocks, T_mel ~ 2000
+    "cond_long": (dict(num_spk=2, num_langs=3, num_heads=1, enc_layers=2, use_breath_embed=False),
+                  80, [300, 257], 0, 44, 144, "mix_1"),
+}
+
+
+def cond_hparams(over):
+    hp = dict(synth.COND_DEFAULTS)
+    hp.update(over)
+    return hp
+
+
+def gen_cond():
+    from modules.svs.prodiff_teacher import ProDiffTeacher
+    for name, (over, V, lengths, padt, ps, xs, spk_mode) in COND_CASES.items():
+        hp = cond_hparams(over)
+        rhp = dict(hp, audio_num_mel_bins=128, dropout=0.1, languages=["l%d" % i for i in range(hp["num_langs"] - 1)],
+                   residual_layers=1, residual_channels=64, dilation_cycle_length=1, timesteps=4, timescale=1000,
+                   schedule_type="vpsde", max_beta=40.0, spec_min=[-12], spec_max=[0])
+        m = ProDiffTeacher(V, rhp).eval()
+        shapes = synth.cond_param_shapes(V, **hp)
+        P = synth.synth_cond_params(shapes, ps)
+        sd = m.state_dict()
+        assert [k for k in sd if not k.startswith("diffusion") and k in shapes] == list(shapes), "state-dict order"
+        for k, v in P.items():
+            assert tuple(sd[k].shape) == v.shape, (k, sd[k].shape, v.shape)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()}, strict=False)
+        x = synth.synth_cond_inputs(xs, lengths, V, hp["num_spk"], hp["num_langs"], pad_tokens=padt)
+        B, Tm = x["mel2ph"].shape
+        kw = dict(lang_seq=torch.from_numpy(x["lang_seq"]))
+        extra = {}
+        if spk_mode == "id":
+            kw["spk_embed_id"] = torch.from_numpy(x["spk_embed_id"])
+        else:
+            frames = Tm if spk_mode == "mix_t" else 1
+            mix = synth.synth_inputs(xs + 7, (B, frames, hp["hidden_size"]), scale=0.3)
+            kw["spk_mix_embed"] = torch.from_numpy(mix)
+            extra["spk_mix_embed"] = mix
+        if hp["use_gender_id"]:
+            gid = np.arange(B, dtype=np.int64) % 2
+            kw["gender_embed_id"] = torch.from_numpy(gid)
+            extra["gender_embed_id"] = gid
+        if hp["use_voicing_embed"]:
+            kw["voicing"] = torch.from_numpy(x["voicing"])
+        if hp["use_breath_embed"]:
+            kw["breath"] = torch.from_numpy(x["breath"])
+        enc_out = {}
+        hook = m.encoder.register_forward_hook(lambda mod, inp, out: enc_out.setdefault("enc", out.detach().clone()))
+        with torch.no_grad():
+            cond = m.forward_condition(torch.from_numpy(x["txt_tokens"]), torch.from_numpy(x["mel2ph"]),
+                                       torch.from_numpy(x["f0"]), **kw).numpy()
+        hook.remove()
+        save(name, vocab=V, lengths=np.array(lengths), pad_tokens=padt, param_seed=ps, input_seed=xs,
+             spk_mode=spk_mode, hp_keys=np.array(list(over)), hp_vals=np.array([int(v) for v in over.values()]),
+             cond=cond, enc=enc_out["enc"].numpy(), **{k: v for k, v in x.items()}, **extra)
 
 
 if __name__ == "__main__":

@@ -32,3 +32,26 @@ def prodiff_params(name):
 
 def prodiff_buffers(d):
     return {k[4:]: v for k, v in d.items() if k.startswith("buf_")}
+
+
+COND_INPUTS = ("lang_seq", "spk_embed_id", "spk_mix_embed", "gender_embed_id", "voicing", "breath")
+
+
+def cond_case(name):
+    """(hparams, params, inputs, golden) of a tests/golden/cond_*.npz fixture (gen_golden.gen_cond)."""
+    d = load(name)
+    over = {str(k): int(v) for k, v in zip(d["hp_keys"], d["hp_vals"])}
+    hp = dict(synth.COND_DEFAULTS)
+    hp.update(over)
+    P = synth.synth_cond_params(synth.cond_param_shapes(int(d["vocab"]), **hp), int(d["param_seed"]))
+    ins = {k: d[k] for k in ("txt_tokens", "mel2ph", "f0") + COND_INPUTS if k in d}
+    if str(d["spk_mode"]) != "id":
+        ins.pop("spk_embed_id")
+    if not hp["use_voicing_embed"]:
+        ins.pop("voicing", None)
+    if not hp["use_breath_embed"]:
+        ins.pop("breath", None)
+    return hp, P, ins, d
+
+
+COND_CASES = ("cond_small", "cond_handler", "cond_mix_gender", "cond_long")

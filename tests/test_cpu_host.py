@@ -110,3 +110,49 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dp, f)).read()
                 assert "oracle" not in re.sub(r"#.*", "", src).replace('"""', ""), f
+
+
+TEACHER_HP = dict(audio_num_mel_bins=128, hidden_size=256, enc_layers=4, enc_ffn_kernel_size=9, dropout=0.1,
+                  num_heads=2, num_spk=3, languages=["zh", "jp"], residual_layers=20, residual_channels=256,
+                  dilation_cycle_length=1, timesteps=4, timescale=1000, schedule_type="vpsde", max_beta=40.0,
+                  spec_min=[-12], spec_max=[0], use_voicing_embed=True, use_breath_embed=True)
+
+
+@pytest.mark.parametrize("gender", [False, True])
+def test_teacher_state_dict_matches_reference_names(gender):
+    """Key order/shapes of the condition stage == the reference teacher's (verified against
+    the reference module by tests/golden/gen_golden.py:gen_cond), diffusion under `diffusion.`."""
+    from prodiff_amd.teacher import ProDiffTeacher
+    hp = dict(TEACHER_HP, use_gender_id=gender)
+    t = ProDiffTeacher(40, hp)
+    sd = t.state_dict()
+    ref = synth.cond_param_shapes(40, num_langs=3, **{k: v for k, v in hp.items() if k != "num_langs"})
+    cond_keys = [k for k in sd if not k.startswith("diffusion.") and k != "encoder.embed_positions._float_tensor"]
+    assert cond_keys == list(ref)
+    assert all(tuple(sd[k].shape) == tuple(v) for k, v in ref.items())
+    assert "encoder.embed_positions._float_tensor" in sd
+    assert list(k[len("diffusion.denoise_fn."):] for k in sd if k.startswith("diffusion.denoise_fn.")) == \
+        list(synth.wavenet_param_shapes(128, 256, 20, 256))
+    dims = t.cond_dims()
+    assert _lib.lib().pd_cond_num_params(dims) == len(t.ordered_cond_params()) == len(ref)
+
+
+def test_teacher_needs_gpu_and_lang_seq():
+    from prodiff_amd.teacher import ProDiffTeacher
+    t = ProDiffTeacher(40, TEACHER_HP)
+    tok = torch.ones(1, 4, dtype=torch.long)
+    m2p = torch.tensor([[1, 2, 3, 4]])
+    with pytest.raises(AssertionError):
+        t.forward_condition(tok, m2p, torch.zeros(1, 4), spk_embed_id=torch.zeros(1, dtype=torch.long))
+    with pytest.raises(_lib.HipError):
+        t.forward_condition(tok, m2p, torch.zeros(1, 4), lang_seq=tok, spk_embed_id=torch.zeros(1, dtype=torch.long),
+                            voicing=torch.zeros(1, 4), breath=torch.zeros(1, 4))
+
+
+def test_cond_create_rejects_bad_dims():
+    lib = _lib.lib()
+    d = _lib.pd_cond_dims(40, 256, 4, 9, 3, 1, 3, 1, 1, 0, 1, 0, 0)   # 256 / 3 heads
+    h = _lib.C.c_void_p()
+    assert lib.pd_cond_create(_lib.C.byref(d), None, 0, None, _lib.C.byref(h)) != 0
+    d = _lib.pd_cond_dims(40, 256, 4, 9, 2, 1, 0, 1, 1, 1, 0, 0, 0)   # gender without lang_embed
+    assert lib.pd_cond_num_params(_lib.C.byref(d)) > 0

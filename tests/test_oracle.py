@@ -155,3 +155,19 @@ def test_torch_port_lvc_matches_numpy():
     ref = OF.lvc(x, k, b, 8)
     out = OT.lvc(_tt(x), _tt(k), _tt(b), 8).numpy()
     assert np.abs(out - ref).max() < 1e-4
+
+
+# ---------------------------------------------------------------- condition stage
+@pytest.mark.parametrize("name", G.COND_CASES)
+def test_cond_oracle(name):
+    """oracle_encoder.forward_condition vs the reference teacher's outputs (fp32 reference,
+    float64 oracle: the gap is the reference's own rounding)."""
+    from oracle import oracle_encoder as OE
+    hp, P, ins, d = G.cond_case(name)
+    cond, enc = OE.forward_condition(P, hp, return_encoder=True, **ins)
+    assert np.abs(enc - d["enc"]).max() <= 5e-5
+    assert np.abs(cond - d["cond"]).max() <= 5e-5
+    # length-regulator invariants: padding frames are exactly zero; dur sums to the frame count
+    assert np.all(cond[d["mel2ph"] == 0] == 0)
+    dur = OE.mel2ph_to_dur(d["mel2ph"], d["txt_tokens"].shape[1])
+    assert np.array_equal(dur.sum(1), (d["mel2ph"] > 0).sum(1))
