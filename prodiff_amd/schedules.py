@@ -86,10 +86,13 @@ def fastdiff_reverse_schedule(reverse_step=4, config_schedule=None):
     """fastdiff.py:54-73: a schedule from the config wins, else the table."""
     if config_schedule:
         return np.asarray(config_schedule, np.float32)
+    # fastdiff.py:60-63 builds these with torch.linspace in float32, whose values differ from
+    # a float64 linspace rounded to float32 in the last bit for some entries; use the same op
+    import torch
     if reverse_step == 1000:
-        return np.linspace(0.000001, 0.01, 1000).astype(np.float32)
+        return torch.linspace(0.000001, 0.01, 1000).numpy()
     if reverse_step == 200:
-        return np.linspace(0.0001, 0.02, 200).astype(np.float32)
+        return torch.linspace(0.0001, 0.02, 200).numpy()
     if reverse_step not in FASTDIFF_REVERSE_SCHEDULES:
         raise NotImplementedError(f"no FastDiff reverse schedule with {reverse_step} steps")
     return np.asarray(FASTDIFF_REVERSE_SCHEDULES[reverse_step], np.float32)

@@ -175,8 +175,10 @@ def gen_schedules():
     dh = fd_util.compute_hyperparams_given_schedule(beta)
     out["fd_train_alpha"] = dh["alpha"].numpy()
     out["fd_train_sigma"] = dh["sigma"].numpy()
-    for n, sched in FASTDIFF_SCHEDULES.items():
-        b = torch.FloatTensor(sched)
+    long_scheds = {1000: torch.linspace(0.000001, 0.01, 1000),   # fastdiff.py:60-63 (torch, float32)
+                   200: torch.linspace(0.0001, 0.02, 200)}
+    for n, sched in list(FASTDIFF_SCHEDULES.items()) + list(long_scheds.items()):
+        b = torch.FloatTensor(sched) if isinstance(sched, list) else sched.clone()
         a = 1 - b
         sg = b + 0
         for i in range(1, len(b)):

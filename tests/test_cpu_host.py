@@ -83,11 +83,16 @@ def test_fastdiff_schedules_match_reference():
     s = G.load("schedules")
     at = S.fastdiff_train_alpha()
     np.testing.assert_array_equal(at, s["fd_train_alpha"])
-    for n in (3, 4, 6, 8):
+    for n in (3, 4, 6, 8, 200, 1000):
         b, a, sg, st = S.fastdiff_infer_params(S.fastdiff_reverse_schedule(n), at)
+        np.testing.assert_array_equal(b, s[f"fd_n{n}_beta"])
         np.testing.assert_allclose(a, s[f"fd_n{n}_alpha"], rtol=1e-6)
         np.testing.assert_allclose(sg, s[f"fd_n{n}_sigma"], rtol=1e-6)
-        np.testing.assert_allclose(st, s[f"fd_n{n}_steps"], atol=1e-4)
+        # steps map alpha into the 1000-entry training table by (alpha[t]-a)/(alpha[t]-alpha[t+1]),
+        # which amplifies a 1-ulp alpha difference ~100x; the fixture ran torch's CPU sqrt, which
+        # is not correctly rounded on 4 of the 1000-step entries (IEEE sqrt here and on the GPU,
+        # where the reference keeps these tensors: fastdiff.py:60-63 `.cuda()`)
+        np.testing.assert_allclose(st, s[f"fd_n{n}_steps"], atol=1e-4 if n < 200 else 2e-4)
 
 
 def test_vocoder_registry():
