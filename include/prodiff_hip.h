@@ -333,7 +333,8 @@ typedef struct {
 
 /* cond [B,T_mel,H] time-major (what pd_prodiff_sample / pd_reflow_sample take), and optionally
  * enc_out [B,T_txt,H] = the FastspeechEncoder output (tts_modules.py:310-317); either may be
- * NULL (not both).  Every utterance needs at least one non-padding token. */
+ * NULL (not both); with cond NULL, mel2ph / T_mel still feed the duration embedding.  Every
+ * utterance needs at least one non-padding token. */
 int pd_cond_forward(const pd_cond* h, const pd_cond_inputs* in, float* cond, float* enc_out, int B,
                     int T_txt, int T_mel, void* workspace, size_t ws_bytes, void* stream);
 

@@ -17,6 +17,7 @@
 //                -> FFN linear GEMM (+ residual)
 //   enc_ln (final LayerNorm * mask) -> enc_cond (length-regulator gather + variance sums)
 // The GEMMs are the implicit-GEMM Conv1d engine (gemm.h) -- MFMA fp32 or bf16.
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -319,11 +320,24 @@ __global__ __launch_bounds__(256) void enc_cond_kernel(const CondArgs a) {
   }
 }
 
-// GEMM tile by grid size: 128 x 64 tiles once they give every CU a block, else 32 x 128.
+// GEMM tile by grid size: 128 x 64 tiles once they give every CU a block, else 32 x 128 tiles
+// with the K axis split over up to 8 blocks (the B = 1 encoder has a few hundred rows: its
+// 32-deep K steps run back to back on ~30 blocks otherwise, latency-bound).
+bool enc_big_tile(long long rows, int N) { return (long long)cdiv(rows, 128) * cdiv(N, 64) >= 256; }
+int enc_ksplit(long long rows, int N, int K) {
+  if (enc_big_tile(rows, N)) return 1;
+  const long long gxy = (long long)cdiv(rows, 32) * cdiv(N, 128);
+  int ks = (int)std::min<long long>(8, (256 + gxy - 1) / gxy);
+  ks = std::min(ks, std::max(1, K / GEMM_BK / 4));   // >= 4 K steps per block
+  return std::max(ks, 1);
+}
+
 template <int EPI, int ID>
-int enc_gemm(const GemmArgs& a, hipStream_t st, const char* tag) {
+int enc_gemm(GemmArgs a, float* part, hipStream_t st, const char* tag) {
   const long long rows = (long long)a.B * a.T;
-  if ((long long)cdiv(rows, 128) * cdiv(a.N, 64) >= 256) return launch_gemm<1, 2, 4, 1, EPI, ID>(a, st, tag);
+  if (enc_big_tile(rows, a.N)) return launch_gemm<1, 2, 4, 1, EPI, ID>(a, st, tag);
+  a.ksplit = enc_ksplit(rows, a.N, a.ldw);
+  a.part = part;
   return launch_gemm<1, 1, 1, 4, EPI, ID>(a, st, tag);
 }
 
@@ -343,7 +357,7 @@ struct pd_cond {
 
 namespace {
 struct CondWs {
-  size_t x, h, qkv, att, f, enc, total;
+  size_t x, h, qkv, att, f, enc, part, total;
 };
 CondWs cond_ws(const pd_cond* h, int B, int Tt) {
   const size_t R = (size_t)B * Tt;
@@ -356,6 +370,15 @@ CondWs cond_ws(const pd_cond* h, int B, int Tt) {
   w.att = o; o += al(R * h->H);
   w.f = o; o += al(R * h->F);
   w.enc = o; o += al(R * h->H);
+  // split-K partial sums: the largest ksplit * rows * N over the four GEMMs
+  const int H = h->H, F = h->F;
+  size_t part = 0;
+  const int NK[4][2] = {{3 * H, H}, {H, H}, {F, h->K * H}, {H, F}};
+  for (auto& nk : NK) {
+    const int ks = enc_ksplit((long long)R, nk[0], nk[1]);
+    if (ks > 1) part = std::max(part, (size_t)ks * R * nk[0]);
+  }
+  w.part = o; o += al(part);
   w.total = o * sizeof(float);
   return w;
 }
@@ -517,6 +540,7 @@ int pd_cond_forward(const pd_cond* h, const pd_cond_inputs* in, float* cond, flo
   float* att = ws + w.att;
   float* ff = ws + w.f;
   float* enc = enc_out ? enc_out : ws + w.enc;
+  float* part = ws + w.part;
   const float neg_freq = (float)(-(std::log(10000.0) / (H / 2 - 1)));
   {
     ProfScope ps("enc_embed", st);
@@ -537,7 +561,7 @@ int pd_cond_forward(const pd_cond* h, const pd_cond_inputs* in, float* cond, flo
     {
       GemmArgs a = make_gemm(B, T_txt, 3 * H, h->Wqkv[l], H, nullptr, qkv, bs * 3 * H, 3 * H);
       add_seg(a, make_seg(hn, bs * H, H, H, 0));
-      PD_TRY((enc_gemm<EPI_STORE, U_ENC_QKV>(a, st, "enc_qkv")));
+      PD_TRY((enc_gemm<EPI_STORE, U_ENC_QKV>(a, part, st, "enc_qkv")));
     }
     {
       ProfScope ps("enc_attn", st);
@@ -554,7 +578,7 @@ int pd_cond_forward(const pd_cond* h, const pd_cond_inputs* in, float* cond, flo
       GemmArgs a = make_gemm(B, T_txt, H, h->Wo[l], H, nullptr, x, bs * H, H);
       add_seg(a, make_seg(att, bs * H, H, H, 0));
       a.res = x; a.res_bs = bs * H; a.res_ld = H;
-      PD_TRY((enc_gemm<EPI_STORE, U_ENC_OUT>(a, st, "enc_outproj")));
+      PD_TRY((enc_gemm<EPI_STORE, U_ENC_OUT>(a, part, st, "enc_outproj")));
     }
     {
       ProfScope ps("enc_ln", st);
@@ -567,13 +591,13 @@ int pd_cond_forward(const pd_cond* h, const pd_cond_inputs* in, float* cond, flo
       for (int tap = 0; tap < K; ++tap) add_seg(a, make_seg(hn, bs * H, H, H, tap - K / 2));
       a.act = ACT_GELU;
       a.alpha = (float)std::pow((double)K, -0.5);
-      PD_TRY((enc_gemm<EPI_STORE, U_ENC_FFN1>(a, st, "enc_ffn1")));
+      PD_TRY((enc_gemm<EPI_STORE, U_ENC_FFN1>(a, part, st, "enc_ffn1")));
     }
     {   // x = x + (f W2^T + b2)   (ffn_2, residual, :667-672)
       GemmArgs a = make_gemm(B, T_txt, H, h->W2[l], F, h->b2[l], x, bs * H, H);
       add_seg(a, make_seg(ff, bs * F, F, F, 0));
       a.res = x; a.res_bs = bs * H; a.res_ld = H;
-      PD_TRY((enc_gemm<EPI_STORE, U_ENC_FFN2>(a, st, "enc_ffn2")));
+      PD_TRY((enc_gemm<EPI_STORE, U_ENC_FFN2>(a, part, st, "enc_ffn2")));
     }
   }
   {

@@ -76,6 +76,8 @@ struct GemmArgs {
   int noise_ld;
   unsigned long long seed;
   unsigned int stream_id;
+  int ksplit;               // STORE, > 1: split-K -- blockIdx.z sums one K range into `part`,
+  float* part;              //   [ksplit][B*T][N] fp32, and gemm_splitk_reduce applies the epilogue
 };
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -196,13 +198,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nchunks = a.ldw / BK;
-  int s = 0, c0 = 0;
-  load_chunk(0, 0, 0);
-  store_chunk(0);
+  int ch_begin = 0, nchunks = a.ldw / BK;
+  if (EPI == EPI_STORE && a.ksplit > 1) {   // this block's K range (host makes every range non-empty)
+    const int cps = (nchunks + a.ksplit - 1) / a.ksplit;
+    ch_begin = blockIdx.z * cps;
+    nchunks = min(nchunks, ch_begin + cps);
+  }
+  int s = 0, c0 = ch_begin * BK;
+  while (c0 >= a.seg[s].kpad) { c0 -= a.seg[s].kpad; ++s; }
+  load_chunk(s, c0, ch_begin * BK);
+  store_chunk(ch_begin & 1);
   __syncthreads();
   const int r32 = lane & 31, h = lane >> 5;
-  for (int ch = 0; ch < nchunks; ++ch) {
+  for (int ch = ch_begin; ch < nchunks; ++ch) {
     const bool more = ch + 1 < nchunks;
     if (more) {
       c0 += BK;
@@ -291,6 +299,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
         for (int j = 0; j < WN_T; ++j) {
           const int n = nb + wn * 32 * WN_T + j * 32 + r32;
           if (n >= a.N) continue;
+          if (EPI == EPI_STORE && a.ksplit > 1) {
+            a.part[((long long)blockIdx.z * rows + R) * a.N + n] = acc[i][j][reg];
+            continue;
+          }
           float v = acc[i][j][reg] + (a.bias ? a.bias[n] : 0.f);
           const long long oi = (long long)b * a.out_bs + (long long)t * a.out_ld + n;
           if constexpr (EPI == EPI_POSTERIOR) {
@@ -317,6 +329,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
 // Host-side validation + launch.  Returns PD_OK or an error code.
 int validate_gemm(const GemmArgs& a);
 
+// Split-K epilogue: out = act(sum_z part[z] + bias) * scale (+ res), as EPI_STORE's.
+int gemm_splitk_reduce(const GemmArgs& a, hipStream_t st);
+
 const __bf16* lookup_bf16(const float* p);
 
 template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int EPI, int ID>
@@ -334,14 +349,25 @@ int launch_gemm(const GemmArgs& a0, hipStream_t st, const char* tag) {
     set_error("paired gemm needs N == 2*half, half % 32 == 0");
     return PD_ERR_ARG;
   }
+  if (a.ksplit > 1) {
+    const int nch = a.ldw / GEMM_BK;
+    if (EPI != EPI_STORE || !a.part || a.ksplit > nch) {
+      set_error("split-K needs EPI_STORE, a partial-sum buffer and ksplit <= K / 32");
+      return PD_ERR_ARG;
+    }
+    const int cps = cdiv(nch, a.ksplit);
+    a.ksplit = cdiv(nch, cps);          // every K range non-empty
+    grid.z = a.ksplit;
+  }
   {
     ProfScope ps(tag, st);
     if (a.Wb)
       hipLaunchKernelGGL((gemm_kernel<__bf16, WM_T, WN_T, WAVES_M, WAVES_N, EPI, ID>), grid, dim3(256), 0, st, a);
     else
       hipLaunchKernelGGL((gemm_kernel<float, WM_T, WN_T, WAVES_M, WAVES_N, EPI, ID>), grid, dim3(256), 0, st, a);
+    PD_LAUNCH_CHECK();
+    if (a.ksplit > 1) PD_TRY(gemm_splitk_reduce(a, st));
   }
-  PD_LAUNCH_CHECK();
   return PD_OK;
 }
 

@@ -41,6 +41,31 @@ int validate_gemm(const GemmArgs& a) {
   return PD_OK;
 }
 
+// ---------------------------------------------------------------- split-K reduce
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs a) {
+  const long long rows = (long long)a.B * a.T;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * a.N) return;
+  const long long R = i / a.N;
+  const int n = (int)(i - R * a.N);
+  float v = 0.f;
+  for (int z = 0; z < a.ksplit; ++z) v += a.part[(z * rows + R) * a.N + n];
+  v += a.bias ? a.bias[n] : 0.f;
+  v = act_apply(v, a.act, a.alpha) * a.scale;
+  const long long b = R / a.T, t = R - b * a.T;
+  if (a.res) v += a.res[b * a.res_bs + t * a.res_ld + n];
+  const long long oi = b * a.out_bs + t * a.out_ld + n;
+  if (a.out_bf16) reinterpret_cast<__bf16*>(a.out)[oi] = (__bf16)v;
+  else a.out[oi] = v;
+}
+
+int gemm_splitk_reduce(const GemmArgs& a, hipStream_t st) {
+  const long long n = (long long)a.B * a.T * a.N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, a);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
 // ---------------------------------------------------------------- matvec
 // out[v][n] = act(W[n] . in[v] + bias[n]).  One wave per output n and MV_NV vectors at
 // once (grid.y covers the vector groups), so each W row is read once per group and

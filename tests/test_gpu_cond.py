@@ -69,19 +69,20 @@ def test_cond_deterministic_and_encoder_only():
     L = _lib.lib()
     h = t.cond_handle()
     B, Tt = args[0].shape
+    Tm = args[1].shape[1]   # mel2ph still feeds the duration embedding
     enc = torch.empty(B, Tt, hp["hidden_size"], device="cuda")
     vp = lambda v: None if v is None else v.data_ptr()
     ins_c = _lib.pd_cond_inputs(vp(args[0]), vp(args[1]), None, vp(x["lang_seq"]), None, None, 0, None, None, 0,
                                 None, None)
-    nb = L.pd_cond_workspace_size(h, B, Tt, 0)
+    nb = L.pd_cond_workspace_size(h, B, Tt, Tm)
     ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
-    _lib.check(L.pd_cond_forward(h, _lib.C.byref(ins_c), None, _lib.fptr(enc), B, Tt, 0, _lib.C.c_void_p(ws.data_ptr()),
+    _lib.check(L.pd_cond_forward(h, _lib.C.byref(ins_c), None, _lib.fptr(enc), B, Tt, Tm, _lib.C.c_void_p(ws.data_ptr()),
                                  nb, _lib.stream_ptr()))
     torch.cuda.synchronize()
     assert torch.equal(enc, e1)
     # missing required inputs fail loudly, before any launch
     ins_c.lang_seq = None
-    assert L.pd_cond_forward(h, _lib.C.byref(ins_c), None, _lib.fptr(enc), B, Tt, 0, _lib.C.c_void_p(ws.data_ptr()),
+    assert L.pd_cond_forward(h, _lib.C.byref(ins_c), None, _lib.fptr(enc), B, Tt, Tm, _lib.C.c_void_p(ws.data_ptr()),
                              nb, _lib.stream_ptr()) == 1
     assert b"lang_seq" in L.pd_last_error()
 
