@@ -10,6 +10,8 @@ wav [B,220416] (10 s at 22.05 kHz, hop 256).  Configurations (BASELINE.json):
   C4   (default at N>1)  32 utterances per GPU (256 at N=8), bf16     weak scaling
   C4S                    256 utterances over all N GPUs, bf16         strong scaling
   C2                     ProDiff 2-iter only, B=1, T=1000, fp32, mel-only (hipGraph replay)
+  C5                     SVS path: teacher condition (FFT encoder) + ProDiff 4-iter (M=128) +
+                         NSF-HiFiGAN (44.1 kHz, hop 512), 8 segments per GPU (64 at N=8), bf16
 
 For N>1 every rank runs its LPT shard (pipeline.distributed_synthesize: no
 data-path collective) and the step ends with the ragged point-to-point gather of
@@ -58,6 +60,10 @@ CONFIGS = {
                      "FastDiff 4-iter, LPT shards + RCCL gather"),
     "C2": dict(batch=1, strong=False, frames=1000, dtype="fp32", vocoder=False, timesteps=2,
                desc="C2: ProDiff 2-iter mel denoiser (WaveNet 20x256, M=80), B={b}, T={t}, fp32, mel only"),
+    "C5": dict(batch=8, strong=False, frames=861, dtype="bf16", vocoder=True, timesteps=4, svs=True, tokens=120,
+               desc="C5: SVS path (modules/svs) -- ProDiffTeacher condition (FFT encoder, {n} phonemes, speaker mix, "
+                    "zh/jp lang ids, voicing/breath) + ProDiff 4-iter (WaveNet 20x256, M=128) + NSF-HiFiGAN "
+                    "(44.1 kHz, hop 512), {b} x {t}-frame segments per GPU (64 at N=8)"),
 }
 
 
@@ -181,6 +187,57 @@ def pmc_traffic(tag, path=None):
     return None, None
 
 
+def nsf_stage_dims(h=None):
+    """(samples per mel frame, channels) after each NSF-HiFiGAN upsample (handler/base_config.yaml)."""
+    rates, ch0 = (8, 8, 2, 2, 2), 512
+    out, r = [], 1
+    for i, u in enumerate(rates):
+        r *= u
+        out.append((r, ch0 // 2 ** (i + 1)))
+    return out
+
+
+def svs_flops_per_launch(B, T, Tt, small_max=16, H=256, k_ffn=9):
+    """Condition-encoder and NSF-HiFiGAN launch FLOPs (per launch; nsf_res = mean over its launches)."""
+    rows = B * Tt
+    F = B * T
+    res = [(2 * F * r * 6 * c * c * (3 + 7 + 11), c) for r, c in nsf_stage_dims()]   # 6 convs x 3 kernels / stage
+    big = [f for f, c in res if c > small_max]
+    small = [f for f, c in res if c <= small_max]
+    return {"enc_qkv": 2 * rows * H * 3 * H, "enc_outproj": 2 * rows * H * H, "enc_ffn1": 2 * rows * H * 4 * H * k_ffn,
+            "enc_ffn2": 2 * rows * 4 * H * H, "enc_attn": 2 * 2 * B * Tt * Tt * H,
+            "nsf_res": sum(big) / (18 * len(big)) if big else 0.0,
+            "nsf_res_small": sum(small) / (18 * len(small)) if small else 0.0}
+
+
+def svs_bytes_per_launch(B, T, Tt, dtype, small_max=16, H=256):
+    wb = 2 if dtype == "bf16" else 4
+    F = B * T
+    rows = B * Tt
+    res = [(F * r * c * 4 * 2.5 * 18 + 6 * c * c * 21 * wb, c) for r, c in nsf_stage_dims()]   # in, out, 1/2 res
+    big = [b for b, c in res if c > small_max]
+    small = [b for b, c in res if c <= small_max]
+    return {"enc_qkv": rows * 4 * H * 4 + 3 * H * H * wb, "enc_outproj": rows * 3 * H * 4 + H * H * wb,
+            "enc_ffn1": rows * 5 * H * 4 + 4 * H * H * 9 * wb, "enc_ffn2": rows * 6 * H * 4 + 4 * H * H * wb,
+            "enc_attn": rows * 4 * H * 4,
+            "nsf_res": sum(big) / (18 * len(big)) if big else 0.0,
+            "nsf_res_small": sum(small) / (18 * len(small)) if small else 0.0}
+
+
+def svs_step_flops(B, T, Tt):
+    f = svs_flops_per_launch(B, T, Tt, small_max=0)
+    enc = 4 * (f["enc_qkv"] + f["enc_outproj"] + f["enc_ffn1"] + f["enc_ffn2"] + f["enc_attn"])
+    nsf = 18 * 5 * f["nsf_res"]
+    ups = 0
+    F = B * T
+    r_in, c_in = 1, 512
+    for (r, c), k in zip(nsf_stage_dims(), (16, 16, 4, 4, 4)):
+        ups += 2 * F * r_in * c_in * c * k
+        r_in, c_in = r, c
+    pre_post = 2 * F * 512 * 128 * 7 + 2 * F * 512 * 16 * 7
+    return enc + 4 * prodiff_step_flops(B, T, M=128) + nsf + ups + pre_post
+
+
 def prodiff_step_flops(B, T, M=80, C=256, H=256):
     """One denoiser call: 26.43 MFLOP per frame at M=80."""
     f = flops_per_launch(B, T, M=M, C=C, H=H)
@@ -203,7 +260,7 @@ def ref_cpu_baseline(config):
         return None
     with open(path) as f:
         d = json.load(f)
-    key = "C2" if config == "C2" else "C3"
+    key = config if config in ("C2", "C5") else "C3"
     e = d.get("configs", {}).get(key)
     if not e:
         return None
@@ -293,6 +350,8 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     cfg_name = args.config if args.config != "auto" else ("C3" if world == 1 else "C4")
     cfg = CONFIGS[cfg_name]
+    svs = cfg.get("svs", False)
+    hop, sample_rate = (512, 44100) if svs else (HOP, SAMPLE_RATE)
     dtype = args.dtype or cfg["dtype"]
     nb = args.batch or cfg["batch"]
     T = args.frames or cfg["frames"]
@@ -318,12 +377,28 @@ def main():
     B = len(mine)                                           # utterances this rank runs per step
     rng = np.random.default_rng(1000 + rank)
     conds = [(T, None)] * n_total
+    from prodiff_amd import synth as _synth
     for i in mine:
-        conds[i] = torch.from_numpy(rng.standard_normal((T, 256), dtype=np.float32)).to(dev)
+        if svs:      # one SVS segment: phonemes + durations summing to T frames, f0, voicing, breath
+            from prodiff_amd.pipeline import SVS_VOCAB
+            u = {k: torch.from_numpy(v).to(dev) for k, v in
+                 _synth.synth_svs_utterance(100 + i, T, cfg["tokens"], SVS_VOCAB).items()}
+            conds[i] = (T, (lambda u=u: u))
+        else:
+            conds[i] = torch.from_numpy(rng.standard_normal((T, 256), dtype=np.float32)).to(dev)
 
     _lib = None
     if dry:
         synth_fn = stub_synth
+        if svs:
+            raise SystemExit("--dry-run covers the C3/C4 launcher; C5 needs the GPU")
+    elif svs:
+        from prodiff_amd import _lib
+        from prodiff_amd.pipeline import SvsSynthesizer
+        syn = SvsSynthesizer.synthetic(dev, seed=0, dtype=dtype)
+        if args.wn_opt:
+            syn.diffusion.denoise_fn.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.wn_opt)})
+        synth_fn = syn
     else:
         from prodiff_amd import _lib
         from prodiff_amd.pipeline import Synthesizer
@@ -336,7 +411,7 @@ def main():
 
     if cfg["vocoder"]:
         def step(i):
-            return distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev)
+            return distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop)
     else:
         # C2: the ProDiff sampler alone on one utterance (B=1), mel only
         gd = syn.diffusion
@@ -350,8 +425,14 @@ def main():
                 return graph.replay()
             return gd.sample(cond_b, seed=10_000 * i)
 
-    fl = flops_per_launch(B, T, dtype)
-    by = bytes_per_launch(B, T, dtype)
+    if svs:
+        fl = flops_per_launch(B, T, dtype, M=128)
+        by = bytes_per_launch(B, T, dtype, M=128)
+        fl.update(svs_flops_per_launch(B, T, cfg["tokens"]))
+        by.update(svs_bytes_per_launch(B, T, cfg["tokens"], dtype))
+    else:
+        fl = flops_per_launch(B, T, dtype)
+        by = bytes_per_launch(B, T, dtype)
     for i in range(args.warmup):
         step(i)
     if not dry:
@@ -405,7 +486,7 @@ def main():
             assert torch.isfinite(out).all()
 
     frames = n_total * T * args.steps
-    audio_s = frames * HOP / SAMPLE_RATE
+    audio_s = frames * hop / sample_rate
     ms_step = dt / args.steps * 1e3
     peak_tf = BF16_PEAK_TFLOPS if dtype == "bf16" else FP32_PEAK_TFLOPS
     ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)          # FLOP/B where MFMA and HBM bounds meet
@@ -434,7 +515,10 @@ def main():
                          "avg_launch_us": round(ms / cnt * 1e3, 2), "launches": cnt,
                          "share_of_step": round(ms / (dt * 1e3), 3),
                          "timing": "HIP events around this kernel only, over the timed steps"})
-    step_fl = 2 * prodiff_step_flops(n_total, T) + (4 * fastdiff_step_flops(n_total, T) if cfg["vocoder"] else 0)
+    if svs:
+        step_fl = svs_step_flops(n_total, T, cfg["tokens"])
+    else:
+        step_fl = 2 * prodiff_step_flops(n_total, T) + (4 * fastdiff_step_flops(n_total, T) if cfg["vocoder"] else 0)
     out_line = {
         "metric": METRIC,
         "value": round(frames / dt, 1),
@@ -447,8 +531,11 @@ def main():
         "scaling": "strong" if cfg["strong"] else "weak",
         "vs_baseline": None,
         "dtype": dtype,
-        "data": "synthetic (cond ~ N(0,1)); random-init weights of the reference architectures; on-device Philox draws",
-        "config": {"workload": cfg["desc"].format(b=nb, t=T), "name": cfg_name, "global_batch": n_total,
+        "data": ("synthetic SVS segments (phonemes, durations summing to T, f0 with unvoiced gaps, voicing/breath, "
+                 "speaker mix)" if svs else "synthetic (cond ~ N(0,1))") +
+                "; random-init weights of the reference architectures; on-device Philox draws",
+        "config": {"workload": cfg["desc"].format(b=nb, t=T, n=cfg.get("tokens")), "name": cfg_name,
+                   "global_batch": n_total,
                    "per_gpu_batch": B, "seq_len": T,
                    "parallelism": f"dp{world} (utterance shards, RCCL gather to rank 0)" if cfg["vocoder"]
                    else "single GPU" + ("" if args.no_graph else ", hipGraph replay")},
@@ -464,7 +551,7 @@ def main():
     }
     if rank == 0 and world == 1 and not dry:
         out_line["cpu_baseline"] = ref_cpu_baseline(cfg_name)
-        if args.cpu_frames > 0:
+        if args.cpu_frames > 0 and not svs:
             out_line["cpu_baseline_port"] = port_cpu_baseline(args.cpu_frames if cfg["vocoder"] else T,
                                                               vocoder=cfg["vocoder"])
     if rank == 0:

@@ -35,6 +35,7 @@ struct NsfConv {
   // ResBlock convs with at most this many channels use nsf_conv_small_kernel (NSF_OPT_SMALL_MAX;
   // measured: 32 channels run faster on the bf16 GEMM)
   int small_max = 16;
+  bool wconv = true;          // NSF_OPT_WCONV: bf16 ResBlock convs on nsf_wconv_kernel
 };
 
 struct NsfUps {
@@ -253,6 +254,159 @@ int launch_conv_small(const NsfConv& c, const float* in, float alpha, float scal
                      c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out);
   PD_LAUNCH_CHECK();
   return PD_OK;
+}
+
+// ---------------------------------------------------------------- windowed MFMA conv (bf16)
+// ResBlock conv y[t] = b + sum_tap W_tap . lrelu(x[t + tap*d - pad]) (+ res) on the bf16 MFMA
+// path.  The implicit-GEMM engine streams one K segment per tap, so each tap re-reads the
+// activations from L2/HBM and every 32-deep K chunk waits on a global load.  Here a block
+// stages its input window ONCE -- TM rows plus the (k-1)*d halo, all C channels,
+// leaky-ReLU'd, scaled and rounded to bf16 -- into LDS; every tap's A fragments are
+// row-shifted reads of that window.  Weights (the pool's bf16 copy, packed
+// [cout][tap*kpad + ci]) stream from L2 into registers one 16-deep k-step ahead.
+// Block = 256 threads = WM x WN waves, wave tile (32 FM rows) x (32 FN channels):
+// TM = 32 FM WM = 128 rows, TN = 32 FN WN output channels (grid.y covers C / TN),
+// grid.z = utterance.  LDS row stride C + 8 bf16: lanes r and r+1 of a b128 fragment read
+// sit 4 banks apart for every C used here, so a wave's fragment read is conflict-free.
+template <int C, int FM, int FN, int WM, int WN, bool IN_BF, bool OUT_BF>
+__global__ __launch_bounds__(256) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
+                                                        int ldw, int kpad, const float* __restrict__ bias, int taps,
+                                                        int dil, float alpha, float scale, int Tl,
+                                                        const float* __restrict__ res, void* __restrict__ out) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN, LDA = C + 8, C8 = C / 8, KS = C / 16;
+  static_assert(C % TN == 0, "channel tiling");
+  extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int b = blockIdx.z, t0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
+  const int pad = (taps - 1) * dil / 2;
+  const int W = TM + (taps - 1) * dil;
+  // 1. the input window, 8 channels (16 B of bf16) per item
+  for (int i = tid; i < W * C8; i += 256) {
+    const int row = i / C8, c8 = i - row * C8;
+    const int t = t0 - pad + row;
+    bf16x8 v;
+    if (t >= 0 && t < Tl) {
+      float f[8];
+      const long long e = ((long long)b * Tl + t) * C + 8 * c8;
+      if constexpr (IN_BF) {
+        const bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(in) + e);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (float)x[j];
+      } else {
+        const float4 x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e);
+        const float4 x1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e + 4);
+        f[0] = x0.x; f[1] = x0.y; f[2] = x0.z; f[3] = x0.w; f[4] = x1.x; f[5] = x1.y; f[6] = x1.z; f[7] = x1.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[j] >= 0.f ? f[j] : alpha * f[j]) * scale);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(nsf_win + row * LDA + 8 * c8) = v;
+  }
+  __syncthreads();
+  // 2. taps x 16-deep k-steps; B fragments prefetched one step ahead
+  const int r32 = lane & 31, h = lane >> 5;
+  const __bf16* wr[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) wr[j] = w + (long long)(n0 + (wn * FN + j) * 32 + r32) * ldw + 8 * h;
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int S = taps * KS;
+  bf16x8 bcur[FN], bnext[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bcur[j] = *reinterpret_cast<const bf16x8*>(wr[j]);
+  const __bf16* arow = nsf_win + (wm * FM * 32 + r32) * LDA + 8 * h;
+  for (int s = 0; s < S; ++s) {
+    const int tap = s / KS, kc = s - tap * KS;
+    if (s + 1 < S) {
+      const int tn = (s + 1) / KS, kn = s + 1 - tn * KS;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bnext[j] = *reinterpret_cast<const bf16x8*>(wr[j] + tn * kpad + 16 * kn);
+    }
+    bf16x8 af[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 32 + tap * dil) * LDA + 16 * kc);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bcur[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bcur[j] = bnext[j];
+  }
+  // 3. epilogue: + bias (+ res), C/D map col = lane&31, row = (reg&3) + 8(reg>>2) + 4(lane>>5)
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int t = t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (t >= Tl) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + (wn * FN + j) * 32 + r32;
+        const long long o = ((long long)b * Tl + t) * C + n;
+        float v = acc[i][j][reg] + bias[n];
+        if (res) v += res[o];
+        if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
+        else reinterpret_cast<float*>(out)[o] = v;
+      }
+    }
+  }
+}
+
+template <int C, int FM, int FN, int WM, int WN>
+int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
+                   int Tl, void* out, bool out_bf, const float* res, hipStream_t st) {
+  constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN;
+  const size_t lds = (size_t)(TM + (c.taps - 1) * c.dil) * (C + 8) * sizeof(__bf16);
+  if (lds > 160 * 1024) { set_error("nsf conv: LDS window too large"); return PD_ERR_UNSUPPORTED; }
+  dim3 grid(cdiv(Tl, TM), C / TN, B);
+  const int ldw = c.taps * c.kpad;
+#define PD_WCONV(IB, OB)                                                                                          \
+  do {                                                                                                            \
+    static const hipError_t attr = hipFuncSetAttribute(                                                           \
+        reinterpret_cast<const void*>(&nsf_wconv_kernel<C, FM, FN, WM, WN, IB, OB>),                              \
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                                                  \
+    if (attr != hipSuccess) { set_error("nsf conv: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }    \
+    hipLaunchKernelGGL((nsf_wconv_kernel<C, FM, FN, WM, WN, IB, OB>), grid, dim3(256), lds, st, in, wb, ldw,      \
+                       c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out);                                   \
+  } while (0)
+  ProfScope ps("nsf_res", st);
+  if (in_bf && out_bf) PD_WCONV(true, true);
+  else if (in_bf) PD_WCONV(true, false);
+  else if (out_bf) PD_WCONV(false, true);
+  else PD_WCONV(false, false);
+#undef PD_WCONV
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// The windowed conv for this ResBlock conv, if it has one (bf16 weights, C in {32..256}).
+bool wconv_ok(const NsfConv& c) {
+  return c.wconv && c.cin == c.cout && c.cout > c.small_max && c.taps <= 11 && lookup_bf16(c.w) != nullptr &&
+         (c.cout == 32 || c.cout == 64 || c.cout == 128 || c.cout == 256);
+}
+
+int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, float scale, int B, int Tl, void* out,
+                 bool out_bf, const float* res, hipStream_t st) {
+  const __bf16* wb = lookup_bf16(c.w);
+  switch (c.cout) {
+    case 256: return launch_wconv_c<256, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st);
+    case 128: return launch_wconv_c<128, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st);
+    case 64: return launch_wconv_c<64, 2, 1, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st);
+    case 32: return launch_wconv_c<32, 1, 1, 4, 1>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st);
+    default: set_error("nsf wconv: unsupported channel count"); return PD_ERR_UNSUPPORTED;
+  }
 }
 
 // ConvTranspose1d weight [Cin][Cout][K] -> phase phi: dst[co][m*cpad + ci] = W[ci][co][phi + m*u]
@@ -530,6 +684,11 @@ int nsf_set_option(nsf_model* m, int option, int value) {
     for (auto& c : m->res) c.small_max = value;
     return PD_OK;
   }
+  if (option == NSF_OPT_WCONV) {
+    PD_CHECK_ARG(value == 0 || value == 1, "NSF_OPT_WCONV is 0 or 1");
+    for (auto& c : m->res) c.wconv = value != 0;
+    return PD_OK;
+  }
   set_error("nsf_set_option: unknown option " + std::to_string(option));
   return PD_ERR_ARG;
 }
@@ -619,13 +778,22 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
         if (d.resblock == 1) {
           const NsfConv& c1 = m->res[r + q];
           const NsfConv& c2 = m->res[r + d.num_dilations + q];
-          PD_TRY(nsf_conv(c1, cur, NSF_LRELU, 1.f, B, Lc, T1, nullptr, ACT_NONE, st, U_NSF_RES));
-          PD_TRY(nsf_conv(c2, T1, NSF_LRELU, 1.f, B, Lc, target, cur, ACT_NONE, st, U_NSF_RES));
+          if (wconv_ok(c1) && wconv_ok(c2)) {
+            // windowed bf16 convs; the inner activation xt = c1(lrelu(x)) travels as bf16
+            PD_TRY(launch_wconv(c1, cur, false, NSF_LRELU, 1.f, B, Lc, T1, true, nullptr, st));
+            PD_TRY(launch_wconv(c2, T1, true, NSF_LRELU, 1.f, B, Lc, target, false, cur, st));
+          } else {
+            PD_TRY(nsf_conv(c1, cur, NSF_LRELU, 1.f, B, Lc, T1, nullptr, ACT_NONE, st, U_NSF_RES));
+            PD_TRY(nsf_conv(c2, T1, NSF_LRELU, 1.f, B, Lc, target, cur, ACT_NONE, st, U_NSF_RES));
+          }
           cur = target;
         } else {
           // out must not alias the taps being read: ping-pong target <-> T1
           float* dst = (cur == target) ? T1 : target;
-          PD_TRY(nsf_conv(m->res[r + q], cur, NSF_LRELU, 1.f, B, Lc, dst, cur, ACT_NONE, st, U_NSF_RES));
+          if (wconv_ok(m->res[r + q]))
+            PD_TRY(launch_wconv(m->res[r + q], cur, false, NSF_LRELU, 1.f, B, Lc, dst, false, cur, st));
+          else
+            PD_TRY(nsf_conv(m->res[r + q], cur, NSF_LRELU, 1.f, B, Lc, dst, cur, ACT_NONE, st, U_NSF_RES));
           cur = dst;
         }
       }

@@ -21,6 +21,8 @@ from . import synth
 from .fastdiff import FastDiff
 from .prodiff import GaussianDiffusion, WaveNet
 from .vocoder import FastDiff as FastDiffVocoder
+from .nsf_hifigan import LOG10_TO_LN, Generator as NsfGenerator
+from .teacher import ProDiffTeacher
 
 # handler/base_config.yaml:195-211 (diffusion/decoder), modules/FastDiff/config/base.yaml:4-42
 PRODIFF_DEFAULTS = dict(in_dims=80, hidden_size=256, residual_layers=20, residual_channels=256,
@@ -61,6 +63,100 @@ class Synthesizer:
         g = None if seed is None else 2 * seed
         mel = self.diffusion.sample(cond, seed=g)
         wav = self.vocoder.spec2wav_torch(mel, seed=None if seed is None else g + 1)
+        return mel, wav
+
+
+# SVS path (handler/base_config.yaml: 128 mels, 44.1 kHz, hop 512, teacher timesteps 4,
+# NSF-HiFiGAN vocoder :216-219)
+SVS_TEACHER = dict(audio_num_mel_bins=128, hidden_size=256, enc_layers=4, enc_ffn_kernel_size=9, dropout=0.1,
+                   num_heads=2, num_spk=4, languages=["zh", "jp"], use_spk_id=True, use_lang_id=True,
+                   use_dur_embed=True, use_voicing_embed=True, use_breath_embed=True, use_gender_id=False,
+                   residual_layers=20, residual_channels=256, dilation_cycle_length=1, timesteps=4,
+                   timescale=1000, schedule_type="vpsde", max_beta=40.0, spec_min=[-12], spec_max=[0])
+SVS_HOP = 512
+SVS_SAMPLE_RATE = 44100
+SVS_VOCAB = 64
+
+TOKEN_KEYS = ("txt_tokens", "lang_seq")
+
+
+class SvsSynthesizer:
+    """SVS segment inputs -> (mel [B,T,128], wav [B,T*512]): ProDiffTeacher.forward(infer=True)
+    (handler/infer/handler.py:133-149 -> prodiff_teacher.py:148-168) then the NSF-HiFiGAN
+    vocoder's spec2wav_torch (component/vocoder/nsf_hifigan.py:29-56), all on the GPU."""
+
+    def __init__(self, teacher: ProDiffTeacher, generator: NsfGenerator, infer_step=4):
+        self.teacher, self.generator, self.infer_step = teacher, generator, infer_step
+        self.diffusion = teacher.diffusion
+
+    @classmethod
+    def synthetic(cls, device, seed=0, dtype="fp32", **over):
+        hp = dict(SVS_TEACHER, **over)
+        t = ProDiffTeacher(SVS_VOCAB, hp)
+        cp = synth.synth_cond_params(synth.cond_param_shapes(SVS_VOCAB, num_langs=len(hp["languages"]) + 1,
+                                                             **{k: v for k, v in hp.items() if k != "num_langs"}),
+                                     seed)
+        wn = synth.synth_params(synth.wavenet_param_shapes(hp["audio_num_mel_bins"], hp["hidden_size"],
+                                                           hp["residual_layers"], hp["residual_channels"]), seed + 1)
+        sd = {k: torch.from_numpy(v) for k, v in cp.items()}
+        sd.update({"diffusion.denoise_fn." + k: torch.from_numpy(v) for k, v in wn.items()})
+        t.load_state_dict(sd, strict=False)
+        h = dict(synth.NSF_DEFAULTS)
+        g = NsfGenerator(h)
+        g.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_params(synth.nsf_param_shapes(**h),
+                                                                                  seed + 2).items()})
+        t = t.to(device).eval().set_compute_dtype(dtype)
+        g = g.to(device).eval().set_compute_dtype(dtype)
+        return cls(t, g)
+
+    @staticmethod
+    def collate(items):
+        """Per-utterance dicts -> one batch: token fields padded with 0 (PAD) to the longest,
+        the frame fields (equal length within a batch) stacked; ``ntok`` keeps each
+        utterance's token count."""
+        out = {"ntok": [int(it["txt_tokens"].shape[0]) for it in items]}
+        for k in items[0]:
+            vs = [it[k] for it in items]
+            if k in TOKEN_KEYS:
+                n = max(v.shape[0] for v in vs)
+                vs = [torch.nn.functional.pad(v, (0, n - v.shape[0])) for v in vs]
+            out[k] = torch.stack(vs)
+        if "spk_mix_embed" in out:            # [B, 1, H]
+            out["spk_mix_embed"] = out["spk_mix_embed"].reshape(len(items), -1, out["spk_mix_embed"].shape[-1])
+        return out
+
+    @torch.no_grad()
+    def condition(self, batch):
+        """cond [B,T,H].  Utterances are encoded in groups of equal token count: token padding
+        is not neutral in the FFT encoder (the FFN conv reads LayerNorm(0) = beta on padded rows,
+        common_layers.py:668-669), and the reference encodes every segment alone (B=1)."""
+        b = {k: v for k, v in batch.items() if k != "ntok"}
+        ntok = batch.get("ntok") or [int(b["txt_tokens"].shape[1])] * int(b["txt_tokens"].shape[0])
+        groups = {}
+        for i, n in enumerate(ntok):
+            groups.setdefault(n, []).append(i)
+        if len(groups) == 1:
+            return self.teacher.forward_condition(b.pop("txt_tokens")[:, :ntok[0]], b.pop("mel2ph"), b.pop("f0"),
+                                                  lang_seq=None if "lang_seq" not in b else b.pop("lang_seq")[:, :ntok[0]],
+                                                  **b)
+        cond = None
+        for n, idx in groups.items():
+            ix = torch.tensor(idx, device=b["txt_tokens"].device)
+            sub = {k: v.index_select(0, ix) for k, v in b.items()}
+            if "lang_seq" in sub:
+                sub["lang_seq"] = sub["lang_seq"][:, :n]
+            c = self.teacher.forward_condition(sub.pop("txt_tokens")[:, :n], sub.pop("mel2ph"), sub.pop("f0"), **sub)
+            if cond is None:
+                cond = c.new_empty((b["txt_tokens"].shape[0],) + tuple(c.shape[1:]))
+            cond.index_copy_(0, ix, c)
+        return cond
+
+    @torch.no_grad()
+    def __call__(self, batch, seed=None):
+        g = None if seed is None else 3 * seed
+        cond = self.condition(batch)
+        mel = self.diffusion.sample(cond, infer_step=self.infer_step, seed=g)
+        wav = self.generator.synthesize(mel, batch["f0"], LOG10_TO_LN, seed=None if seed is None else g + 1)
         return mel, wav
 
 
@@ -140,7 +236,8 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     (handler/infer/handler.py:373-388).
 
     synth_fn(cond [B,T,H], seed) -> (mel [B,T,M], wav [B,T*hop]): one rank's
-      batched synthesis (a ``Synthesizer``).
+      batched synthesis (a ``Synthesizer``; an ``SvsSynthesizer`` takes per-utterance
+      input dicts, batched by its ``collate``).
     conds: list over ALL utterances (same order on every rank) of [T_i,H] tensors
       on this rank's device, or (T_i, callable returning one) pairs, so that only
       this rank's shard is materialized.
@@ -155,8 +252,9 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     shards = lpt_shards(lengths, world)
     mel_parts, wav_parts, order = [], [], []
     M = None
+    collate = getattr(synth_fn, "collate", torch.stack)
     for g, (T, idx) in enumerate(length_groups(lengths, shards[rank])):
-        cb = torch.stack([conds[i] if torch.is_tensor(conds[i]) else conds[i][1]() for i in idx])
+        cb = collate([conds[i] if torch.is_tensor(conds[i]) else conds[i][1]() for i in idx])
         mel, wav = synth_fn(cb, seed + 7919 * g + 104729 * rank)
         M = mel.shape[-1]
         mel_parts.append(mel.reshape(-1))

@@ -299,3 +299,21 @@ def synth_cond_inputs(seed, lengths, vocab_size, num_spk=1, num_langs=3, max_dur
     spk = rng.integers(0, num_spk, B).astype(np.int64)
     return dict(txt_tokens=tok, mel2ph=mel2ph, f0=f0, lang_seq=lang, spk_embed_id=spk,
                 voicing=voicing, breath=breath)
+
+
+def synth_svs_utterance(seed, frames, n_tokens, vocab_size, num_langs=3, hidden=256):
+    """One SVS segment as the inference handler builds it (handler/infer/handler.py:220-262):
+    n_tokens phonemes whose durations sum to exactly `frames` mel frames, f0 with unvoiced
+    gaps, voicing / breath curves and a time-invariant speaker mix [1, H]."""
+    rng = np.random.default_rng([int(seed), 0x5F5])
+    cuts = np.sort(rng.choice(np.arange(1, frames), n_tokens - 1, replace=False))
+    dur = np.diff(np.concatenate([[0], cuts, [frames]]))
+    tok = rng.integers(1, vocab_size, n_tokens).astype(np.int64)
+    lang = rng.integers(1, max(num_langs, 2), n_tokens).astype(np.int64)
+    mel2ph = np.repeat(np.arange(1, n_tokens + 1), dur).astype(np.int64)
+    f0 = rng.uniform(120.0, 700.0, frames).astype(np.float32)
+    f0[rng.random(frames) < 0.1] = 0.0
+    return dict(txt_tokens=tok, mel2ph=mel2ph, f0=f0, lang_seq=lang,
+                spk_mix_embed=(0.3 * rng.standard_normal((1, hidden))).astype(np.float32),
+                voicing=rng.uniform(-1.5, 1.0, frames).astype(np.float32),
+                breath=rng.uniform(-1.5, 1.0, frames).astype(np.float32))

@@ -103,3 +103,25 @@ def test_teacher_forward_infer_end_to_end():
     ref = t.diffusion(t.forward_condition(*args, **x), infer=True)
     assert mel.shape == (args[0].shape[0], args[1].shape[1], 128)
     assert torch.isfinite(mel).all() and torch.equal(mel, ref)
+
+
+def test_svs_synthesizer_ragged_tokens_and_pipeline():
+    """SvsSynthesizer (bench C5): a batch with different phoneme counts encodes each group
+    exactly as alone (B=1, the reference handler's way); the whole path returns finite
+    mel [B,T,128] and wav [B,T*512]; distributed_synthesize un-permutes it."""
+    from prodiff_amd import synth
+    from prodiff_amd.pipeline import SVS_VOCAB, SvsSynthesizer, distributed_synthesize
+    syn = SvsSynthesizer.synthetic(torch.device("cuda"), seed=0, dtype="fp32", residual_layers=2)
+    T = 40
+    utts = [{k: torch.from_numpy(v).cuda() for k, v in synth.synth_svs_utterance(s, T, n, SVS_VOCAB).items()}
+            for s, n in ((1, 9), (2, 13), (3, 9))]
+    batch = SvsSynthesizer.collate(utts)
+    cond = syn.condition(batch)
+    for i, u in enumerate(utts):
+        alone = syn.condition(SvsSynthesizer.collate([u]))
+        assert torch.equal(cond[i], alone[0]), i
+    mel, wav = syn(batch, seed=5)
+    assert mel.shape == (3, T, 128) and wav.shape == (3, T * 512)
+    assert torch.isfinite(mel).all() and torch.isfinite(wav).all() and wav.abs().max() <= 1.0
+    mels, wavs = distributed_synthesize(syn, [(T, (lambda u=u: u)) for u in utts], seed=5, hop=512)
+    assert len(mels) == 3 and all(m.shape == (T, 128) for m in mels) and all(w.shape == (T * 512,) for w in wavs)

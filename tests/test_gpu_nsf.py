@@ -82,19 +82,23 @@ def test_device_draws_deterministic_and_bounded():
     assert float((a[0].cpu() - torch.from_numpy(io["wav"][0])).abs().mean()) < 0.1
 
 
-def test_bf16_full_dims_vs_oracle():
-    """bf16 MFMA GEMMs against the fp64 oracle, with the shared bf16 bar (tests/bf16_bar.py)."""
+@pytest.mark.parametrize("wconv,T,B", [(1, 24, 1), (0, 24, 1), (1, 37, 2)])
+def test_bf16_full_dims_vs_oracle(wconv, T, B):
+    """bf16 path (windowed MFMA ResBlock convs, or the implicit-GEMM engine with wconv=0) against
+    the fp64 oracle with the shared bf16 bar (tests/bf16_bar.py); T=37 leaves partial 128-row
+    tiles at every stage, B=2 checks utterances do not bleed into each other's windows."""
     h = dict(synth.NSF_DEFAULTS)
     g, p = _gen(h, 7)
-    g.set_compute_dtype("bf16")
-    T, L = 24, 24 * 512
+    g.set_compute_dtype("bf16").set_options(wconv=wconv)
+    L = T * 512
     rng = np.random.default_rng(11)
-    mel = rng.normal(-2.0, 1.0, size=(1, T, 128)).astype(np.float32)
-    f0 = rng.uniform(60.0, 900.0, size=(1, T)).astype(np.float32)
+    mel = rng.normal(-2.0, 1.0, size=(B, T, 128)).astype(np.float32)
+    f0 = rng.uniform(60.0, 900.0, size=(B, T)).astype(np.float32)
     ri = rng.random(9, dtype=np.float32)
-    nz = rng.standard_normal((1, L, 9), dtype=np.float32)
+    nz = rng.standard_normal((B, L, 9), dtype=np.float32)
     wav = g.synthesize(torch.from_numpy(mel).to(DEV), torch.from_numpy(f0).to(DEV), 2.30259,
-                       rand_ini=torch.from_numpy(ri), noise=torch.from_numpy(nz)).cpu().numpy()[0]
-    ref = ON.spec2wav(p, h, mel, f0, ri, nz)[0]
+                       rand_ini=torch.from_numpy(ri), noise=torch.from_numpy(nz)).cpu().numpy()
     from tests.bf16_bar import assert_bf16_close
-    assert_bf16_close(wav, ref, "nsf full dims T=24")
+    for b in range(B):
+        ref = ON.spec2wav(p, h, mel[b:b + 1], f0[b:b + 1], ri, nz[b:b + 1])[0]
+        assert_bf16_close(wav[b], ref, f"nsf full dims T={T} wconv={wconv} b={b}")
