@@ -258,9 +258,9 @@ size_t nsf_workspace_size(const nsf_model* m, int B, int T);
 /* NSF_OPT_SMALL_MAX: ResBlock convs with at most this many channels run on the LDS/VALU small-channel
  * kernel (default 16, measured; 0 = never).  Set before the first forward call. */
 #define NSF_OPT_SMALL_MAX 0
-/* NSF_OPT_WCONV: 1 (default) runs the bf16 ResBlock convs with 32..256 channels on the windowed
- * MFMA conv kernel (input window staged once in LDS for all taps); 0 = the
- * implicit-GEMM engine.  No effect on the fp32 path. */
+/* NSF_OPT_WCONV: 1 (default) runs the bf16 ResBlock convs with 16..256 channels on the windowed
+ * MFMA conv kernels (input window staged once in LDS for all taps), ahead of
+ * NSF_OPT_SMALL_MAX; 0 = the implicit-GEMM engine / small kernel.  No effect on the fp32 path. */
 #define NSF_OPT_WCONV 1
 int nsf_set_option(nsf_model* m, int option, int value);
 

@@ -268,11 +268,14 @@ int launch_conv_small(const NsfConv& c, const float* in, float alpha, float scal
 // TM = 32 FM WM = 128 rows, TN = 32 FN WN output channels (grid.y covers C / TN),
 // grid.z = utterance.  LDS row stride C + 8 bf16: lanes r and r+1 of a b128 fragment read
 // sit 4 banks apart for every C used here, so a wave's fragment read is conflict-free.
+constexpr int NSF_PF = 4;   // weight-fragment prefetch depth (k-steps)
+
 template <int C, int FM, int FN, int WM, int WN, bool IN_BF, bool OUT_BF>
 __global__ __launch_bounds__(256) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
                                                         int ldw, int kpad, const float* __restrict__ bias, int taps,
                                                         int dil, float alpha, float scale, int Tl,
-                                                        const float* __restrict__ res, void* __restrict__ out) {
+                                                        const float* __restrict__ res, void* __restrict__ out,
+                                                        int accum) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN, LDA = C + 8, C8 = C / 8, KS = C / 16;
   static_assert(C % TN == 0, "channel tiling");
@@ -320,43 +323,176 @@ __global__ __launch_bounds__(256) void nsf_wconv_kernel(const void* __restrict__
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // B fragments run PF k-steps ahead in a register ring (one L2 round trip is ~2k cycles, one
+  // k-step of MFMAs ~100-200).  PF divides the k-steps per tap, so S = taps * KS is a multiple
+  // of PF and the loop body -- unrolled by PF, every slot index static -- has no branch; the
+  // last prefetches re-load the final step instead of testing the bound.
+  constexpr int PF = KS >= NSF_PF ? NSF_PF : KS;
+  static_assert(KS % PF == 0, "ring depth divides the k-steps per tap");
   const int S = taps * KS;
-  bf16x8 bcur[FN], bnext[FN];
+  bf16x8 bq[PF][FN];
+  auto bload = [&](int st, bf16x8* dst) {
+    const int tn = st / KS, kn = st - tn * KS;
 #pragma unroll
-  for (int j = 0; j < FN; ++j) bcur[j] = *reinterpret_cast<const bf16x8*>(wr[j]);
+    for (int j = 0; j < FN; ++j) dst[j] = *reinterpret_cast<const bf16x8*>(wr[j] + tn * kpad + 16 * kn);
+  };
+#pragma unroll
+  for (int q = 0; q < PF - 1; ++q) bload(q, bq[q]);
   const __bf16* arow = nsf_win + (wm * FM * 32 + r32) * LDA + 8 * h;
-  for (int s = 0; s < S; ++s) {
-    const int tap = s / KS, kc = s - tap * KS;
-    if (s + 1 < S) {
-      const int tn = (s + 1) / KS, kn = s + 1 - tn * KS;
+  for (int s0 = 0; s0 < S; s0 += PF) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bnext[j] = *reinterpret_cast<const bf16x8*>(wr[j] + tn * kpad + 16 * kn);
+    for (int q = 0; q < PF; ++q) {
+      const int s = s0 + q;
+      bload(min(s + PF - 1, S - 1), bq[(q + PF - 1) % PF]);
+      const int tap = s / KS, kc = s - tap * KS;
+      bf16x8 af[FM];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 32 + tap * dil) * LDA + 16 * kc);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bq[q][j], acc[i][j], 0, 0, 0);
     }
-    bf16x8 af[FM];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 32 + tap * dil) * LDA + 16 * kc);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bcur[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bcur[j] = bnext[j];
   }
-  // 3. epilogue: + bias (+ res), C/D map col = lane&31, row = (reg&3) + 8(reg>>2) + 4(lane>>5)
+  // 3. epilogue: + bias (+ res), C/D map col = lane&31, row = (reg&3) + 8(reg>>2) + 4(lane>>5).
+  // Branch-free loads (rows past the end clamp to the last row), so the residual reads of one
+  // M fragment are all in flight together; only the stores are predicated.
+  float bv[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bv[j] = bias[n0 + (wn * FN + j) * 32 + r32];
+  const long long rowb = (long long)b * Tl;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
+    float rv[16][FN];
+    if (res) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int t = min(t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tl - 1);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const long long o = (rowb + t) * C + n0 + (wn * FN + j) * 32 + r32;
+          rv[reg][j] = res[o];
+          if constexpr (!OUT_BF)
+            if (accum) rv[reg][j] += reinterpret_cast<const float*>(out)[o];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) rv[reg][j] = 0.f;
+    }
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int t = t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (t >= Tl) continue;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int n = n0 + (wn * FN + j) * 32 + r32;
-        const long long o = ((long long)b * Tl + t) * C + n;
-        float v = acc[i][j][reg] + bias[n];
-        if (res) v += res[o];
+        const long long o = (rowb + t) * C + n0 + (wn * FN + j) * 32 + r32;
+        const float v = acc[i][j][reg] + bv[j] + rv[reg][j];
+        if (t < Tl) {
+          if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
+          else reinterpret_cast<float*>(out)[o] = v;
+        }
+      }
+    }
+  }
+}
+
+// 16-channel variant (the last upsample stage, 512 samples per frame) on
+// v_mfma_f32_16x16x32_bf16: one MFMA's 32-deep K covers TWO taps x 16 channels (lane group
+// g = lane>>4 holds channels 8(g&1).. of tap 2p + (g>>1)); an odd tap count pads the last
+// pair with zero weights and zero activations.  All taps' weights fit in registers (<= 6
+// fragments), loaded once.  Block = 4 waves x 64 rows (4 M fragments of 16) = 256 rows.
+// MFMA 16x16x32 layouts: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15],
+// D[row 4(l>>4)+r][col l&15].
+template <bool IN_BF, bool OUT_BF>
+__global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
+                                                          int kpad, const float* __restrict__ bias, int taps, int dil,
+                                                          float alpha, float scale, int Tl,
+                                                          const float* __restrict__ res, void* __restrict__ out,
+                                                          int accum) {
+  constexpr int C = 16, TM = 256, LDA = 24, MAXP = 6;
+  extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win16[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.y, t0 = blockIdx.x * TM;
+  const int pad = (taps - 1) * dil / 2;
+  const int W = TM + (taps - 1) * dil;
+  for (int i = tid; i < W * 2; i += 256) {
+    const int row = i >> 1, c8 = i & 1;
+    const int t = t0 - pad + row;
+    bf16x8 v;
+    if (t >= 0 && t < Tl) {
+      float f[8];
+      const long long e = ((long long)b * Tl + t) * C + 8 * c8;
+      if constexpr (IN_BF) {
+        const bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(in) + e);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (float)x[j];
+      } else {
+        const float4 x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e);
+        const float4 x1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e + 4);
+        f[0] = x0.x; f[1] = x0.y; f[2] = x0.z; f[3] = x0.w; f[4] = x1.x; f[5] = x1.y; f[6] = x1.z; f[7] = x1.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[j] >= 0.f ? f[j] : alpha * f[j]) * scale);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(nsf_win16 + row * LDA + 8 * c8) = v;
+  }
+  const int r16 = lane & 15, g = lane >> 4, kg = g & 1, tg = g >> 1;
+  const int npair = (taps + 1) >> 1;
+  bf16x8 bw[MAXP];
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int tap = 2 * p + tg;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bw[p][j] = (__bf16)0.f;
+    if (p < npair && tap < taps) bw[p] = *reinterpret_cast<const bf16x8*>(w + (long long)r16 * (taps * kpad) + tap * kpad + 8 * kg);
+  }
+  __syncthreads();
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    if (p < npair) {
+      const int tap = 2 * p + tg;
+      const bool live = tap < taps;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bf16x8 af;
+        if (live) {
+          af = *reinterpret_cast<const bf16x8*>(nsf_win16 + (wave * 64 + i * 16 + r16 + tap * dil) * LDA + 8 * kg);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) af[j] = (__bf16)0.f;
+        }
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[p], acc[i], 0, 0, 0);
+      }
+    }
+  }
+  const float bn = bias[r16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float rv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = min(t0 + wave * 64 + i * 16 + 4 * g + r, Tl - 1);
+      const long long o = ((long long)b * Tl + t) * C + r16;
+      rv[r] = res ? res[o] : 0.f;
+      if constexpr (!OUT_BF)
+        if (accum) rv[r] += reinterpret_cast<const float*>(out)[o];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = t0 + wave * 64 + i * 16 + 4 * g + r;
+      const long long o = ((long long)b * Tl + t) * C + r16;
+      const float v = acc[i][r] + bn + rv[r];
+      if (t < Tl) {
         if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
         else reinterpret_cast<float*>(out)[o] = v;
       }
@@ -364,9 +500,62 @@ __global__ __launch_bounds__(256) void nsf_wconv_kernel(const void* __restrict__
   }
 }
 
+int launch_wconv16(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
+                   int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum) {
+  if (c.taps > 12) { set_error("nsf wconv16: at most 12 taps"); return PD_ERR_UNSUPPORTED; }
+  const size_t lds = (size_t)(256 + (c.taps - 1) * c.dil) * 24 * sizeof(__bf16);
+  dim3 grid(cdiv(Tl, 256), B);
+  ProfScope ps("nsf_res_small", st);
+#define PD_WCONV16(IB, OB)                                                                                      \
+  hipLaunchKernelGGL((nsf_wconv16_kernel<IB, OB>), grid, dim3(256), lds, st, in, wb, c.kpad, c.b, c.taps, c.dil, \
+                     alpha, scale, Tl, res, out, accum)
+  if (in_bf && out_bf) PD_WCONV16(true, true);
+  else if (in_bf) PD_WCONV16(true, false);
+  else if (out_bf) PD_WCONV16(false, true);
+  else PD_WCONV16(false, false);
+#undef PD_WCONV16
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// conv_post (models.py:280-282): wav = tanh(conv7(leaky_relu(x, 0.01) * scale)) with ONE output
+// channel -- a GEMM with N = 1 would leave 31/32 of every MFMA tile empty.  fp32 VALU: each
+// block stages 256 + 6 rows of the C-channel input (activation applied once) and the C x 7
+// weights in LDS; one thread per output sample.
+template <int C>
+__global__ __launch_bounds__(256) void nsf_post_kernel(const float* __restrict__ in, const float* __restrict__ wp,
+                                                       int kpad, const float* __restrict__ bias, float alpha,
+                                                       float scale, int Tl, float* __restrict__ out) {
+  constexpr int TR = 256, K = 7, P = C + 1;
+  __shared__ float s_x[(TR + K - 1) * P];
+  __shared__ float s_w[K * C];
+  const int tid = threadIdx.x, b = blockIdx.y, t0 = blockIdx.x * TR;
+  for (int i = tid; i < K * C; i += 256) s_w[i] = wp[(i / C) * kpad + i % C];
+  const float* ib = in + (long long)b * Tl * C;
+  for (int i = tid; i < (TR + K - 1) * C; i += 256) {
+    const int row = i / C, c = i - row * C;
+    const int t = t0 - (K - 1) / 2 + row;
+    float v = 0.f;
+    if (t >= 0 && t < Tl) {
+      v = ib[(long long)t * C + c];
+      v = (v >= 0.f ? v : alpha * v) * scale;
+    }
+    s_x[row * P + c] = v;
+  }
+  __syncthreads();
+  const int t = t0 + tid;
+  if (t >= Tl) return;
+  float acc = bias[0];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc = fmaf(s_w[k * C + c], s_x[(tid + k) * P + c], acc);
+  out[(long long)b * Tl + t] = tanhf(acc);
+}
+
 template <int C, int FM, int FN, int WM, int WN>
 int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
-                   int Tl, void* out, bool out_bf, const float* res, hipStream_t st) {
+                   int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum) {
   constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN;
   const size_t lds = (size_t)(TM + (c.taps - 1) * c.dil) * (C + 8) * sizeof(__bf16);
   if (lds > 160 * 1024) { set_error("nsf conv: LDS window too large"); return PD_ERR_UNSUPPORTED; }
@@ -379,7 +568,7 @@ int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_b
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                                                  \
     if (attr != hipSuccess) { set_error("nsf conv: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }    \
     hipLaunchKernelGGL((nsf_wconv_kernel<C, FM, FN, WM, WN, IB, OB>), grid, dim3(256), lds, st, in, wb, ldw,      \
-                       c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out);                                   \
+                       c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out, accum);                            \
   } while (0)
   ProfScope ps("nsf_res", st);
   if (in_bf && out_bf) PD_WCONV(true, true);
@@ -391,20 +580,24 @@ int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_b
   return PD_OK;
 }
 
-// The windowed conv for this ResBlock conv, if it has one (bf16 weights, C in {32..256}).
+// The windowed conv for this ResBlock conv, if it has one (bf16 weights, C in {16..256}); on the
+// bf16 path it takes precedence over NSF_OPT_SMALL_MAX, which then only routes the fp32 path.
 bool wconv_ok(const NsfConv& c) {
-  return c.wconv && c.cin == c.cout && c.cout > c.small_max && c.taps <= 11 && lookup_bf16(c.w) != nullptr &&
-         (c.cout == 32 || c.cout == 64 || c.cout == 128 || c.cout == 256);
+  return c.wconv && c.cin == c.cout && c.taps <= 11 && lookup_bf16(c.w) != nullptr &&
+         (c.cout == 16 || c.cout == 32 || c.cout == 64 || c.cout == 128 || c.cout == 256);
 }
 
+// accum = 1: out (fp32) += conv + res -- the ResBlock sum xs += resblock_j(x) (models.py:275-279)
+// fused into the block's last conv instead of a separate pass.
 int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, float scale, int B, int Tl, void* out,
-                 bool out_bf, const float* res, hipStream_t st) {
+                 bool out_bf, const float* res, hipStream_t st, int accum = 0) {
   const __bf16* wb = lookup_bf16(c.w);
   switch (c.cout) {
-    case 256: return launch_wconv_c<256, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st);
-    case 128: return launch_wconv_c<128, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st);
-    case 64: return launch_wconv_c<64, 2, 1, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st);
-    case 32: return launch_wconv_c<32, 1, 1, 4, 1>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st);
+    case 256: return launch_wconv_c<256, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
+    case 128: return launch_wconv_c<128, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
+    case 64: return launch_wconv_c<64, 2, 1, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
+    case 32: return launch_wconv_c<32, 1, 1, 4, 1>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
+    case 16: return launch_wconv16(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
     default: set_error("nsf wconv: unsupported channel count"); return PD_ERR_UNSUPPORTED;
   }
 }
@@ -774,14 +967,19 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
     for (int j = 0; j < nk; ++j) {
       float* target = j == 0 ? XS : R;
       const float* cur = X;
+      bool summed = false;   // resblock_j(x) already added into XS by its last conv
       for (int q = 0; q < d.num_dilations; ++q) {
         if (d.resblock == 1) {
           const NsfConv& c1 = m->res[r + q];
           const NsfConv& c2 = m->res[r + d.num_dilations + q];
           if (wconv_ok(c1) && wconv_ok(c2)) {
-            // windowed bf16 convs; the inner activation xt = c1(lrelu(x)) travels as bf16
+            // windowed bf16 convs; the inner activation xt = c1(lrelu(x)) travels as bf16; the
+            // last pair of resblock j >= 1 accumulates straight into XS
+            const bool last_acc = j > 0 && q == d.num_dilations - 1;
             PD_TRY(launch_wconv(c1, cur, false, NSF_LRELU, 1.f, B, Lc, T1, true, nullptr, st));
-            PD_TRY(launch_wconv(c2, T1, true, NSF_LRELU, 1.f, B, Lc, target, false, cur, st));
+            PD_TRY(launch_wconv(c2, T1, true, NSF_LRELU, 1.f, B, Lc, last_acc ? XS : target, false, cur, st,
+                                last_acc ? 1 : 0));
+            if (last_acc) { summed = true; continue; }
           } else {
             PD_TRY(nsf_conv(c1, cur, NSF_LRELU, 1.f, B, Lc, T1, nullptr, ACT_NONE, st, U_NSF_RES));
             PD_TRY(nsf_conv(c2, T1, NSF_LRELU, 1.f, B, Lc, target, cur, ACT_NONE, st, U_NSF_RES));
@@ -798,6 +996,7 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
         }
       }
       r += m->convs_per_block;
+      if (summed) continue;
       if (j == 0 && cur == XS) continue;
       ProfScope ps("nsf_accum", st);
       hipLaunchKernelGGL(nsf_accum_kernel, dim3(cdiv(n4, 256)), dim3(256), 0, st, reinterpret_cast<float4*>(XS),
@@ -808,7 +1007,18 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
     in_scale = 1.f / (float)nk;
   }
   // tanh(conv_post(leaky_relu(x, 0.01)))  (models.py:280-282)
-  PD_TRY(nsf_conv(m->post, XS, 0.01f, in_scale, B, Tin, wav, nullptr, ACT_TANH, st, U_NSF_POST));
+  if (m->post.taps == 7 && m->post.cout == 1 && (m->post.cin == 16 || m->post.cin == 32)) {
+    ProfScope ps("nsf_post", st);
+    if (m->post.cin == 16)
+      hipLaunchKernelGGL(nsf_post_kernel<16>, dim3(cdiv(Tin, 256), B), dim3(256), 0, st, XS, m->post.w, m->post.kpad,
+                         m->post.b, 0.01f, in_scale, Tin, wav);
+    else
+      hipLaunchKernelGGL(nsf_post_kernel<32>, dim3(cdiv(Tin, 256), B), dim3(256), 0, st, XS, m->post.w, m->post.kpad,
+                         m->post.b, 0.01f, in_scale, Tin, wav);
+    PD_LAUNCH_CHECK();
+  } else {
+    PD_TRY(nsf_conv(m->post, XS, 0.01f, in_scale, B, Tin, wav, nullptr, ACT_TANH, st, U_NSF_POST));
+  }
   return PD_OK;
 }
 
