@@ -200,7 +200,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   int ch_begin = 0, nchunks = a.ldw / BK;
-  if (EPI == EPI_STORE && a.ksplit > 1) {   // this block's K range (host makes every range non-empty)
+  constexpr bool SPLITTABLE = (EPI == EPI_STORE || PAIRED);
+  if (SPLITTABLE && a.ksplit > 1) {   // this block's K range (host makes every range non-empty)
     const int cps = (nchunks + a.ksplit - 1) / a.ksplit;
     ch_begin = blockIdx.z * cps;
     nchunks = min(nchunks, ch_begin + cps);
@@ -281,6 +282,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
       const int rl = wm * 32 * WM_T + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
       const int R = row0 + rl;
       if (R >= rows) continue;
+      if constexpr (PAIRED) {
+        if (a.ksplit > 1) {   // raw partial sums of both halves; gemm_splitk_reduce applies the epilogue
+          float* pz = a.part + ((long long)blockIdx.z * rows + R) * a.N + nb + r32;
+          pz[0] = acc[i][0][reg];
+          pz[a.half] = acc[i][1][reg];
+          continue;
+        }
+      }
       const int b = R / a.T, t = R - b * a.T;
       if constexpr (EPI == EPI_GATE) {
         const int n = nb + r32;
@@ -330,8 +339,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
 // Host-side validation + launch.  Returns PD_OK or an error code.
 int validate_gemm(const GemmArgs& a);
 
-// Split-K epilogue: out = act(sum_z part[z] + bias) * scale (+ res), as EPI_STORE's.
-int gemm_splitk_reduce(const GemmArgs& a, hipStream_t st);
+// Split-K epilogue: out = act(sum_z part[z] + bias) * scale (+ res), as EPI_STORE's; or the
+// paired GATE / RESSKIP epilogues on the summed halves.
+int gemm_splitk_reduce(const GemmArgs& a, int epi, hipStream_t st);
 
 const __bf16* lookup_bf16(const float* p);
 
@@ -352,8 +362,8 @@ int launch_gemm(const GemmArgs& a0, hipStream_t st, const char* tag) {
   }
   if (a.ksplit > 1) {
     const int nch = a.ldw / GEMM_BK;
-    if (EPI != EPI_STORE || !a.part || a.ksplit > nch) {
-      set_error("split-K needs EPI_STORE, a partial-sum buffer and ksplit <= K / 32");
+    if (!(EPI == EPI_STORE || PAIRED) || !a.part || a.ksplit > nch) {
+      set_error("split-K needs EPI_STORE / GATE / RESSKIP, a partial-sum buffer and ksplit <= K / 32");
       return PD_ERR_ARG;
     }
     const int cps = cdiv(nch, a.ksplit);
@@ -367,7 +377,7 @@ int launch_gemm(const GemmArgs& a0, hipStream_t st, const char* tag) {
     else
       hipLaunchKernelGGL((gemm_kernel<float, WM_T, WN_T, WAVES_M, WAVES_N, EPI, ID>), grid, dim3(256), 0, st, a);
     PD_LAUNCH_CHECK();
-    if (a.ksplit > 1) PD_TRY(gemm_splitk_reduce(a, st));
+    if (a.ksplit > 1) PD_TRY(gemm_splitk_reduce(a, EPI, st));
   }
   return PD_OK;
 }

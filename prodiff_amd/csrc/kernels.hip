@@ -59,9 +59,42 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs a) {
   else a.out[oi] = v;
 }
 
-int gemm_splitk_reduce(const GemmArgs& a, hipStream_t st) {
-  const long long n = (long long)a.B * a.T * a.N;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, a);
+// paired epilogues over (row, n < half): columns n and n + half combine (gemm.h EPI_GATE / EPI_RESSKIP)
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_paired_kernel(const GemmArgs a) {
+  const long long rows = (long long)a.B * a.T;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * a.half) return;
+  const long long R = i / a.half;
+  const int n = (int)(i - R * a.half);
+  float v0 = a.bias[n], v1 = a.bias[a.half + n];
+  for (int z = 0; z < a.ksplit; ++z) {
+    const float* pz = a.part + (z * rows + R) * a.N + n;
+    v0 += pz[0];
+    v1 += pz[a.half];
+  }
+  const long long b = R / a.T, t = R - b * a.T;
+  if constexpr (EPI == EPI_GATE) {
+    a.out[b * a.out_bs + t * a.out_ld + n] = sigmoidf_(v0) * tanhf_(v1);
+  } else {
+    float* xp = a.out + b * a.out_bs + t * a.out_ld + n;
+    *xp = (*xp + v0) * 0.70710678118654752440f;
+    float* sp = a.out2 + b * a.out2_bs + t * a.out2_ld + n;
+    *sp = a.flag ? v1 : (*sp + v1);
+  }
+}
+
+int gemm_splitk_reduce(const GemmArgs& a, int epi, hipStream_t st) {
+  const long long rows = (long long)a.B * a.T;
+  if (epi == EPI_GATE || epi == EPI_RESSKIP) {
+    const long long n = rows * a.half;
+    if (epi == EPI_GATE)
+      hipLaunchKernelGGL(splitk_reduce_paired_kernel<EPI_GATE>, dim3(cdiv(n, 256)), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL(splitk_reduce_paired_kernel<EPI_RESSKIP>, dim3(cdiv(n, 256)), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(rows * a.N, 256)), dim3(256), 0, st, a);
+  }
   PD_LAUNCH_CHECK();
   return PD_OK;
 }

@@ -401,8 +401,19 @@ __global__ void wn_xa_kernel(const float* __restrict__ x, const float* __restric
 }
 
 struct WsLayout {
-  size_t x, x2, g, skip, hs, xin, condT, outT, steps, emb, h1, d, dproj, xa, condb, total;
+  size_t x, x2, g, skip, hs, xin, condT, outT, steps, emb, h1, d, dproj, xa, condb, part, total;
 };
+
+// fp32 residual-layer GEMMs (128 x 64 paired tiles): split K over up to 8 blocks when the
+// row x channel grid leaves CUs idle -- the B = 1 latency case (C2: T = 1000 gives 64 blocks
+// and 32 K steps each).  Partials [ks][B*T][2C] are reduced by the paired GATE / RESSKIP epilogue.
+int wn_ksplit(long long rows, int half, int K) {
+  const long long gxy = (long long)cdiv(rows, 128) * (half / 32);
+  if (gxy >= 256) return 1;
+  int ks = (int)std::min<long long>(8, (256 + gxy - 1) / gxy);
+  ks = std::min(ks, std::max(1, K / GEMM_BK / 4));
+  return std::max(ks, 1);
+}
 
 WsLayout ws_layout(const pd_wavenet* h, int B, int T, int S) {
   WsLayout w{};
@@ -428,6 +439,13 @@ WsLayout ws_layout(const pd_wavenet* h, int B, int T, int S) {
   w.dproj = take((size_t)S * B * h->L * h->C);
   w.xa = take(BT * h->C / 2 + 8);                 // bf16 [B*T][C] (two-GEMM layer path)
   w.condb = take(BT * h->H / 2 + 8);              // bf16 [B*T][H]
+  size_t part = 0;
+  if (!h->W1f) {
+    const int k1 = wn_ksplit((long long)BT, h->C, h->ldw1), k2 = wn_ksplit((long long)BT, h->C, h->C);
+    const int ks = std::max(k1, k2);
+    if (ks > 1) part = (size_t)ks * BT * 2 * h->C;
+  }
+  w.part = take(part);
   w.total = off * sizeof(float);
   return w;
 }
@@ -539,6 +557,8 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       }
       add_seg(a, make_seg(cond, BTs * H, H, H, 0));
       a.half = C;
+      a.ksplit = wn_ksplit((long long)B * T, C, h->ldw1);
+      a.part = ws + Lw.part;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_GATE, U_WN_GATE>(a, st, "wn_gate")));
     }
     {  // o = W_out g + b ; x = (x + o[:C]) / sqrt2 ; skip += o[C:]   (wavenet.py:69-72)
@@ -548,6 +568,8 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       a.half = C;
       a.out2 = skip; a.out2_bs = BTs * C; a.out2_ld = C;
       a.flag = (l == 0);
+      a.ksplit = wn_ksplit((long long)B * T, C, C);
+      a.part = ws + Lw.part;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_RESSKIP, U_WN_RESSKIP>(a, st, "wn_resskip")));
     }
   }
