@@ -88,6 +88,9 @@ void pd_wavenet_destroy(pd_wavenet* h);
  * block (B*T >= 16384 frames) else 32, 1 two GEMM launches per layer with 128 x 128 tiles
  * (DESIGN.md §4). */
 #define PD_WN_OPT_LAYER 0
+/* PD_WN_OPT_KSPLIT (fp32 path): the residual-layer GEMMs split their K range over several blocks
+ * until the grid holds 512 (default) or 256 blocks; 0 = never split. */
+#define PD_WN_OPT_KSPLIT 1
 int pd_wavenet_set_option(pd_wavenet* h, int option, int value);
 /* S = number of reverse steps the workspace must serve (1 for pd_wavenet_forward). */
 size_t pd_wavenet_workspace_size(const pd_wavenet* h, int B, int T, int S);

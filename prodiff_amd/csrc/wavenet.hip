@@ -33,6 +33,7 @@ struct pd_wavenet {
   // bf16 residual layer (PD_WN_OPT_LAYER): 0 = fused kernel, 32 frames per block; 3 = fused, 64
   // frames per block; 2 = auto between the two by grid size; 1 = two 128x128-tile GEMMs
   int layer_mode = 2;
+  int ksplit_blocks = 512;   // PD_WN_OPT_KSPLIT: fp32 layer GEMMs split K up to this many blocks
 };
 
 namespace {
@@ -406,12 +407,13 @@ struct WsLayout {
 
 // fp32 residual-layer GEMMs (128 x 64 paired tiles): split K over up to 8 blocks when the
 // row x channel grid leaves CUs idle -- the B = 1 latency case (C2: T = 1000 gives 64 blocks
-// and 32 K steps each).  Partials [ks][B*T][2C] are reduced by the paired GATE / RESSKIP epilogue.
-int wn_ksplit(long long rows, int half, int K) {
+// and 32 K steps each).  Target 512 blocks (two per CU) measured best (r02: C2 2.10 ms/step vs
+// 2.40 at 256 and 4.79 unsplit).  Partials [ks][B*T][2C] are reduced by the paired GATE / RESSKIP epilogue.
+int wn_ksplit(long long rows, int half, int K, int target = 512) {
   const long long gxy = (long long)cdiv(rows, 128) * (half / 32);
   if (gxy >= 256) return 1;
-  int ks = (int)std::min<long long>(8, (256 + gxy - 1) / gxy);
-  ks = std::min(ks, std::max(1, K / GEMM_BK / 4));
+  int ks = (int)std::min<long long>(8, (target + gxy - 1) / gxy);
+  ks = std::min(ks, std::max(1, K / GEMM_BK / 2));   // >= 2 K steps per block
   return std::max(ks, 1);
 }
 
@@ -441,7 +443,7 @@ WsLayout ws_layout(const pd_wavenet* h, int B, int T, int S) {
   w.condb = take(BT * h->H / 2 + 8);              // bf16 [B*T][H]
   size_t part = 0;
   if (!h->W1f) {
-    const int k1 = wn_ksplit((long long)BT, h->C, h->ldw1), k2 = wn_ksplit((long long)BT, h->C, h->C);
+    const int k1 = wn_ksplit((long long)BT, h->C, h->ldw1, 512), k2 = wn_ksplit((long long)BT, h->C, h->C, 512);
     const int ks = std::max(k1, k2);
     if (ks > 1) part = (size_t)ks * BT * 2 * h->C;
   }
@@ -557,7 +559,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       }
       add_seg(a, make_seg(cond, BTs * H, H, H, 0));
       a.half = C;
-      a.ksplit = wn_ksplit((long long)B * T, C, h->ldw1);
+      a.ksplit = wn_ksplit((long long)B * T, C, h->ldw1, h->ksplit_blocks);
       a.part = ws + Lw.part;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_GATE, U_WN_GATE>(a, st, "wn_gate")));
     }
@@ -568,7 +570,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       a.half = C;
       a.out2 = skip; a.out2_bs = BTs * C; a.out2_ld = C;
       a.flag = (l == 0);
-      a.ksplit = wn_ksplit((long long)B * T, C, C);
+      a.ksplit = wn_ksplit((long long)B * T, C, C, h->ksplit_blocks);
       a.part = ws + Lw.part;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_RESSKIP, U_WN_RESSKIP>(a, st, "wn_resskip")));
     }
@@ -701,6 +703,11 @@ int pd_wavenet_set_option(pd_wavenet* h, int option, int value) {
   if (option == PD_WN_OPT_LAYER) {
     PD_CHECK_ARG(value >= 0 && value <= 3, "PD_WN_OPT_LAYER is 0, 1, 2 or 3");
     h->layer_mode = value;
+    return PD_OK;
+  }
+  if (option == PD_WN_OPT_KSPLIT) {
+    PD_CHECK_ARG(value == 0 || value == 256 || value == 512, "PD_WN_OPT_KSPLIT is 0 (no split), 256 or 512");
+    h->ksplit_blocks = value == 0 ? 1 : value;
     return PD_OK;
   }
   set_error("pd_wavenet_set_option: unknown option " + std::to_string(option));
