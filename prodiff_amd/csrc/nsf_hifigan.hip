@@ -59,6 +59,7 @@ struct nsf_model {
   NsfConv pre, post;
   std::vector<NsfUps> ups;
   std::vector<NsfConv> res;      // [stage][kernel][conv] flattened in state-dict order
+  bool ups_window = true;        // NSF_OPT_WCONV also selects the windowed ConvTranspose
   int convs_per_block = 0;
 };
 
@@ -553,6 +554,173 @@ __global__ __launch_bounds__(256) void nsf_post_kernel(const float* __restrict__
   out[(long long)b * Tl + t] = tanhf(acc);
 }
 
+// ConvTranspose1d(k = ntap*u, stride u, padding p) + noise-conv add (models.py:270-274) on the
+// bf16 MFMA path, windowed like nsf_wconv_kernel.  Output row o_phi + q*u (phase phi, input row
+// q) = b + sum_mt W_phi,mt . lrelu(x[q + q0_phi - mt]) + res; q0_phi = ceil((p - phi)/u) if
+// p > phi else 0, o_phi = q0_phi*u + phi - p (the host's NsfUps::qmin).  A block stages TQ + halo
+// input rows ONCE and runs every phase from that window (the phase-GEMM path re-reads the
+// input 2u times); weights of all phases are contiguous [phi][cout][ntap*kpad] (bf16 mirror),
+// streamed in a PF-deep register ring across the phase boundaries.  NPAD: cout < 32 channels
+// on a 32-wide tile (weight rows clamped, extra columns dropped).
+template <int CIN, int FM, int FN, int WM, int WN, bool NPAD>
+__global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict__ in, const __bf16* __restrict__ w,
+                                                      long long wstride, int kpad, int ntap, int u, int p, int dlo,
+                                                      int cout, const float* __restrict__ bias, float alpha,
+                                                      float scale, int Tin, const float* __restrict__ res,
+                                                      float* __restrict__ out) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN, LDA = CIN + 8, C8 = CIN / 8, KS = CIN / 16;
+  constexpr int PF = KS >= NSF_PF ? NSF_PF : KS;
+  extern __shared__ __attribute__((aligned(16))) __bf16 nsf_uwin[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int b = blockIdx.z, i0 = blockIdx.x * TQ, n0 = blockIdx.y * TN;
+  const int W = TQ + ntap;                 // rows i0 + dlo ... (dlo = 1 - ntap, top offset q0 <= 1)
+  for (int i = tid; i < W * C8; i += 256) {
+    const int row = i / C8, c8 = i - row * C8;
+    const int q = i0 + dlo + row;
+    bf16x8 v;
+    if (q >= 0 && q < Tin) {
+      const float* src = in + ((long long)b * Tin + q) * CIN + 8 * c8;
+      const float4 x0 = *reinterpret_cast<const float4*>(src);
+      const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+      const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[j] >= 0.f ? f[j] : alpha * f[j]) * scale);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(nsf_uwin + row * LDA + 8 * c8) = v;
+  }
+  __syncthreads();
+  const int r32 = lane & 31, h = lane >> 5;
+  const int ldw = ntap * kpad;
+  const __bf16* wr[FN];
+  bool ncol[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + (wn * FN + j) * 32 + r32;
+    ncol[j] = !NPAD || n < cout;
+    wr[j] = w + (long long)(NPAD ? min(n, cout - 1) : n) * ldw + 8 * h;
+  }
+  const int Sph = ntap * KS, S = u * Sph;
+  bf16x8 bq[PF][FN];
+  auto bload = [&](int st, bf16x8* dst) {
+    const int ph = st / Sph, rem = st - ph * Sph, mt = rem / KS, kn = rem - mt * KS;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      dst[j] = *reinterpret_cast<const bf16x8*>(wr[j] + ph * wstride + mt * kpad + 16 * kn);
+  };
+#pragma unroll
+  for (int q = 0; q < PF - 1; ++q) bload(q, bq[q]);
+  float bv[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bv[j] = ncol[j] ? bias[n0 + (wn * FN + j) * 32 + r32] : 0.f;
+  const __bf16* arow = nsf_uwin + (wm * FM * 32 + r32) * LDA + 8 * h;
+#pragma unroll 1
+  for (int phi = 0; phi < u; ++phi) {
+    const int q0 = p - phi > 0 ? (p - phi + u - 1) / u : 0;
+    const int o = q0 * u + phi - p;
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll 1
+    for (int s0 = 0; s0 < Sph; s0 += PF) {
+#pragma unroll
+      for (int qq = 0; qq < PF; ++qq) {
+        const int sl = s0 + qq, sg = phi * Sph + sl;
+        bload(min(sg + PF - 1, S - 1), bq[(qq + PF - 1) % PF]);
+        const int mt = sl / KS, kc = sl - mt * KS;
+        const int roff = q0 - mt - dlo;
+        bf16x8 af[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 32 + roff) * LDA + 16 * kc);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bq[qq][j], acc[i][j], 0, 0, 0);
+      }
+    }
+    // epilogue of this phase: rows o + q*u (q < Tin), + bias + noise-conv output; the 16
+    // residual loads of one fragment are issued together (clamped rows, predicated stores)
+    const int Lc = Tin * u;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + (wn * FN + j) * 32 + r32;
+        const int nc = NPAD ? min(n, cout - 1) : n;
+        float rv[16];
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int q = min(i0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tin - 1);
+          rv[reg] = res[((long long)b * Lc + o + (long long)q * u) * cout + nc];
+        }
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int q = i0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          if (q < Tin && ncol[j])
+            out[((long long)b * Lc + o + (long long)q * u) * cout + n] = acc[i][j][reg] + bv[j] + rv[reg];
+        }
+      }
+    }
+  }
+}
+
+template <int CIN, int FM, int FN, int WM, int WN, bool NPAD>
+int launch_ups_c(const NsfUps& U, const __bf16* wb, const float* in, float scale, int B, int Tin, const float* res,
+                 float* out, hipStream_t st) {
+  constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN;
+  const int p = (U.k - U.u) / 2;
+  const size_t lds = (size_t)(TQ + U.ntap) * (CIN + 8) * sizeof(__bf16);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) { set_error("nsf ups: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
+  dim3 grid(cdiv(Tin, TQ), NPAD ? 1 : U.cout / TN, B);
+  ProfScope ps("nsf_ups", st);
+  hipLaunchKernelGGL((nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD>), grid, dim3(256), lds, st, in, wb,
+                     (long long)(U.w[1] - U.w[0]), U.kpad, U.ntap, U.u, p, 1 - U.ntap, U.cout, U.b, NSF_LRELU,
+                     scale, Tin, res, out);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// The windowed ConvTranspose for this upsample, if it has one: bf16 weights, phases packed
+// back to back, k = 2u with the phase offsets the kernel derives, a channel pair it is built for.
+bool ups_window_ok(const NsfUps& U, bool wconv) {
+  if (!wconv || U.u < 2 || U.ntap != 2 || U.k != 2 * U.u || U.w.size() != (size_t)U.u || !lookup_bf16(U.w[0]))
+    return false;
+  const long long stride = U.w[1] - U.w[0];
+  if (stride != (long long)U.cout * U.ntap * U.kpad) return false;
+  for (int phi = 1; phi < U.u; ++phi)
+    if (U.w[phi] - U.w[phi - 1] != stride) return false;
+  const int p = (U.k - U.u) / 2;
+  for (int phi = 0; phi < U.u; ++phi) {
+    const int q0 = p - phi > 0 ? (p - phi + U.u - 1) / U.u : 0;
+    if (q0 != U.qmin[phi] || q0 > 1) return false;
+  }
+  return (U.cin == 512 && U.cout == 256) || (U.cin == 256 && U.cout == 128) || (U.cin == 128 && U.cout == 64) ||
+         (U.cin == 64 && U.cout == 32) || (U.cin == 32 && U.cout == 16);
+}
+
+int launch_ups_window(const NsfUps& U, const float* in, float scale, int B, int Tin, const float* res, float* out,
+                      hipStream_t st) {
+  const __bf16* wb = lookup_bf16(U.w[0]);
+  if (U.cin == 512) return launch_ups_c<512, 1, 2, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);
+  if (U.cin == 256) return launch_ups_c<256, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);
+  if (U.cin == 128) return launch_ups_c<128, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);
+  if (U.cin == 64) return launch_ups_c<64, 1, 1, 4, 1, false>(U, wb, in, scale, B, Tin, res, out, st);
+  return launch_ups_c<32, 1, 1, 4, 1, true>(U, wb, in, scale, B, Tin, res, out, st);
+}
+
 template <int C, int FM, int FN, int WM, int WN>
 int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
                    int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum) {
@@ -880,6 +1048,7 @@ int nsf_set_option(nsf_model* m, int option, int value) {
   if (option == NSF_OPT_WCONV) {
     PD_CHECK_ARG(value == 0 || value == 1, "NSF_OPT_WCONV is 0 or 1");
     for (auto& c : m->res) c.wconv = value != 0;
+    m->ups_window = value != 0;
     return PD_OK;
   }
   set_error("nsf_set_option: unknown option " + std::to_string(option));
@@ -941,9 +1110,12 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
                          L, U.nc_w, U.nc_b, U.cout, U.nc_k, U.nc_stride, U.nc_pad, (long long)Lc, XSRC);
       PD_LAUNCH_CHECK();
     }
-    // x = ups(leaky_relu(x, 0.1)) + noise_conv(har)  (models.py:270-274), one GEMM per phase
+    // x = ups(leaky_relu(x, 0.1)) + noise_conv(har)  (models.py:270-274): the windowed bf16
+    // kernel, or one GEMM per phase
     const int p = (U.k - U.u) / 2;
-    for (int phi = 0; phi < U.u; ++phi) {
+    const bool upsw = ups_window_ok(U, m->ups_window);
+    if (upsw) PD_TRY(launch_ups_window(U, XS, in_scale, B, Tin, XSRC, X, st));
+    for (int phi = 0; phi < (upsw ? 0 : U.u); ++phi) {
       const int q0 = U.qmin[phi];
       const int o = q0 * U.u + phi - p;        // first output row of this phase, in [0, u)
       GemmArgs a = make_gemm(B, Tin, U.cout, U.w[phi], U.ntap * U.kpad, U.b, X + (long long)o * U.cout,

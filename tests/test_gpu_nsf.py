@@ -82,11 +82,12 @@ def test_device_draws_deterministic_and_bounded():
     assert float((a[0].cpu() - torch.from_numpy(io["wav"][0])).abs().mean()) < 0.1
 
 
-@pytest.mark.parametrize("wconv,T,B", [(1, 24, 1), (0, 24, 1), (1, 37, 2)])
+@pytest.mark.parametrize("wconv,T,B", [(1, 24, 1), (0, 24, 1), (1, 37, 2), (1, 1, 3), (1, 70, 1)])
 def test_bf16_full_dims_vs_oracle(wconv, T, B):
-    """bf16 path (windowed MFMA ResBlock convs, or the implicit-GEMM engine with wconv=0) against
-    the fp64 oracle with the shared bf16 bar (tests/bf16_bar.py); T=37 leaves partial 128-row
-    tiles at every stage, B=2 checks utterances do not bleed into each other's windows."""
+    """bf16 path (windowed MFMA ResBlock convs and ConvTranspose upsamples, or the implicit-GEMM
+    engine with wconv=0) against the fp64 oracle with the shared bf16 bar (tests/bf16_bar.py);
+    T=37/70 leave partial tiles at every stage (the 512-channel upsample's 64-row input tiles
+    included), T=1 is all halo, B>1 checks utterances do not bleed into each other's windows."""
     h = dict(synth.NSF_DEFAULTS)
     g, p = _gen(h, 7)
     g.set_compute_dtype("bf16").set_options(wconv=wconv)
