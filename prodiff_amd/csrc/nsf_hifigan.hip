@@ -269,7 +269,10 @@ int launch_conv_small(const NsfConv& c, const float* in, float alpha, float scal
 // TM = 32 FM WM = 128 rows, TN = 32 FN WN output channels (grid.y covers C / TN),
 // grid.z = utterance.  LDS row stride C + 8 bf16: lanes r and r+1 of a b128 fragment read
 // sit 4 banks apart for every C used here, so a wave's fragment read is conflict-free.
-constexpr int NSF_PF = 4;   // weight-fragment prefetch depth (k-steps)
+// weight-fragment prefetch depth (k-steps).  Measured (r02, C5 B=8): ring 4 without a
+// sched_barrier 386 us for the 128-channel k=11 conv; pinning the ring with sched_barrier
+// raised VGPRs to 2 waves/SIMD and ran slower (459 us at depth 4, 486 us at depth 8).
+constexpr int NSF_PF = 4;
 
 template <int C, int FM, int FN, int WM, int WN, bool IN_BF, bool OUT_BF>
 __global__ __launch_bounds__(256) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
