@@ -159,31 +159,37 @@ TAG_KERNEL = {
     "fd_lvc_block_sub": "lvc_block_bf16_kernel<128, true, false, false, false, true>",
     "fd_kp_kernel": "kp_kernel_bf16_kernel",
     "wn_layer": "wn_layer_bf16_kernel",
+    "nsf_res": "nsf_wconv_kernel<",
 }
 
 
 def pmc_traffic(tag, path=None):
-    """HBM bytes per launch of `tag`'s kernel from the newest committed PMC summary
-    (profiles/rNN_vMM_traffic.json, written by tools/pmc_traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench command).  None if absent."""
+    """HBM bytes per launch of `tag`'s kernel(s) from the newest committed PMC summary that
+    holds them (profiles/rNN_vMM_traffic.json, written by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of the bench command).  A tag served by several
+    template instantiations (nsf_res) gets the launch-weighted mean.  None if absent."""
     import glob
     import re
+    sym = TAG_KERNEL.get(tag)
+    if sym is None:
+        return None, None
     if path is None:
         def ver(f):
-            m = re.search(r"r(\d+)_v(\d+)_traffic\.json$", f)
+            m = re.search(r"r(\d+)_v(\d+)[a-z0-9_]*_traffic\.json$", f)
             return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
-        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_v*_traffic.json")), key=ver)
-        if not files:
-            return None, None
-        path = files[-1]
-    sym = TAG_KERNEL.get(tag)
-    if sym is None or not os.path.exists(path):
-        return None, None
-    with open(path) as f:
-        kern = json.load(f)["kernels"]
-    for name, v in kern.items():
-        if sym in name:
-            return float(v["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_v*_traffic.json")), key=ver, reverse=True)
+    else:
+        files = [path]
+    for fpath in files:
+        if not os.path.exists(fpath):
+            continue
+        with open(fpath) as f:
+            kern = json.load(f)["kernels"]
+        hits = [v for name, v in kern.items() if sym in name]
+        if hits:
+            n = sum(v["launches"] for v in hits)
+            tb = sum(v["traffic_bytes_per_launch"] * v["launches"] for v in hits) / n
+            return float(tb), os.path.relpath(fpath, ROOT)
     return None, None
 
 

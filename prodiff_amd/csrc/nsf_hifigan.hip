@@ -269,19 +269,70 @@ int launch_conv_small(const NsfConv& c, const float* in, float alpha, float scal
 // TM = 32 FM WM = 128 rows, TN = 32 FN WN output channels (grid.y covers C / TN),
 // grid.z = utterance.  LDS row stride C + 8 bf16: lanes r and r+1 of a b128 fragment read
 // sit 4 banks apart for every C used here, so a wave's fragment read is conflict-free.
+// Stage rows [r0, r0 + W) of utterance b (zero outside [0, Tl)) of a time-major [B][Tl][C]
+// tensor into LDS as bf16 (row pitch lda), leaky_relu(alpha) * scale applied: the input window
+// of the windowed convs.  Each thread keeps NSF_WB 16-byte items in flight: all loads of a batch
+// are issued before any is converted (r02: C5 21.6 -> 21.0 ms/step).
+constexpr int NSF_WB = 4;
+template <int C, bool IN_BF>
+__device__ __forceinline__ void stage_window(const void* __restrict__ in, int b, int Tl, int r0, int W, float alpha,
+                                             float scale, __bf16* __restrict__ win, int lda, int tid) {
+  constexpr int C8 = C / 8;
+  const int nitems = W * C8;
+  for (int base = tid; base < nitems; base += 256 * NSF_WB) {
+    float f[NSF_WB][8];
+#pragma unroll
+    for (int u = 0; u < NSF_WB; ++u) {
+      const int i = base + 256 * u;
+      const int row = i / C8, c8 = i - row * C8;
+      const int t = r0 + row;
+      const bool ok = i < nitems && t >= 0 && t < Tl;
+      const long long e = ((long long)b * Tl + (ok ? t : 0)) * C + 8 * c8;
+      if constexpr (IN_BF) {
+        bf16x8 x;
+        if (ok) x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(in) + e);
+        else
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = (__bf16)0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[u][j] = (float)x[j];
+      } else {
+        float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+        if (ok) {
+          x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e);
+          x1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e + 4);
+        }
+        f[u][0] = x0.x; f[u][1] = x0.y; f[u][2] = x0.z; f[u][3] = x0.w;
+        f[u][4] = x1.x; f[u][5] = x1.y; f[u][6] = x1.z; f[u][7] = x1.w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NSF_WB; ++u) {
+      const int i = base + 256 * u;
+      if (i < nitems) {
+        const int row = i / C8, c8 = i - row * C8;
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[u][j] >= 0.f ? f[u][j] : alpha * f[u][j]) * scale);
+        *reinterpret_cast<bf16x8*>(win + row * lda + 8 * c8) = v;
+      }
+    }
+  }
+}
+
 // weight-fragment prefetch depth (k-steps).  Measured (r02, C5 B=8): ring 4 without a
 // sched_barrier 386 us for the 128-channel k=11 conv; pinning the ring with sched_barrier
 // raised VGPRs to 2 waves/SIMD and ran slower (459 us at depth 4, 486 us at depth 8).
 constexpr int NSF_PF = 4;
 
 template <int C, int FM, int FN, int WM, int WN, bool IN_BF, bool OUT_BF>
-__global__ __launch_bounds__(256) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
+__global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
                                                         int ldw, int kpad, const float* __restrict__ bias, int taps,
                                                         int dil, float alpha, float scale, int Tl,
                                                         const float* __restrict__ res, void* __restrict__ out,
                                                         int accum) {
   static_assert(WM * WN == 4, "4 waves");
-  constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN, LDA = C + 8, C8 = C / 8, KS = C / 16;
+  constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN, LDA = C + 8, KS = C / 16;
   static_assert(C % TN == 0, "channel tiling");
   extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -289,31 +340,9 @@ __global__ __launch_bounds__(256) void nsf_wconv_kernel(const void* __restrict__
   const int b = blockIdx.z, t0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
   const int pad = (taps - 1) * dil / 2;
   const int W = TM + (taps - 1) * dil;
-  // 1. the input window, 8 channels (16 B of bf16) per item
-  for (int i = tid; i < W * C8; i += 256) {
-    const int row = i / C8, c8 = i - row * C8;
-    const int t = t0 - pad + row;
-    bf16x8 v;
-    if (t >= 0 && t < Tl) {
-      float f[8];
-      const long long e = ((long long)b * Tl + t) * C + 8 * c8;
-      if constexpr (IN_BF) {
-        const bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(in) + e);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = (float)x[j];
-      } else {
-        const float4 x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e);
-        const float4 x1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e + 4);
-        f[0] = x0.x; f[1] = x0.y; f[2] = x0.z; f[3] = x0.w; f[4] = x1.x; f[5] = x1.y; f[6] = x1.z; f[7] = x1.w;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[j] >= 0.f ? f[j] : alpha * f[j]) * scale);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-    }
-    *reinterpret_cast<bf16x8*>(nsf_win + row * LDA + 8 * c8) = v;
-  }
+  // 1. the input window, 8 channels (16 B of bf16) per item, NSF_WB items per thread in flight
+  //    together (a load-convert-store loop waits one HBM round trip per item)
+  stage_window<C, IN_BF>(in, b, Tl, t0 - pad, W, alpha, scale, nsf_win, LDA, tid);
   __syncthreads();
   // 2. taps x 16-deep k-steps; B fragments prefetched one step ahead
   const int r32 = lane & 31, h = lane >> 5;
@@ -360,44 +389,40 @@ __global__ __launch_bounds__(256) void nsf_wconv_kernel(const void* __restrict__
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bq[q][j], acc[i][j], 0, 0, 0);
     }
   }
-  // 3. epilogue: + bias (+ res), C/D map col = lane&31, row = (reg&3) + 8(reg>>2) + 4(lane>>5).
-  // Branch-free loads (rows past the end clamp to the last row), so the residual reads of one
-  // M fragment are all in flight together; only the stores are predicated.
-  float bv[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) bv[j] = bias[n0 + (wn * FN + j) * 32 + r32];
-  const long long rowb = (long long)b * Tl;
+  // 3. epilogue: + bias (+ res) (+ out when accumulating), C/D map col = lane&31,
+  // row = (reg&3) + 8(reg>>2) + 4(lane>>5).  Per (M, N) fragment: all 16 residual loads in
+  // flight together (rows past the end clamp to the last row), then predicated stores.
+  // 32-bit element offsets (the host checks B*Tl*C < 2^31) keep one VGPR per address
+  const int rowb = b * Tl;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    float rv[16][FN];
-    if (res) {
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int t = min(t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tl - 1);
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + (wn * FN + j) * 32 + r32;
+      const float bn = bias[n];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const long long o = (rowb + t) * C + n0 + (wn * FN + j) * 32 + r32;
-          rv[reg][j] = res[o];
+      for (int hb = 0; hb < 16; hb += 8) {   // two batches of 8 rows: fewer live registers
+        float rv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int reg = hb + q;
+          const int t = min(t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tl - 1);
+          const int o = (rowb + t) * C + n;
+          float v = res ? res[o] : 0.f;
           if constexpr (!OUT_BF)
-            if (accum) rv[reg][j] += reinterpret_cast<const float*>(out)[o];
+            if (accum) v += reinterpret_cast<const float*>(out)[o];
+          rv[q] = v;
         }
-      }
-    } else {
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) rv[reg][j] = 0.f;
-    }
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int t = t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const long long o = (rowb + t) * C + n0 + (wn * FN + j) * 32 + r32;
-        const float v = acc[i][j][reg] + bv[j] + rv[reg][j];
-        if (t < Tl) {
-          if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
-          else reinterpret_cast<float*>(out)[o] = v;
+        for (int q = 0; q < 8; ++q) {
+          const int reg = hb + q;
+          const int t = t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          const int o = (rowb + t) * C + n;
+          const float v = acc[i][j][reg] + bn + rv[q];
+          if (t < Tl) {
+            if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
+            else reinterpret_cast<float*>(out)[o] = v;
+          }
         }
       }
     }
@@ -572,30 +597,14 @@ __global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict
                                                       float scale, int Tin, const float* __restrict__ res,
                                                       float* __restrict__ out) {
   static_assert(WM * WN == 4, "4 waves");
-  constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN, LDA = CIN + 8, C8 = CIN / 8, KS = CIN / 16;
+  constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN, LDA = CIN + 8, KS = CIN / 16;
   constexpr int PF = KS >= NSF_PF ? NSF_PF : KS;
   extern __shared__ __attribute__((aligned(16))) __bf16 nsf_uwin[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int b = blockIdx.z, i0 = blockIdx.x * TQ, n0 = blockIdx.y * TN;
   const int W = TQ + ntap;                 // rows i0 + dlo ... (dlo = 1 - ntap, top offset q0 <= 1)
-  for (int i = tid; i < W * C8; i += 256) {
-    const int row = i / C8, c8 = i - row * C8;
-    const int q = i0 + dlo + row;
-    bf16x8 v;
-    if (q >= 0 && q < Tin) {
-      const float* src = in + ((long long)b * Tin + q) * CIN + 8 * c8;
-      const float4 x0 = *reinterpret_cast<const float4*>(src);
-      const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
-      const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[j] >= 0.f ? f[j] : alpha * f[j]) * scale);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-    }
-    *reinterpret_cast<bf16x8*>(nsf_uwin + row * LDA + 8 * c8) = v;
-  }
+  stage_window<CIN, false>(in, b, Tin, i0 + dlo, W, alpha, scale, nsf_uwin, LDA, tid);
   __syncthreads();
   const int r32 = lane & 31, h = lane >> 5;
   const int ldw = ntap * kpad;
@@ -763,6 +772,10 @@ bool wconv_ok(const NsfConv& c) {
 int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, float scale, int B, int Tl, void* out,
                  bool out_bf, const float* res, hipStream_t st, int accum = 0) {
   const __bf16* wb = lookup_bf16(c.w);
+  if ((long long)B * Tl * c.cout >= (1ll << 31)) {
+    set_error("nsf wconv: B * T * C >= 2^31 elements (32-bit epilogue offsets)");
+    return PD_ERR_UNSUPPORTED;
+  }
   switch (c.cout) {
     case 256: return launch_wconv_c<256, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
     case 128: return launch_wconv_c<128, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
