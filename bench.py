@@ -272,7 +272,8 @@ def ref_cpu_baseline(config):
         return None
     return {"value": e["mel_frames_per_s"], "unit": "mel-frames/s", "cores": d["threads"], "kind": "reference",
             "sample": e["sample"], "rtf": e.get("rtf"), "host": d["host"],
-            "timing": f"median of {d['repeats']} after 1 warm-up, fp32, torch.no_grad", "source": os.path.relpath(path, ROOT)}
+            "timing": f"median of {e.get('repeats', d['repeats'])} after 1 warm-up, fp32, torch.no_grad",
+            "source": os.path.relpath(path, ROOT)}
 
 
 def port_cpu_baseline(frames, vocoder=True):

@@ -131,7 +131,7 @@ def main():
 
     med, ts = timed(c3, args.repeats)
     audio = B * T * HOP / SR
-    res["C3"] = {"mel_frames_per_s": round(B * T / med, 2), "seconds_median": round(med, 3),
+    res["C3"] = {"mel_frames_per_s": round(B * T / med, 2), "seconds_median": round(med, 3), "repeats": args.repeats,
                  "seconds_all": [round(t, 3) for t in ts], "rtf": round(med / audio, 4),
                  "x_realtime": round(audio / med, 3),
                  "prodiff_s_median": round(float(np.median(split["prodiff"][1:])), 3),
@@ -143,7 +143,7 @@ def main():
     # C2: ProDiff 2-iter, B=1, T=1000
     cond2 = torch.from_numpy(synth.synth_inputs(0, (1, 1000, 256)))
     med2, ts2 = timed(torch.no_grad()(lambda: gd(cond2, infer=True)), args.repeats)
-    res["C2"] = {"mel_frames_per_s": round(1000 / med2, 2), "seconds_median": round(med2, 4),
+    res["C2"] = {"mel_frames_per_s": round(1000 / med2, 2), "seconds_median": round(med2, 4), "repeats": args.repeats,
                  "seconds_all": [round(t, 4) for t in ts2], "rtf": round(med2 / (1000 * 512 / 44100), 4),
                  "sample": "reference modules, ProDiff 2-iter, B=1 x 1000 frames, M=80, fp32, mel only"}
     print("C2", res["C2"], flush=True)
@@ -191,7 +191,7 @@ def bench_c5(repeats, B=2, T=861, tokens=120):
 
     med, ts = timed(c5, repeats)
     audio = B * T * 512 / 44100
-    return {"mel_frames_per_s": round(B * T / med, 2), "seconds_median": round(med, 3),
+    return {"mel_frames_per_s": round(B * T / med, 2), "seconds_median": round(med, 3), "repeats": repeats,
             "seconds_all": [round(x, 3) for x in ts], "rtf": round(med / audio, 4), "x_realtime": round(audio / med, 3),
             "teacher_s_median": round(float(np.median(split["teacher"][1:])), 3),
             "nsf_s_median": round(float(np.median(split["nsf"][1:])), 3),
