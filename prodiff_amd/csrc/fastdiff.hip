@@ -1513,10 +1513,16 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   const int b = blockIdx.y, i0 = blockIdx.x * DB_TS, ib = i0 - 7;
   const long long Lin = (long long)Lout * f;
   const float* src = in + (long long)b * Lin * CI;
-  for (int i = tid; i < DB_ROWS * 8; i += 256) {
+  // staging: every thread's (<= DB_NI) items are loaded before any is converted, so their
+  // strided HBM reads are in flight together (one round trip per block, not one per item)
+  constexpr int DB_NI = (DB_ROWS * 8 + 255) / 256;
+  float4 sv[DB_NI];
+#pragma unroll
+  for (int u = 0; u < DB_NI; ++u) {
+    const int i = tid + 256 * u;
     const int p = i >> 3, q = (i & 7) * 4, ii = ib + p;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p < DB_TS + 14 && ii >= 0 && ii < Lout) {
+    if (i < DB_ROWS * 8 && p < DB_TS + 14 && ii >= 0 && ii < Lout) {
       if (audio) {   // input = first_conv(audio) (FastDiff_model.py:90), recomputed: no a0 tensor
         const long long t = (long long)ii * f;
         const float* au = audio + (long long)b * Lin;
@@ -1535,6 +1541,14 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
         v = *reinterpret_cast<const float4*>(src + (long long)ii * f * CI + q);
       }
     }
+    sv[u] = v;
+  }
+#pragma unroll
+  for (int u = 0; u < DB_NI; ++u) {
+    const int i = tid + 256 * u;
+    if (i >= DB_ROWS * 8) continue;
+    const int p = i >> 3, q = (i & 7) * 4;
+    float4 v = sv[u];
     *reinterpret_cast<bf16x4*>(&R0[p * DB_LD + q]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
     v.x = v.x >= 0.f ? v.x : 0.2f * v.x; v.y = v.y >= 0.f ? v.y : 0.2f * v.y;
     v.z = v.z >= 0.f ? v.z : 0.2f * v.z; v.w = v.w >= 0.f ? v.w : 0.2f * v.w;
