@@ -135,3 +135,27 @@ def test_c3_full_bf16_vs_fp32():
     wav32 = fastdiff(1).sample(mel32, b, a, s, st, x_T=wT, noise=wn).cpu().numpy()
     wav16 = fastdiff(1, "bf16").sample(mel32, b, a, s, st, x_T=wT, noise=wn).cpu().numpy()
     assert_bf16_close(wav16, wav32, "C3 FastDiff bf16 vs fp32, B=8x861")
+
+
+def test_c5_full_bf16_vs_fp32():
+    """C5 at full utterance length (2 SVS segments x 861 frames, 120 phonemes each): the bf16
+    pipeline (condition encoder, ProDiff 4-iter M=128, NSF-HiFiGAN on the windowed MFMA convs)
+    against the exact fp32 pipeline with the same weights and the same on-device draws
+    (Philox, keyed by seed and element index: identical in both dtypes).  The fp32 path is
+    pinned to the reference goldens; the bar is the shared bf16 output bar."""
+    from prodiff_amd import synth
+    from prodiff_amd.pipeline import SVS_VOCAB, SvsSynthesizer
+    from tests.bf16_bar import assert_bf16_close
+    dev = torch.device("cuda")
+    utts = [{k: torch.from_numpy(v).to(dev) for k, v in synth.synth_svs_utterance(100 + i, 861, 120, SVS_VOCAB).items()}
+            for i in range(2)]
+    batch = SvsSynthesizer.collate(utts)
+    outs = {}
+    for dt in ("fp32", "bf16"):
+        syn = SvsSynthesizer.synthetic(dev, seed=0, dtype=dt)
+        mel, wav = syn(batch, seed=11)
+        outs[dt] = (mel.cpu().numpy(), wav.cpu().numpy())
+        del syn
+    assert np.isfinite(outs["fp32"][1]).all() and np.abs(outs["fp32"][1]).max() <= 1.0
+    assert_bf16_close(outs["bf16"][0], outs["fp32"][0], "C5 mel bf16 vs fp32, 2x861")
+    assert_bf16_close(outs["bf16"][1], outs["fp32"][1], "C5 wav bf16 vs fp32, 2x861")

@@ -123,3 +123,59 @@ def test_bench_self_launches_n_ranks_dry_run():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["dry_run"] is True
     assert d["config"]["global_batch"] == 2 * d["config"]["per_gpu_batch"]
+
+
+class StubSvs:
+    """Per-utterance dict inputs like SvsSynthesizer's (phoneme tokens + frame features),
+    batched by the real SvsSynthesizer.collate; output independent of the batch."""
+    from prodiff_amd.pipeline import SvsSynthesizer as _S
+    collate = staticmethod(_S.collate)
+
+    def __call__(self, batch, seed):
+        n = torch.tensor(batch["ntok"], dtype=torch.float32)[:, None]
+        tok_sum = batch["txt_tokens"].float().sum(1, keepdim=True)        # pads are 0: neutral
+        mel = batch["f0"][..., None].repeat(1, 1, M) + tok_sum[..., None] + n[..., None]
+        wav = torch.repeat_interleave(batch["f0"], HOP, dim=1) - batch["voicing"].sum(1, keepdim=True)
+        return mel, wav
+
+
+def _svs_items(lengths, ntoks):
+    g = torch.Generator().manual_seed(99)
+    return [dict(txt_tokens=torch.randint(1, 50, (n,), generator=g), mel2ph=torch.zeros(T, dtype=torch.long),
+                 f0=torch.rand(T, generator=g) * 500, voicing=torch.randn(T, generator=g),
+                 spk_mix_embed=torch.randn(1, 8, generator=g))
+            for T, n in zip(lengths, ntoks)]
+
+
+def _svs_worker(rank, world, port, q, lengths, ntoks):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        items = _svs_items(lengths, ntoks)
+        mels, wavs = distributed_synthesize(StubSvs(), [(T, (lambda it=it: it)) for T, it in zip(lengths, items)],
+                                            hop=HOP)
+        if rank == 0:
+            q.put(([m.numpy() for m in mels], [w.numpy() for w in wavs]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_synthesize_svs_collate():
+    """C5's path at world size 2: dict items with ragged phoneme counts (padded by
+    SvsSynthesizer.collate) sharded and gathered back in input order."""
+    lengths, ntoks = [6, 9, 6, 4, 9], [3, 5, 2, 4, 5]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_svs_worker, args=(r, 2, port, q, lengths, ntoks)) for r in range(2)]
+    for p in procs:
+        p.start()
+    mels, wavs = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for i, it in enumerate(_svs_items(lengths, ntoks)):
+        em, ew = StubSvs()(StubSvs.collate([it]), 0)
+        np.testing.assert_allclose(mels[i], em[0].numpy(), rtol=0, atol=1e-4)
+        np.testing.assert_allclose(wavs[i], ew[0].numpy(), rtol=0, atol=1e-4)
