@@ -1701,18 +1701,24 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   for (int j = 0; j < 6; ++j) {
     const __bf16* In = Hb[j == 0 ? 0 : (j & 1 ? 1 : 2)];
     __bf16* Out = Hb[j & 1 ? 2 : 1];
+    // a wave's jobs (wave, wave + 4) share the column tile nt = wave & 1: its 12 weight fragments
+    // are loaded once per stage, all in flight together, and reused by both jobs
+    bf16x8 bwf[12];
+    {
+      const __bf16* wrow = A.Wr[nblk][j] + ((wave & 1) * 32 + r32) * 192 + h * 8;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) bwf[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+    }
     for (int job = wave, q = 0; job < 6; job += 4, ++q) {
       const int mt = job >> 1, nt = job & 1;
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const __bf16* wrow = A.Wr[nblk][j] + (nt * 32 + r32) * 192 + h * 8;
 #pragma unroll
       for (int kk = 0; kk < 12; ++kk) {
         const int tap = kk >> 2, kc = kk & 3;
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(In + (mt * 32 + r32 + tap) * LDH + kc * 16 + h * 8);
-        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bwf[kk], acc, 0, 0, 0);
       }
       const int n = nt * 32 + r32;
       const float bias = A.br[nblk][j][n];
@@ -1729,19 +1735,24 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
     }
     __syncthreads();
   }
-  // bias_conv on the 64 output frames: 2 row tiles x 8 column tiles
-  for (int job = wave; job < 16; job += 4) {
-    const int mt = job >> 3, nt = job & 7;
+  bf16x8 bwb[12];
+  // bias_conv on the 64 output frames: 2 row tiles x 8 column tiles; wave w owns column tiles
+  // 2w and 2w+1 (weights loaded once per tile, reused by both row tiles)
+  for (int job = 0; job < 4; ++job) {
+    const int nt = 2 * wave + (job >> 1), mt = job & 1;
+    if (mt == 0) {
+      const __bf16* wrow = A.Wb[nblk] + (nt * 32 + r32) * 192 + h * 8;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) bwb[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+    }
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const __bf16* wrow = A.Wb[nblk] + (nt * 32 + r32) * 192 + h * 8;
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk) {
       const int tap = kk >> 2, kc = kk & 3;
       const bf16x8 af = *reinterpret_cast<const bf16x8*>(Hb[2] + (16 + mt * 32 + r32 + tap) * LDH + kc * 16 + h * 8);
-      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bwb[kk], acc, 0, 0, 0);
     }
     const int n = nt * 32 + r32;
     const float bias = A.bb[nblk][n];
