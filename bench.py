@@ -80,7 +80,7 @@ def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256):
         "wn_gate": 2 * F * 2 * C * (3 * C + H),
         "wn_resskip": 2 * F * 2 * C * C,
         "wn_layer": 2 * F * 2 * C * (3 * C + H) + 2 * F * 2 * C * C,     # fused gate + res/skip (bf16)
-        "wn_gate2": 2 * F * 2 * C * (3 * C + H),                            # two-GEMM layer (bf16)
+        "wn_gate2": 2 * F * 2 * C * (3 * C + H),                            # two-kernel layer (bf16)
         "wn_resskip2": 2 * F * 2 * C * C * 39 / 40,                          # last of 20 layers: skip half only
         "wn_skiphead": 2 * F * C * C,
         "wn_outproj_posterior": 2 * F * M * C,
@@ -131,6 +131,8 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         # g in; x read + written, skip read + written (fp32), xa' written
         "wn_resskip2": F * (C * 2 + C * 4 * 2 + C * 4 * 2 + C * 2) + 2 * C * C * wb,
         "wn_skiphead": F * 2 * C * 4 + C * C * wb,
+        # two-kernel layer path, once per denoiser call: x + dp and cond (fp32) -> bf16 copies
+        "wn_xa": F * (C + H) * (4 + 2),
         "wn_outproj_posterior": F * (C + 3 * M) * 4 + M * C * wb,
         "fd_first_conv": F * 256 * (1 + 32) * 4,
         # fused DBlock: strided input rows (32 ch) read once + output written once
@@ -159,6 +161,8 @@ TAG_KERNEL = {
     "fd_lvc_block_sub": "lvc_block_bf16_kernel<128, true, false, false, false, true>",
     "fd_kp_kernel": "kp_kernel_bf16_kernel",
     "wn_layer": "wn_layer_bf16_kernel",
+    "wn_gate2": "wn_gate_bf16_kernel",
+    "wn_resskip2": "wn_resskip_bf16_kernel",
     "nsf_res": "nsf_wconv_kernel<",
 }
 

@@ -84,9 +84,10 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
 void pd_wavenet_destroy(pd_wavenet* h);
 /* Kernel-variant option of a handle; set before its first call.  PD_WN_OPT_LAYER selects the
  * bf16 residual-layer implementation: 0 the fused kernel with 32-frame blocks, 3 the fused
- * kernel with 64-frame blocks, 2 (default) 64-frame blocks when they still give every CU a
- * block (B*T >= 16384 frames) else 32, 1 two GEMM launches per layer with 128 x 128 tiles
- * (DESIGN.md §4). */
+ * kernel with 64-frame blocks, 1 two launches per layer (GATE: 128 frames x 64 gated channels
+ * per block, activation window staged once; RESSKIP: 64 frames x 128 outputs), 2 (default)
+ * 64-frame fused blocks when they still give every CU a block (B*T >= 16384 frames) else 32.
+ * DESIGN.md §4 has the measurements. */
 #define PD_WN_OPT_LAYER 0
 /* PD_WN_OPT_KSPLIT (fp32 path): the residual-layer GEMMs split their K range over several blocks
  * until the grid holds 512 (default) or 256 blocks; 0 = never split. */

@@ -30,8 +30,9 @@ struct pd_wavenet {
   __bf16* frag = nullptr;
   __bf16* W1f = nullptr;   // [L][2C/32 tiles][K/16 steps][64 lanes][8]
   __bf16* W2f = nullptr;
+  __bf16* W1p = nullptr;   // [L][C/16 pair tiles][K/16][64][8] (wn_gate_bf16_kernel)
   // bf16 residual layer (PD_WN_OPT_LAYER): 0 = fused kernel, 32 frames per block; 3 = fused, 64
-  // frames per block; 2 = auto between the two by grid size; 1 = two 128x128-tile GEMMs
+  // frames per block; 1 = GATE + RESSKIP kernels; 2 = auto between 0 and 3 by grid size
   int layer_mode = 2;
   int ksplit_blocks = 512;   // PD_WN_OPT_KSPLIT: fp32 layer GEMMs split K up to this many blocks
 };
@@ -229,153 +230,311 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
     }
 }
 
-// ------------------------------------------------------------------ two-GEMM residual layer (bf16)
-// The same layer as wn_layer_bf16_kernel as two launches with 128 x 128 tiles
-// (wavenet.py:60-72):
+// ------------------------------------------------------------------ two-kernel residual layer (bf16)
+// The same layer as wn_layer_bf16_kernel as two launches (wavenet.py:60-72), PD_WN_OPT_LAYER = 1:
 //   GATE     g = sigmoid(W1_g . a + b_g) * tanh(W1_f . a + b_f),  a = [xa(t-d); xa(t); xa(t+d); cond(t)]
 //   RESSKIP  o = W2 . g + b2;  x = (x + o[:C]) / sqrt2 (and xa' = bf16(x + dp of the next layer));
 //            skip (+)= o[C:]
-// The fused kernel holds 32 frames and streams all 1.3 MB of a layer's weights through
-// every block, so it is bound by the L2 -> CU port (about 64 B/clk/CU; its MFMA needs four
-// times that).  Here a block reuses each 128-row weight tile for 128 frames (A = weights
-// staged in LDS, B = activations; both k-contiguous, double-buffered 64-k stages): about as
-// many bytes per MFMA as the port delivers.  The activations the GATE GEMM reads are bf16
-// copies kept beside the fp32 state: xa = bf16(x + dp_l) (written by the previous RESSKIP
-// epilogue, which knows dp_{l+1}) and condb = bf16(cond) (once per call).  x and skip stay fp32.
-// GATE block (bx, cg): frames [128 bx, +128), gate channels [64 cg, +64) and their filter
-// channels; RESSKIP block (bx, nt): output channels [128 nt, +128) (nt < C/128: residual).
-constexpr int WG_BM = 128, WG_BN = 128, WG_KC = 64, WG_LD = 72;
-enum { WG_GATE = 0, WG_RESSKIP = 1 };
+// Why it exists: the fused kernel holds 32 frames per block and streams all 1.3 MB of a layer's
+// weights through every block, so the L2 -> CU port (~60 GB/s per CU measured) bounds it at
+// ~22 us per layer at B*T = 6888.  A GATE block holds 128 frames x 64 gated channels: its
+// activation window (the frames' x rows with a dilation halo, and their cond rows) is staged in
+// LDS once for all K = 3C + H (the three taps are row-shifted reads of one window), and each
+// weight byte is read once per block: ~390 KB per block instead of 1.3 MB per 32 frames.
+// Why it is not the default: each launch pays its own load round trip and drain (~5 us at any
+// batch on MI355X), so the pair measured 12.6 + 16.6 us vs 22.2 us fused at B = 8 and 42 + 44 vs
+// ~87 us at B = 32.
+// The activations are bf16 copies kept beside the fp32 state: xa = bf16(x + dp_l) (written by
+// the previous RESSKIP epilogue, which knows dp_{l+1}) and condb = bf16(cond); x and skip stay
+// fp32 -- the same roundings as the fused kernel's LDS staging.
+//
+// GATE weight tiles pair the halves: pair tile p holds rows 16p..16p+15 of the gate half, then
+// the same 16 channels of the filter half, so in the transposed 32x32 C layout (lane = frame,
+// registers = weight rows (r&3) + 8(r>>2) + 4h) register r < 8 holds a gate channel and
+// register r + 8 its filter channel: the gate needs no data movement.
+constexpr int WG2_ROWS = 128;   // GATE frames per block
+constexpr int WG2_LD = 264;     // bf16 per LDS row: 512 B + 16 B (conflict-free b128 fragment reads)
+constexpr int WN_RS_RQ = 2;     // RESSKIP frame tiles (32 frames each) per block
 
-struct WnGemmArgs {
-  const __bf16* W;       // [N][ldw] bf16 weights (rows = output channels, k contiguous)
-  int ldw, K;
-  const float* bias;     // [N]
-  const __bf16* xa;      // GATE: [rows][C] bf16(x + dp_l)
-  const __bf16* condb;   // GATE: [rows][H] bf16(cond)
-  __bf16* g;             // GATE: out / RESSKIP: in, [rows][C] bf16
-  float* x;              // RESSKIP: [rows][C] fp32 residual state, updated in place
-  float* skip;           // RESSKIP: [rows][C] fp32
-  __bf16* xa_next;       // RESSKIP: [rows][C] bf16(x + dp_{l+1}) or null (last layer)
-  const float* dp_next;  // RESSKIP: dp_{l+1}[b * dp_ld + c]
-  int dp_ld, first, nt0;
-  int B, T, C, H, dil;
+// XCD-aware block order for (row group, column) grids: the hardware deals consecutive block ids
+// round-robin over the 8 XCDs; remap so each XCD walks a contiguous run of logical blocks, column
+// fastest, and the column blocks of one row group -- which read the same activation rows -- share
+// one XCD's L2.
+__device__ __forceinline__ void wn_xcd_block(int& bx, int& by) {
+  const int total = gridDim.x * gridDim.y, id = blockIdx.y * gridDim.x + blockIdx.x;
+  const int xcd = id & 7, slot = id >> 3, per = total >> 3, rem = total & 7;
+  const int logical = xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
+  bx = logical / gridDim.y;
+  by = logical - bx * gridDim.y;
+}
+
+// dst[((p*KS + ks)*64 + lane)*8 + j] = bf16(src[row(p, lane%32) * ld + ks*16 + (lane/32)*8 + j]),
+// row(p, i) = i < 16 ? 16p + i : C + 16p + i - 16
+__global__ void pack_frag_pair_kernel(__bf16* dst, const float* src, int C, int K, int ld) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)2 * C * K) return;
+  const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
+  const long long rest = i >> 9;
+  const int KS = K / 16, ks = (int)(rest % KS), p = (int)(rest / KS);
+  const int r = lane & 31, row = r < 16 ? 16 * p + r : C + 16 * p + r - 16;
+  dst[i] = (__bf16)src[(long long)row * ld + ks * 16 + (lane >> 5) * 8 + j];
+}
+
+struct WnGateArgs {
+  const __bf16* xa;      // [rows][C] bf16(x + dp_l)
+  const __bf16* condb;   // [rows][H] bf16(cond)
+  const __bf16* Wp;      // [C/16 pair tiles][K1/16][64][8]
+  const float* b1;       // [2C] (dilated-conv + conditioner biases)
+  __bf16* g;             // [rows][C] gated output
+  int rows, T, dil;
 };
 
-template <int MODE>
-__global__ __launch_bounds__(512, 2) void wn_gemm_bf16_kernel(const WnGemmArgs P) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][WG_BN * WG_LD];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][WG_BM * WG_LD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n32 = lane & 31, h = lane >> 5;
-  const int wm = wave & 3, wn = wave >> 2;
-  const int C = P.C, T = P.T, rows = P.B * P.T, R0 = blockIdx.x * WG_BM;
-  const int cg = blockIdx.y;                          // GATE: channel group; RESSKIP: output tile
-  // weight row of LDS A row i
-  auto wrow = [&](int i) {
-    if (MODE == WG_GATE) return i < 64 ? 64 * cg + i : C + 64 * cg + (i - 64);
-    return WG_BN * (cg + P.nt0) + i;
-  };
-  // this thread's two 16-B pieces of a stage: piece p -> row p >> 3, k offset (p & 7) * 8
-  uint4 ra[2], rb[2];
-  auto load = [&](int kc) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = tid + 512 * q, row = p >> 3, kk = kc * WG_KC + (p & 7) * 8;
-      ra[q] = *reinterpret_cast<const uint4*>(P.W + (long long)wrow(row) * P.ldw + kk);
-      const int R = R0 + row;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (R < rows) {
-        if (MODE == WG_GATE) {
-          const int b = R / T, t = R - b * T;
-          if (kk < 3 * C) {
-            const int tap = kk / C, c = kk - tap * C, tt = t + (tap - 1) * P.dil;
-            if (tt >= 0 && tt < T) v = *reinterpret_cast<const uint4*>(P.xa + ((long long)b * T + tt) * C + c);
-          } else {
-            v = *reinterpret_cast<const uint4*>(P.condb + (long long)R * P.H + (kk - 3 * C));
-          }
-        } else {
-          v = *reinterpret_cast<const uint4*>(P.g + (long long)R * C + kk);
-        }
-      }
-      rb[q] = v;
+// B fragment (frames 32q + n, k-step ks) of the GATE input: ks < 48 the x window at tap ks / 16,
+// else the cond rows.  EDGE: taps outside the frame's utterance read as zero (select: staged rows
+// of the neighbouring utterance, or clamped rows, are never multiplied in).
+template <int DW, bool EDGE>
+__device__ __forceinline__ bf16x8 wn_gate_bfrag(const __bf16* Xs, const __bf16* Cs, int ks, int q, int n, int h,
+                                                int d, const bool (&inv0)[4], const bool (&inv2)[4]) {
+  if (ks < 48) {
+    const int tap = ks >> 4;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(&Xs[(32 * q + n + DW + (tap - 1) * d) * WG2_LD + (ks & 15) * 16 + 8 * h]);
+    if (EDGE && tap != 1) {
+      const bf16x8 z = {};
+      v = (tap == 0 ? inv0[q] : inv2[q]) ? z : v;
     }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = tid + 512 * q, row = p >> 3, col = (p & 7) * 8;
-      *reinterpret_cast<uint4*>(&As[buf][row * WG_LD + col]) = ra[q];
-      *reinterpret_cast<uint4*>(&Bs[buf][row * WG_LD + col]) = rb[q];
-    }
-  };
-  // wave (wm, wn): frames 32 wm.., weight tiles t0 = LDS rows [32 wn, +32) and t1 = [64 + 32 wn, +32)
-  // (GATE: the gate and the filter half of the same 32 channels) or [64 wn, +32), [64 wn + 32, +32)
-  const int t0 = MODE == WG_GATE ? 32 * wn : 64 * wn, t1 = MODE == WG_GATE ? 64 + 32 * wn : 64 * wn + 32;
-  f32x16 acc0, acc1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
-  const int NKC = P.K / WG_KC;
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int kc = 0; kc < NKC; ++kc) {
-    const int buf = kc & 1;
-    if (kc + 1 < NKC) load(kc + 1);
-#pragma unroll
-    for (int ks = 0; ks < WG_KC / 16; ++ks) {
-      const bf16x8 bx = *reinterpret_cast<const bf16x8*>(&Bs[buf][(32 * wm + n32) * WG_LD + ks * 16 + 8 * h]);
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&As[buf][(t0 + n32) * WG_LD + ks * 16 + 8 * h]);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&As[buf][(t1 + n32) * WG_LD + ks * 16 + 8 * h]);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bx, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bx, acc1, 0, 0, 0);
-    }
-    if (kc + 1 < NKC) store(buf ^ 1);
-    __syncthreads();
+    return v;
   }
-  // C[n][m]: lane (frame m = 32 wm + n32, h) holds weight rows (reg&3) + 8(reg>>2) + 4h of each tile
-  const int R = R0 + 32 * wm + n32;
-  if (R >= rows) return;
-  if (MODE == WG_GATE) {
-    const int ch0 = 64 * cg + 32 * wn;
+  return *reinterpret_cast<const bf16x8*>(&Cs[(32 * q + n) * WG2_LD + (ks - 48) * 16 + 8 * h]);
+}
+
+// K loop of one GATE wave over k-steps [K0, K0 + 32): 4 frame tiles (128 frames) x one pair tile.
+// The next k-step's B fragments are read from LDS before this step's MFMAs, and the weight ring
+// refills WD steps ahead (sched_barrier keeps both where they are: the scheduler sinks loads to
+// their first use).
+template <int DW, int WD, int K0, bool EDGE>
+__device__ __forceinline__ void wn_gate_kloop(f32x16 (&acc)[4], bf16x8 (&rw)[WD], const bf16x8* wp,
+                                              const __bf16* Xs, const __bf16* Cs, int n, int h, int d,
+                                              const bool (&inv0)[4], const bool (&inv2)[4]) {
+  constexpr int NK = 32;
+  bf16x8 b[2][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = ch0 + 8 * i + 4 * h;
-      const float4 bg = *reinterpret_cast<const float4*>(P.bias + c);
-      const float4 bf = *reinterpret_cast<const float4*>(P.bias + C + c);
-      *reinterpret_cast<bf16x4*>(P.g + (long long)R * C + c) =
-          bf16x4{(__bf16)gate_fast(acc0[4 * i] + bg.x, acc1[4 * i] + bf.x),
-                 (__bf16)gate_fast(acc0[4 * i + 1] + bg.y, acc1[4 * i + 1] + bf.y),
-                 (__bf16)gate_fast(acc0[4 * i + 2] + bg.z, acc1[4 * i + 2] + bf.z),
-                 (__bf16)gate_fast(acc0[4 * i + 3] + bg.w, acc1[4 * i + 3] + bf.w)};
+  for (int q = 0; q < 4; ++q) b[0][q] = wn_gate_bfrag<DW, EDGE>(Xs, Cs, K0, q, n, h, d, inv0, inv2);
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const bf16x8 w = rw[i % WD];
+    if (i + WD < NK) rw[i % WD] = wp[(K0 + i + WD) * 64];
+    if (i + 1 < NK) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[(i + 1) & 1][q] = wn_gate_bfrag<DW, EDGE>(Xs, Cs, K0 + i + 1, q, n, h, d, inv0, inv2);
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, b[i & 1][q], acc[q], 0, 0, 0);
+  }
+}
+
+// GATE block (bx, by): frames [128 bx, +128), gated channels [64 by, +64) = pair tiles 4 by + w.
+// 8 waves: wave w < 4 runs k-steps [0, 32) of pair tile 4 by + w (taps t-d, t), wave w + 4 the
+// k-steps [32, 64) (tap t+d and cond) of the same tile, so a SIMD hosts two waves and each weight
+// byte is still read once per block; the halves meet through LDS at the end and each wave of
+// the pair finalises two of the four frame tiles.  Requires C = H = 256 and dil <= DW.
+template <int DW>
+__global__ __launch_bounds__(512, 1) void wn_gate_bf16_kernel(const WnGateArgs P) {
+  constexpr int C = 256, KS = 64, XR = WG2_ROWS + 2 * DW, WD = 12;
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[XR * WG2_LD];          // frames R0 - DW + i
+  __shared__ __attribute__((aligned(16))) __bf16 Cs[WG2_ROWS * WG2_LD];    // frames R0 + i
+  static_assert(XR * WG2_LD * 2 >= 4 * 2 * 2 * 16 * 64 * 4, "partial-sum exchange reuses the x window");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, h = lane >> 5;
+  int bx, by;
+  wn_xcd_block(bx, by);
+  const int R0 = bx * WG2_ROWS, d = P.dil, rows = P.rows;
+  const int pw = wave & 3, half = wave >> 2, p = by * 4 + pw;
+  const bf16x8* wp = reinterpret_cast<const bf16x8*>(P.Wp) + (long long)p * KS * 64 + lane;
+  // staging: 32 16-B pieces per row; unconditional loads at clamped rows, masked at the store
+  constexpr int NX = XR * 32, IX = (NX + 511) / 512, IC = WG2_ROWS * 32 / 512;
+  uint4 xv[IX], cv[IC];
+#pragma unroll
+  for (int it = 0; it < IX; ++it) {
+    const int i = tid + 512 * it, r = min(max(R0 - DW + (i >> 5), 0), rows - 1);
+    xv[it] = *reinterpret_cast<const uint4*>(P.xa + (long long)r * C + (i & 31) * 8);
+  }
+#pragma unroll
+  for (int it = 0; it < IC; ++it) {
+    const int i = tid + 512 * it, r = min(R0 + (i >> 5), rows - 1);
+    cv[it] = *reinterpret_cast<const uint4*>(P.condb + (long long)r * C + (i & 31) * 8);
+  }
+  bf16x8 rw[WD];
+  const int k0 = half * 32;
+#pragma unroll
+  for (int i = 0; i < WD; ++i) rw[i] = wp[(k0 + i) * 64];
+#pragma unroll
+  for (int it = 0; it < IX; ++it) {
+    const int i = tid + 512 * it;
+    if (i < NX) *reinterpret_cast<uint4*>(&Xs[(i >> 5) * WG2_LD + (i & 31) * 8]) = xv[it];
+  }
+#pragma unroll
+  for (int it = 0; it < IC; ++it) {
+    const int i = tid + 512 * it;
+    *reinterpret_cast<uint4*>(&Cs[(i >> 5) * WG2_LD + (i & 31) * 8]) = cv[it];
+  }
+  // taps outside the frame's utterance (zero padding of the dilated conv)
+  bool inv0[4], inv2[4], any = false;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int R = min(R0 + 32 * q + n, rows - 1), b = R / P.T, t = R - b * P.T;
+    inv0[q] = t - d < 0;
+    inv2[q] = t + d >= P.T;
+    any |= inv0[q] | inv2[q];
+  }
+  const bool edge = __ballot(any) != 0;
+  __syncthreads();
+  f32x16 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+  if (half == 0) {
+    if (edge) wn_gate_kloop<DW, WD, 0, true>(acc, rw, wp, Xs, Cs, n, h, d, inv0, inv2);
+    else wn_gate_kloop<DW, WD, 0, false>(acc, rw, wp, Xs, Cs, n, h, d, inv0, inv2);
   } else {
-    const int b = R / T;
-    const float rs2 = 0.70710678118654752440f;
+    if (edge) wn_gate_kloop<DW, WD, 32, true>(acc, rw, wp, Xs, Cs, n, h, d, inv0, inv2);
+    else wn_gate_kloop<DW, WD, 32, false>(acc, rw, wp, Xs, Cs, n, h, d, inv0, inv2);
+  }
+  // exchange: wave (pw, half) finalises frame tiles 2 half, 2 half + 1 and hands the other two
+  // tiles' partial sums to its partner (x window space, every wave is past its reads).  Tile
+  // indices stay compile-time (a run-time index would put acc in scratch).
+  __syncthreads();
+  float* ex = reinterpret_cast<float*>(Xs);     // [pw][half][2 tiles][16 regs][64 lanes]
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const f32x16& acc = q ? acc1 : acc0;
-      const int n0 = WG_BN * (cg + P.nt0) + (q ? t1 : t0);
+  for (int q = 0; q < 4; ++q)
+    if ((q >> 1) != half) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int n = n0 + 8 * i + 4 * h;
-        const float4 bb = *reinterpret_cast<const float4*>(P.bias + n);
-        const float4 o = make_float4(acc[4 * i] + bb.x, acc[4 * i + 1] + bb.y, acc[4 * i + 2] + bb.z,
-                                     acc[4 * i + 3] + bb.w);
-        if (n < C) {
-          float4* xp = reinterpret_cast<float4*>(P.x + (long long)R * C + n);
-          const float4 xv = *xp;
-          const float4 xn = make_float4((xv.x + o.x) * rs2, (xv.y + o.y) * rs2, (xv.z + o.z) * rs2,
-                                        (xv.w + o.w) * rs2);
-          *xp = xn;
+      for (int r = 0; r < 16; ++r) ex[(((pw * 2 + half) * 2 + (q & 1)) * 16 + r) * 64 + lane] = acc[q][r];
+    }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if ((q >> 1) == half) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[q][r] += ex[(((pw * 2 + (1 - half)) * 2 + (q & 1)) * 16 + r) * 64 + lane];
+    }
+  // epilogue: register r < 8 = gate channel 16p + (r&3) + 8(r>>2) + 4h, r + 8 = its filter channel
+  float bg[8], bf[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int c = 16 * p + (r & 3) + 8 * (r >> 2) + 4 * h;
+    bg[r] = P.b1[c];
+    bf[r] = P.b1[C + c];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int R = R0 + 32 * q + n;
+    if ((q >> 1) == half && R < rows) {
+#pragma unroll
+      for (int gq = 0; gq < 2; ++gq) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * gq + e;
+          o[e] = (__bf16)gate_fast(acc[q][r] + bg[r], acc[q][r + 8] + bf[r]);
+        }
+        *reinterpret_cast<bf16x4*>(P.g + (long long)R * C + 16 * p + 8 * gq + 4 * h) = o;
+      }
+    }
+  }
+}
+
+struct WnResSkipArgs {
+  const __bf16* g;       // [rows][C] gated activations
+  const __bf16* W2f;     // [2C/32][C/16][64][8] (fragment order; tiles 0..C/32-1 residual, then skip)
+  const float* b2;       // [2C]
+  float* x;              // [rows][C] fp32 residual state, updated in place
+  float* skip;           // [rows][C] fp32
+  __bf16* xa_next;       // [rows][C] bf16(x + dp_{l+1}) or null (last layer)
+  const float* dp_next;  // dp_{l+1}[b * dp_ld + c]
+  int dp_ld, first, nt0, rows, T;
+};
+
+// RESSKIP block (bx, by): frames [32 RQ bx, +32 RQ), output tile nt = nt0 + 4 by + wave (32
+// channels; nt < C/32: residual, else skip).  The block's g rows live in LDS (A operand, frames on
+// the accumulator rows), a wave's 16 weight fragments (its whole K) sit in registers (B operand,
+// channels on the lanes), so the epilogue's fp32 x / skip accesses are 128-B row segments.
+// The epilogue operands are loaded before the MFMAs.
+template <int RQ>
+__global__ __launch_bounds__(256, 2) void wn_resskip_bf16_kernel(const WnResSkipArgs P) {
+  constexpr int C = 256, KS = C / 16, BR = 32 * RQ;
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[BR * WG2_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, h = lane >> 5;
+  int bx, by;
+  wn_xcd_block(bx, by);
+  const int R0 = bx * BR, rows = P.rows, T = P.T;
+  const int nt = P.nt0 + by * 4 + wave;
+  constexpr int IG = BR * 32 / 256;
+  uint4 gv[IG];
+#pragma unroll
+  for (int it = 0; it < IG; ++it) {
+    const int i = tid + 256 * it, r = min(R0 + (i >> 5), rows - 1);
+    gv[it] = *reinterpret_cast<const uint4*>(P.g + (long long)r * C + (i & 31) * 8);
+  }
+  const bf16x8* wp = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)nt * KS * 64 + lane;
+  bf16x8 w[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) w[ks] = wp[ks * 64];
+#pragma unroll
+  for (int it = 0; it < IG; ++it) {
+    const int i = tid + 256 * it;
+    *reinterpret_cast<uint4*>(&Gs[(i >> 5) * WG2_LD + (i & 31) * 8]) = gv[it];
+  }
+  // lane (n, h) of frame tile q holds channel c = 32 (nt mod C/32) + n of frames
+  // R0 + 32q + (r&3) + 8(r>>2) + 4h, r < 16
+  const bool res = nt < C / 32;
+  const int c = (res ? nt : nt - C / 32) * 32 + n;
+  float* io = res ? P.x : P.skip;
+  const bool rd = res || !P.first;
+  float xo[RQ][16];
+#pragma unroll
+  for (int q = 0; q < RQ; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int R = min(R0 + 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h, rows - 1);
+      xo[q][r] = rd ? io[(long long)R * C + c] : 0.f;
+    }
+  const float bias = P.b2[(res ? 0 : C) + c];
+  __syncthreads();
+  f32x16 acc[RQ];
+#pragma unroll
+  for (int q = 0; q < RQ; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    bf16x8 a[RQ];
+#pragma unroll
+    for (int q = 0; q < RQ; ++q)
+      a[q] = *reinterpret_cast<const bf16x8*>(&Gs[(32 * q + n) * WG2_LD + ks * 16 + 8 * h]);
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], w[ks], acc[q], 0, 0, 0);
+  }
+  const float rs2 = 0.70710678118654752440f;
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    // utterance of each row: one division per 32-row tile (T >= 32: at most one boundary inside)
+    const int Rq = R0 + 32 * q, bq = Rq / T, Rb = (bq + 1) * T;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int R = Rq + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (R < rows) {
+        const long long o = (long long)R * C + c;
+        const float v = acc[q][r] + bias;
+        if (res) {
+          const float xn = (xo[q][r] + v) * rs2;
+          io[o] = xn;
           if (P.xa_next) {
-            const float4 d = *reinterpret_cast<const float4*>(P.dp_next + (long long)b * P.dp_ld + n);
-            *reinterpret_cast<bf16x4*>(P.xa_next + (long long)R * C + n) =
-                bf16x4{(__bf16)(xn.x + d.x), (__bf16)(xn.y + d.y), (__bf16)(xn.z + d.z), (__bf16)(xn.w + d.w)};
+            const int b = T >= 32 ? bq + (R >= Rb ? 1 : 0) : R / T;
+            P.xa_next[o] = (__bf16)(xn + P.dp_next[(long long)b * P.dp_ld + c]);
           }
         } else {
-          float4* sp = reinterpret_cast<float4*>(P.skip + (long long)R * C + (n - C));
-          const float4 sv = P.first ? make_float4(0.f, 0.f, 0.f, 0.f) : *sp;
-          *sp = make_float4(sv.x + o.x, sv.y + o.y, sv.z + o.z, sv.w + o.w);
+          io[o] = xo[q][r] + v;
         }
       }
     }
@@ -486,41 +645,48 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     a.act = ACT_RELU;
     PD_TRY((launch_small_gemm<EPI_STORE, U_WN_INPROJ>(a, st, "wn_inproj")));
   }
-  if (h->W1f && h->layer_mode == 1 && C % WG_BN == 0 && (3 * C + H) % WG_KC == 0 && H % 8 == 0) {
-    // bf16: two launches per residual layer with 128 x 128 tiles (wn_gemm_bf16_kernel)
-    const int rows = B * T;
+  const int rows = B * T;
+  const int dil_max = 1 << (h->cyc - 1);
+  // bf16 layer implementation (PD_WN_OPT_LAYER 1): GATE + RESSKIP launches.  Not the default: at
+  // B*T = 1722 .. 27552 frames it measured equal to or slower than the fused kernel.
+  const bool two = h->W1p && dil_max <= 16 && h->layer_mode == 1;
+  if (two) {
+    // bf16: GATE + RESSKIP launches per residual layer (wn_gate_bf16_kernel, wn_resskip_bf16_kernel)
     __bf16* xa = reinterpret_cast<__bf16*>(ws + Lw.xa);
     __bf16* condb = reinterpret_cast<__bf16*>(ws + Lw.condb);
     __bf16* gb = reinterpret_cast<__bf16*>(ws + Lw.g);
     {
+      ProfScope ps("wn_xa", st);
       const long long n4 = ((long long)rows * (C > H ? C : H) + 3) / 4;
       hipLaunchKernelGGL(wn_xa_kernel, dim3(cdiv(n4, 256)), dim3(256), 0, st, x, dproj, Ly * C, xa, cond, condb,
                          rows, T, C, H);
       PD_LAUNCH_CHECK();
     }
-    const __bf16* W1 = lookup_bf16(h->Wl1);
-    const __bf16* W2 = lookup_bf16(h->Wl2);
     const int K1 = 3 * C + H;
     for (int l = 0; l < Ly; ++l) {
-      WnGemmArgs P{};
-      P.B = B; P.T = T; P.C = C; P.H = H; P.dil = 1 << (l % h->cyc);
-      P.W = W1 + (size_t)l * 2 * C * h->ldw1; P.ldw = h->ldw1; P.K = K1; P.bias = h->bl1 + (size_t)l * 2 * C;
-      P.xa = xa; P.condb = condb; P.g = gb;
+      WnGateArgs G{};
+      G.xa = xa; G.condb = condb; G.Wp = h->W1p + (size_t)l * 2 * C * K1; G.b1 = h->bl1 + (size_t)l * 2 * C;
+      G.g = gb; G.rows = rows; G.T = T; G.dil = 1 << (l % h->cyc);
       {
         ProfScope ps("wn_gate2", st);
-        hipLaunchKernelGGL(wn_gemm_bf16_kernel<WG_GATE>, dim3(cdiv(rows, WG_BM), C / 64), dim3(512), 0, st, P);
+        if (dil_max == 1)
+          hipLaunchKernelGGL(wn_gate_bf16_kernel<1>, dim3(cdiv(rows, WG2_ROWS), C / 64), dim3(512), 0, st, G);
+        else
+          hipLaunchKernelGGL(wn_gate_bf16_kernel<16>, dim3(cdiv(rows, WG2_ROWS), C / 64), dim3(512), 0, st, G);
         PD_LAUNCH_CHECK();
       }
       const bool last = l == Ly - 1;
-      P.W = W2 + (size_t)l * 2 * C * C; P.ldw = C; P.K = C; P.bias = h->bl2 + (size_t)l * 2 * C;
+      WnResSkipArgs P{};
+      P.g = gb; P.W2f = h->W2f + (size_t)l * 2 * C * C; P.b2 = h->bl2 + (size_t)l * 2 * C;
       P.x = x; P.skip = skip; P.first = l == 0;
       P.xa_next = last ? nullptr : xa; P.dp_next = last ? nullptr : dproj + (size_t)(l + 1) * C; P.dp_ld = Ly * C;
       // the last layer's residual half feeds nothing (wavenet.py:115-119 keeps only skip)
-      P.nt0 = last ? C / WG_BN : 0;
+      P.nt0 = last ? C / 32 : 0;
+      P.rows = rows; P.T = T;
       {
         ProfScope ps("wn_resskip2", st);
-        hipLaunchKernelGGL(wn_gemm_bf16_kernel<WG_RESSKIP>, dim3(cdiv(rows, WG_BM), (last ? C : 2 * C) / WG_BN),
-                           dim3(512), 0, st, P);
+        hipLaunchKernelGGL(wn_resskip_bf16_kernel<WN_RS_RQ>, dim3(cdiv(rows, 32 * WN_RS_RQ), (last ? C : 2 * C) / 128),
+                           dim3(256), 0, st, P);
         PD_LAUNCH_CHECK();
       }
     }
@@ -669,10 +835,11 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
       register_bf16_pool(h->pool, off, h->pool_bf);
       if (C == WNF_C && 3 * C + H == 1024) {   // H == 256: the fused kernel is built for K1 = 1024
         const int K1 = 3 * C + H;
-        const size_t per = (size_t)2 * C * K1 + (size_t)2 * C * C;
+        const size_t per = (size_t)4 * C * K1 + (size_t)2 * C * C;
         PD_HIP(hipMalloc(&h->frag, (size_t)L * per * sizeof(__bf16)));
         h->W1f = h->frag;
         h->W2f = h->frag + (size_t)L * 2 * C * K1;
+        h->W1p = h->W2f + (size_t)L * 2 * C * C;
         for (int l = 0; l < L; ++l) {
           const long long n1 = (long long)2 * C * K1, n2 = (long long)2 * C * C;
           hipLaunchKernelGGL(pack_frag_kernel, dim3(cdiv(n1, 256)), dim3(256), 0, st, h->W1f + l * n1,
@@ -680,6 +847,9 @@ int pd_wavenet_create(const pd_wavenet_dims* dims, const float* const* params, i
           PD_LAUNCH_CHECK();
           hipLaunchKernelGGL(pack_frag_kernel, dim3(cdiv(n2, 256)), dim3(256), 0, st, h->W2f + l * n2,
                              h->Wl2 + (size_t)l * 2 * C * C, 2 * C, C, C);
+          PD_LAUNCH_CHECK();
+          hipLaunchKernelGGL(pack_frag_pair_kernel, dim3(cdiv(n1, 256)), dim3(256), 0, st, h->W1p + l * n1,
+                             h->Wl1 + (size_t)l * 2 * C * h->ldw1, C, K1, h->ldw1);
           PD_LAUNCH_CHECK();
         }
       }

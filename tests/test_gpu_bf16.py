@@ -27,8 +27,9 @@ def tt(a):
                                   "wavenet_m80_c64_l4_cyc2"])
 def test_wavenet_bf16(name, layer):
     """Every bf16 residual-layer kernel (PD_WN_OPT_LAYER: 3 = fused, 64 frames per block; 0 =
-    fused, 32 frames; 1 = two 128x128-tile GEMMs; the default 2 picks 3 or 0 by grid size)
-    against the reference goldens."""
+    fused, 32 frames; 1 = GATE + RESSKIP kernels, 128-frame GATE tiles; the default 2 picks 3 or 0
+    by grid size) against the reference goldens.  cyc5 runs the 16-row-halo
+    GATE variant (dilations 1..16); the C=64 net has no fused kernel (engine path)."""
     d = G.load(name)
     M, H, L, C, cyc = [int(v) for v in d["dims"]]
     net = WaveNet(M, H, L, C, cyc)
