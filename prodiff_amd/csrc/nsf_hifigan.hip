@@ -777,9 +777,14 @@ int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, floa
     return PD_ERR_UNSUPPORTED;
   }
   switch (c.cout) {
-    case 256: return launch_wconv_c<256, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
-    case 128: return launch_wconv_c<128, 2, 2, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
-    case 64: return launch_wconv_c<64, 2, 1, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
+    // Tilings: a wave owns all TM rows of its 32-channel column tiles (WM = 1), so each weight
+    // fragment crosses the L2 -> CU port once per block instead of once per row-wave (r02:
+    // 2 x 2 wave grids at C = 128/256 read every fragment twice; C5 21.07 -> 19.19 ms/step,
+    // ResBlock convs 187 -> 159 us avg).  C = 32: 128, 256 or 512 rows per block measured
+    // equal or slower than 128 rows with four row-waves.
+    case 256: return launch_wconv_c<256, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
+    case 128: return launch_wconv_c<128, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
+    case 64: return launch_wconv_c<64, 4, 1, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
     case 32: return launch_wconv_c<32, 1, 1, 4, 1>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
     case 16: return launch_wconv16(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
     default: set_error("nsf wconv: unsupported channel count"); return PD_ERR_UNSUPPORTED;
