@@ -726,6 +726,7 @@ bool ups_window_ok(const NsfUps& U, bool wconv) {
 int launch_ups_window(const NsfUps& U, const float* in, float scale, int B, int Tin, const float* res, float* out,
                       hipStream_t st) {
   const __bf16* wb = lookup_bf16(U.w[0]);
+  // (r02: one row-wave per column tile, <512,2,1,1,4> / <256,4,1,1,4>, measured slower: 188 vs 178 us avg)
   if (U.cin == 512) return launch_ups_c<512, 1, 2, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);
   if (U.cin == 256) return launch_ups_c<256, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);
   if (U.cin == 128) return launch_ups_c<128, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);

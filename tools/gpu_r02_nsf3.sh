@@ -6,7 +6,7 @@ mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_nsf.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for v in new old new old; do
-  if [ $v = old ]; then export PRODIFF_HIP_LIB=$GRAFT_REPO_ROOT/ab/libprodiff_hip_nsfv1.so; else unset PRODIFF_HIP_LIB; fi
+  if [ $v = old ]; then export PRODIFF_HIP_LIB=$GRAFT_REPO_ROOT/ab/libprodiff_hip_prev.so; else unset PRODIFF_HIP_LIB; fi
   timeout -k 10 300 python -u bench.py --config C5 --cpu-frames 0 > $O/bench_$v.json 2> $O/bench_$v.err || { tail -5 $O/bench_$v.err; exit 1; }
   python - $v $O/bench_$v.json <<'PY'
 import json, sys
