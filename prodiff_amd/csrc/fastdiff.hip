@@ -1543,6 +1543,17 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
     }
     sv[u] = v;
   }
+  // every stage's weight fragments, issued behind the staging loads (vmcnt retires in order: the
+  // staging stores below wait only for the staging loads) -- no L2 round trip per conv stage
+  bf16x8 wf0[6], wf1[6], wf2[8];
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) {
+    wf0[kk] = *reinterpret_cast<const bf16x8*>(W0 + r32 * 96 + kk * 16 + h * 8);
+    wf1[kk] = *reinterpret_cast<const bf16x8*>(W1 + r32 * 96 + kk * 16 + h * 8);
+  }
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) wf2[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
+  const float bv0 = b0[r32], bv1 = b1[r32], bv2 = b2[r32];
 #pragma unroll
   for (int u = 0; u < DB_NI; ++u) {
     const int i = tid + 256 * u;
@@ -1556,11 +1567,7 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   }
   __syncthreads();
   // one dilated 32->32 conv stage over 5 row tiles starting at local row `first`
-  auto stage = [&](const __bf16* In, __bf16* Out, const __bf16* Wt, const float* bias, int first, int dil) {
-    bf16x8 wf[6];
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const bf16x8*>(Wt + r32 * 96 + kk * 16 + h * 8);
-    const float bv = bias[r32];
+  auto stage = [&](const __bf16* In, __bf16* Out, const bf16x8 (&wf)[6], float bv, int first, int dil) {
     for (int mt = wave; mt < 5; mt += 4) {
       f32x16 acc;
 #pragma unroll
@@ -1581,16 +1588,14 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
       }
     }
   };
-  stage(U0, H1, W0, b0, 1, 1);    // h1 on p in [1, 161)
+  stage(U0, H1, wf0, bv0, 1, 1);    // h1 on p in [1, 161)
   __syncthreads();
-  stage(H1, H2, W1, b1, 3, 2);    // h2 on p in [3, 163)
+  stage(H1, H2, wf1, bv1, 3, 2);    // h2 on p in [3, 163)
   __syncthreads();
   // out on p in [7, 135): conv_d4(h2) ++ residual_dense(x), K = 96 + 32
   {
-    bf16x8 wf[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) wf[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
-    const float bv = b2[r32];
+    const bf16x8 (&wf)[8] = wf2;
+    const float bv = bv2;
     const int mt = wave;   // 4 tiles, one per wave
     f32x16 acc;
 #pragma unroll
@@ -1652,16 +1657,29 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   __bf16* hout = A.hout + (long long)z * A.B * Tc * HK;
   float* Bfo = A.Bf + (long long)z * A.B * Tc * (2 * CI * NLY);
 
-  // c' = c + fc_t(e) on frames f0-18 .. f0+81 (channels 80..95 zero)
-  for (int i = tid; i < 100 * 24; i += 256) {
-    const int p = i / 24, g = (i - p * 24) * 4, f = f0 - 18 + p;
-    bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-    if (g < CC && f >= 0 && f < Tc) {
-      const float4 c = *reinterpret_cast<const float4*>(A.condT + (rb + f) * CC + g);
-      const float4 n = *reinterpret_cast<const float4*>(nzrow + g);
-      v = bf16x4{(__bf16)(c.x + n.x), (__bf16)(c.y + n.y), (__bf16)(c.z + n.z), (__bf16)(c.w + n.w)};
+  // c' = c + fc_t(e) on frames f0-18 .. f0+81 (channels 80..95 zero).  All loads are issued
+  // before any is used (clamped addresses, masked at the store): one round trip, not ten.
+  constexpr int NCI = (100 * 24 + 255) / 256;
+  float4 cv[NCI], nv[NCI];
+#pragma unroll
+  for (int u = 0; u < NCI; ++u) {
+    const int i = min(tid + 256 * u, 100 * 24 - 1), p = i / 24, g = min((i - p * 24) * 4, CC - 4);
+    const int f = min(max(f0 - 18 + p, 0), Tc - 1);
+    cv[u] = *reinterpret_cast<const float4*>(A.condT + (rb + f) * CC + g);
+    nv[u] = *reinterpret_cast<const float4*>(nzrow + g);
+  }
+#pragma unroll
+  for (int u = 0; u < NCI; ++u) {
+    const int i = tid + 256 * u;
+    if (i < 100 * 24) {
+      const int p = i / 24, g = (i - p * 24) * 4, f = f0 - 18 + p;
+      bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+      if (g < CC && f >= 0 && f < Tc) {
+        const float4 c = cv[u], n = nv[u];
+        v = bf16x4{(__bf16)(c.x + n.x), (__bf16)(c.y + n.y), (__bf16)(c.z + n.z), (__bf16)(c.w + n.w)};
+      }
+      *reinterpret_cast<bf16x4*>(Cs + p * LDC + g) = v;
     }
-    *reinterpret_cast<bf16x4*>(Cs + p * LDC + g) = v;
   }
   for (int i = tid; i < 3 * 2 * LDH; i += 256) {   // zero guard rows 0 and 97
     const int buf = i / (2 * LDH), j = i - buf * 2 * LDH;
@@ -1677,7 +1695,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const __bf16* wrow = A.Win[nblk] + (nt * 32 + r32) * 480 + h * 8;
-#pragma unroll 6
+#pragma unroll
     for (int kk = 0; kk < 30; ++kk) {
       const int tap = kk / 6, kc = kk - tap * 6;
       const bf16x8 af = *reinterpret_cast<const bf16x8*>(Cs + (mt * 32 + r32 + tap) * LDC + kc * 16 + h * 8);
@@ -1697,17 +1715,29 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
     }
   }
   __syncthreads();
-  // stages 1..6: residual convs H0 -> R0 -> R1 -> R0 -> R1 -> R0 -> R1
+  // stages 1..6: residual convs H0 -> R0 -> R1 -> R0 -> R1 -> R0 -> R1.
+  // A wave's jobs (wave, wave + 4) share the column tile nt = wave & 1: its 12 weight fragments
+  // are loaded once per stage and reused by both jobs; stage j + 1's fragments are loaded while
+  // stage j computes (no L2 round trip at a stage start).
+  bf16x8 bwn[12];
+  {
+    const __bf16* wrow = A.Wr[nblk][0] + ((wave & 1) * 32 + r32) * 192 + h * 8;
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk) bwn[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+  }
+#pragma unroll
   for (int j = 0; j < 6; ++j) {
     const __bf16* In = Hb[j == 0 ? 0 : (j & 1 ? 1 : 2)];
     __bf16* Out = Hb[j & 1 ? 2 : 1];
-    // a wave's jobs (wave, wave + 4) share the column tile nt = wave & 1: its 12 weight fragments
-    // are loaded once per stage, all in flight together, and reused by both jobs
     bf16x8 bwf[12];
-    {
-      const __bf16* wrow = A.Wr[nblk][j] + ((wave & 1) * 32 + r32) * 192 + h * 8;
 #pragma unroll
-      for (int kk = 0; kk < 12; ++kk) bwf[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+    for (int kk = 0; kk < 12; ++kk) bwf[kk] = bwn[kk];
+    {
+      // next stage's fragments, or the bias_conv's first column tile after the last stage
+      const __bf16* wrow = j < 5 ? A.Wr[nblk][j + 1] + ((wave & 1) * 32 + r32) * 192 + h * 8
+                                 : A.Wb[nblk] + (2 * wave * 32 + r32) * 192 + h * 8;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) bwn[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
     }
     for (int job = wave, q = 0; job < 6; job += 4, ++q) {
       const int mt = job >> 1, nt = job & 1;
@@ -1736,14 +1766,21 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
     __syncthreads();
   }
   bf16x8 bwb[12];
+#pragma unroll
+  for (int kk = 0; kk < 12; ++kk) bwb[kk] = bwn[kk];   // column tile 2w, loaded during stage 6
   // bias_conv on the 64 output frames: 2 row tiles x 8 column tiles; wave w owns column tiles
   // 2w and 2w+1 (weights loaded once per tile, reused by both row tiles)
+#pragma unroll
   for (int job = 0; job < 4; ++job) {
     const int nt = 2 * wave + (job >> 1), mt = job & 1;
-    if (mt == 0) {
-      const __bf16* wrow = A.Wb[nblk] + (nt * 32 + r32) * 192 + h * 8;
+    if (job == 1) {   // tile 2w + 1's fragments, in flight under tile 2w's second row tile
+      const __bf16* wrow = A.Wb[nblk] + ((nt + 1) * 32 + r32) * 192 + h * 8;
 #pragma unroll
-      for (int kk = 0; kk < 12; ++kk) bwb[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+      for (int kk = 0; kk < 12; ++kk) bwn[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+    }
+    if (job == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) bwb[kk] = bwn[kk];
     }
     f32x16 acc;
 #pragma unroll
