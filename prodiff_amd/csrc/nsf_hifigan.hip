@@ -390,42 +390,47 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
     }
   }
   // 3. epilogue: + bias (+ res) (+ out when accumulating), C/D map col = lane&31,
-  // row = (reg&3) + 8(reg>>2) + 4(lane>>5).  Per (M, N) fragment: all 16 residual loads in
-  // flight together (rows past the end clamp to the last row), then predicated stores.
+  // row = (reg&3) + 8(reg>>2) + 4(lane>>5).  In two batches of 8 rows per fragment, the
+  // residual / accumulator loads of EVERY fragment are in flight together (rows past the end
+  // clamp to the last row), then the predicated stores: two memory round trips per block
+  // instead of two per fragment (r02: the residual convs ran ~1.5x their plain twins).
   // 32-bit element offsets (the host checks B*Tl*C < 2^31) keep one VGPR per address
   const int rowb = b * Tl;
+  float bn[FN];
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
+  for (int j = 0; j < FN; ++j) bn[j] = bias[n0 + (wn * FN + j) * 32 + r32];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + (wn * FN + j) * 32 + r32;
-      const float bn = bias[n];
+  for (int hb = 0; hb < 16; hb += 8) {   // two batches of 8 rows: fewer live registers
+    float rv[FM][FN][8];
 #pragma unroll
-      for (int hb = 0; hb < 16; hb += 8) {   // two batches of 8 rows: fewer live registers
-        float rv[8];
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const int reg = hb + q;
+          const int reg = hb + q, n = n0 + (wn * FN + j) * 32 + r32;
           const int t = min(t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tl - 1);
           const int o = (rowb + t) * C + n;
           float v = res ? res[o] : 0.f;
           if constexpr (!OUT_BF)
             if (accum) v += reinterpret_cast<const float*>(out)[o];
-          rv[q] = v;
+          rv[i][j][q] = v;
         }
 #pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const int reg = hb + q;
+          const int reg = hb + q, n = n0 + (wn * FN + j) * 32 + r32;
           const int t = t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
           const int o = (rowb + t) * C + n;
-          const float v = acc[i][j][reg] + bn + rv[q];
+          const float v = acc[i][j][reg] + bn[j] + rv[i][j][q];
           if (t < Tl) {
             if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
             else reinterpret_cast<float*>(out)[o] = v;
           }
         }
-      }
-    }
   }
 }
 
@@ -448,30 +453,9 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
   const int b = blockIdx.y, t0 = blockIdx.x * TM;
   const int pad = (taps - 1) * dil / 2;
   const int W = TM + (taps - 1) * dil;
-  for (int i = tid; i < W * 2; i += 256) {
-    const int row = i >> 1, c8 = i & 1;
-    const int t = t0 - pad + row;
-    bf16x8 v;
-    if (t >= 0 && t < Tl) {
-      float f[8];
-      const long long e = ((long long)b * Tl + t) * C + 8 * c8;
-      if constexpr (IN_BF) {
-        const bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(in) + e);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = (float)x[j];
-      } else {
-        const float4 x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e);
-        const float4 x1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e + 4);
-        f[0] = x0.x; f[1] = x0.y; f[2] = x0.z; f[3] = x0.w; f[4] = x1.x; f[5] = x1.y; f[6] = x1.z; f[7] = x1.w;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[j] >= 0.f ? f[j] : alpha * f[j]) * scale);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-    }
-    *reinterpret_cast<bf16x8*>(nsf_win16 + row * LDA + 8 * c8) = v;
-  }
+  // the window (W rows x 2 items) in batches of NSF_WB items per thread, every load of a batch
+  // issued before any is converted (one round trip per batch, not one per item)
+  stage_window<C, IN_BF>(in, b, Tl, t0 - pad, W, alpha, scale, nsf_win16, LDA, tid);
   const int r16 = lane & 15, g = lane >> 4, kg = g & 1, tg = g >> 1;
   const int npair = (taps + 1) >> 1;
   bf16x8 bw[MAXP];
@@ -482,6 +466,19 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
     for (int j = 0; j < 8; ++j) bw[p][j] = (__bf16)0.f;
     if (p < npair && tap < taps) bw[p] = *reinterpret_cast<const bf16x8*>(w + (long long)r16 * (taps * kpad) + tap * kpad + 8 * kg);
   }
+  // the epilogue's residual / accumulator operands, loaded now so they land under the MFMAs
+  float rv[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = min(t0 + wave * 64 + i * 16 + 4 * g + r, Tl - 1);
+      const long long o = ((long long)b * Tl + t) * C + r16;
+      float v = res ? res[o] : 0.f;
+      if constexpr (!OUT_BF)
+        if (accum) v += reinterpret_cast<const float*>(out)[o];
+      rv[i][r] = v;
+    }
   __syncthreads();
   f32x4 acc[4];
 #pragma unroll
@@ -507,20 +504,11 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
   const float bn = bias[r16];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    float rv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = min(t0 + wave * 64 + i * 16 + 4 * g + r, Tl - 1);
-      const long long o = ((long long)b * Tl + t) * C + r16;
-      rv[r] = res ? res[o] : 0.f;
-      if constexpr (!OUT_BF)
-        if (accum) rv[r] += reinterpret_cast<const float*>(out)[o];
-    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int t = t0 + wave * 64 + i * 16 + 4 * g + r;
       const long long o = ((long long)b * Tl + t) * C + r16;
-      const float v = acc[i][r] + bn + rv[r];
+      const float v = acc[i][r] + bn + rv[i][r];
       if (t < Tl) {
         if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
         else reinterpret_cast<float*>(out)[o] = v;
