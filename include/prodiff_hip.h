@@ -200,6 +200,7 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 #define FD_OPT_LVC_SUB 4      /* 1: the hop < 32 block on the whole-block kernel too */
 #define FD_OPT_KP_SIDE 5      /* 1: kernel-predictor GEMMs of fd_sample on a low-priority side stream */
 #define FD_OPT_LVC_STREAM 6   /* 1: hop % 32 == 0 blocks on the streaming LVC pipeline kernel (default 0) */
+#define FD_OPT_KP_CHUNK 7     /* n > 0: kernel predictor + LVC block per chunk of n utterances (default 0 = whole batch) */
 int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */

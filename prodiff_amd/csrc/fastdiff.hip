@@ -72,6 +72,7 @@ struct fd_model {
   // the two streams share the CUs, so each kernel slows down by about the time the overlap
   // saves (r01 ab_v16b: 7.41 vs 7.33 ms/step).
   bool kp_side = false;
+  int kp_chunk = 0;   // FD_OPT_KP_CHUNK: utterances per kernel-predictor -> LVC chunk (0 = whole batch)
   mutable hipStream_t side = nullptr;
   mutable hipEvent_t ev_hidden = nullptr, ev_kp[4] = {}, ev_lvc[4] = {};
   float* pool = nullptr;
@@ -361,6 +362,7 @@ struct LvcBlockArgs {
   unsigned long long seed;
   unsigned stream;
   int Tc, hop;
+  int b_off;                // utterance index of blockIdx.y = 0 in the whole batch (Philox draws)
 #ifdef LB_TRACE
   unsigned long long* trace;   // tools/lvc_probe.hip: per-phase s_memtime stamps
 #endif
@@ -570,7 +572,8 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
       const int s2 = tid + it * G::NT, t = t0 + (s2 >> 1);
       zr[it] = 0.f;
       if (s2 < 2 * TS && (s2 & 1) == 0 && t < Lh && P.sig != 0.f)
-        zr[it] = P.noise ? P.noise[base + t] : philox_normal(P.seed, (unsigned long long)(base + t), P.stream);
+        zr[it] = P.noise ? P.noise[base + t]
+                         : philox_normal(P.seed, (unsigned long long)((long long)(b + P.b_off) * Lh + t), P.stream);
     }
   }
   // ---- LDS stores of the staged operands
@@ -1469,7 +1472,9 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
             e += P.bfin[0];
             float v = (FS[AU_OFF + ((32 * j + sm) & (NAU - 1))] - P.ce * e) / P.den;
             if (P.sig != 0.f)
-              v += P.sig * (P.noise ? P.noise[base + t] : philox_normal(P.seed, (unsigned long long)(base + t), P.stream));
+              v += P.sig * (P.noise ? P.noise[base + t]
+                                    : philox_normal(P.seed, (unsigned long long)((long long)(b + P.b_off) * Lh + t),
+                                                    P.stream));
             P.audio_out[base + t] = v;
           }
         }
@@ -2303,38 +2308,46 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         PD_LAUNCH_CHECK();
       }
       __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf);
-      const int rows = B * Tc;
+      // FD_OPT_KP_CHUNK: kernel predictor + LVC block per chunk of utterances, so a chunk's
+      // kernel tensor can still be on-die (Infinity Cache) when the LVC block reads it
+      const bool stream_path = m->lvc_stream && ups && hop % 32 == 0 && r >= 4 && (last && aud ? r <= 4 : r <= 8);
+      const int cb = (!side && !stream_path && m->kp_chunk > 0 && m->kp_chunk < B) ? m->kp_chunk : B;
+      for (int b0 = 0; b0 < B; b0 += cb) {
+      const int nbk = B - b0 < cb ? B - b0 : cb;
+      const int rows = nbk * Tc;
+      __bf16* Kc = Kb;
       if (side) {   // written on the side stream (fd_sample)
-        Kb += (size_t)n * rows * NLY * KPERLAYER;
+        Kc += (size_t)n * rows * NLY * KPERLAYER;
         PD_HIP(hipStreamWaitEvent(st, m->ev_kp[n], 0));
       } else {
-        PD_TRY(kp_kernels_all(K, hkb, Kb, B, Tc, st, true));
+        PD_TRY(kp_kernels_all(K, hkb + (size_t)b0 * Tc * HK, Kc, nbk, Tc, st, true));
       }
       LvcBlockArgs la{};
       for (int i = 0; i < NLY; ++i) {
-        la.Kf[i] = Kb + (size_t)i * rows * KPERLAYER;
+        la.Kf[i] = Kc + (size_t)i * rows * KPERLAYER;
         la.Wc[i] = lookup_bf16(K.cv_w[i]);
         la.bc[i] = K.cv_b[i];
       }
       // never write the buffer this launch reads: with the upsample fused, x_prev is the
       // previous block's output (the other ping-pong buffer, or the DBlock output)
-      la.xin = ups ? x : xn;
-      la.xout = ups ? xn : ws + W.y;
-      la.a = (last && aud) ? nullptr : ad;
-      la.Bf = Bfp; la.Tc = Tc; la.hop = hop;
+      la.xin = (ups ? x : xn) + (size_t)b0 * (ups ? Tin : Tout) * CI;
+      la.xout = (ups ? xn : ws + W.y) + (size_t)b0 * Tout * CI;
+      la.a = (last && aud) ? nullptr : ad + (size_t)b0 * Tout * CI;
+      la.Bf = Bfp + (size_t)b0 * Tc * 2 * CI * NLY; la.Tc = Tc; la.hop = hop; la.b_off = b0;
       la.Wup = lookup_bf16(K.upf_w); la.bup = K.up_b; la.r = r; la.p = r / 2 + r % 2;
-      la.audio = xa; la.fw = m->first_w; la.fb = m->first_b;
+      la.audio = xa + (size_t)b0 * L; la.fw = m->first_w; la.fb = m->first_b;
       la.wfin = m->final_w; la.bfin = m->final_b;
       if (fuse_fin) {
-        la.audio_out = fin->audio_out; la.noise = fin->noise; la.ce = fin->ce; la.den = fin->den;
+        la.audio_out = fin->audio_out + (size_t)b0 * L; la.noise = fin->noise ? fin->noise + (size_t)b0 * L : nullptr;
+        la.ce = fin->ce; la.den = fin->den;
         la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream;
       }
       // (the LDS image holds upsample weights for r <= 4 with the audio fusions, r <= 8 without)
-      if (m->lvc_stream && ups && hop % 32 == 0 && r >= 4 && (last && aud ? r <= 4 : r <= 8)) {
+      if (stream_path) {
         // streaming pipeline: one long time range per workgroup (lvc_stream_bf16_kernel)
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : "fd_lvc_block_ups", st);
-        const int Lh = (int)Tout, seg = lvc_stream_seg(Lh, B);
-        const dim3 grid(cdiv(Lh, seg), B);
+        const int Lh = (int)Tout, seg = lvc_stream_seg(Lh, nbk);
+        const dim3 grid(cdiv(Lh, seg), nbk);
         if (last && aud && fuse_fin)
           hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, true, 4>), grid, dim3(512), 0, st, la, seg);
         else if (last && aud)
@@ -2349,13 +2362,15 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
                                                                                    : "fd_lvc_block", st);
         const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
         const bool pf = m->lvc_pf && hop % 64 == 0;   // a 64-row tile pair shares one frame
-        if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
-        else if (ts == 384) PD_TRY(launch_lvc_block_ts<384>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
-        else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, pf, Tout, B, st));
+        if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
+        else if (ts == 384) PD_TRY(launch_lvc_block_ts<384>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
+        else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
       }
+      }
+      float* xo = ups ? xn : ws + W.y;
       if (side) PD_HIP(hipEventRecord(m->ev_lvc[n], st));   // ring slot n free again
       if (fuse_fin) { *xout = nullptr; return PD_OK; }
-      x = la.xout;
+      x = xo;
       Tin = Tout;
       continue;
     }
@@ -2606,6 +2621,10 @@ int fd_set_option(fd_model* m, int option, int value) {
     case FD_OPT_LVC_SUB: m->lvc_sub = value != 0; return PD_OK;
     case FD_OPT_KP_SIDE: m->kp_side = value != 0; return PD_OK;
     case FD_OPT_LVC_STREAM: m->lvc_stream = value != 0; return PD_OK;
+    case FD_OPT_KP_CHUNK:
+      PD_CHECK_ARG(value >= 0, "FD_OPT_KP_CHUNK >= 0");
+      m->kp_chunk = value;
+      return PD_OK;
     default: break;
   }
   set_error("fd_set_option: unknown option " + std::to_string(option));

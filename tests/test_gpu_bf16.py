@@ -146,3 +146,23 @@ def test_reflow_euler_bf16():
     xT = synth.synth_inputs(73, (2, 1, 80, 37))
     x = rf.sample(tt(cond), infer_step=20, x_T=tt(xT)).cpu().numpy()
     assert_bf16_close(x, OR.reflow_sample(p, cond, xT, 20, "euler", 1000, 20, 1), "reflow_euler_20")
+
+
+@pytest.mark.parametrize("chunk", [1, 2])
+def test_fastdiff_kp_chunk_bitexact(chunk):
+    """FD_OPT_KP_CHUNK (kernel predictor + LVC block per chunk of utterances) changes only the
+    launch order: the sample -- on-device Philox draws included -- is bit-identical."""
+    p = G.fastdiff_params(31)
+    s = G.load("schedules")
+    B, Tc = 3, 7
+    c = synth.synth_inputs(77, (B, 80, Tc), loc=-5.0, scale=2.0)
+    outs = []
+    for ch in (0, chunk):
+        m = FastDiff()
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+        m = m.to(DEV).set_compute_dtype("bf16").set_options(kp_chunk=ch)
+        wav = sampling_given_noise_schedule(m, (B, 1, Tc * 256), {"alpha": torch.from_numpy(s["fd_train_alpha"])},
+                                            torch.from_numpy(s["fd_n4_beta"]), condition=tt(c), seed=1234)
+        outs.append(wav.cpu().numpy())
+    assert np.isfinite(outs[0]).all()
+    np.testing.assert_array_equal(outs[0], outs[1])
