@@ -416,7 +416,7 @@ __device__ __forceinline__ f32x2 gate2s(f32x2 gs, f32x2 fs) {
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0 ? a : a - b + 1) / b; }
 
 template <int TS, bool UPS, bool AUD, bool FIN, bool PF = false, bool SUB = false>
-__global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
+__global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
   static_assert(!(PF && SUB), "prefetch assumes one frame per tile");
   using G = LbGeo<TS>;
   constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF, GR = NG * 32;
@@ -872,22 +872,38 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, PF ? 2 : 3) void lvc_block_bf16_kern
           // hop < 32: the tile spans 32/hop frames.  Column n belongs to frame (ts + n)/hop;
           // one MFMA chain per frame with the other frames' columns zeroed in B, so every
           // column accumulates exactly its own frame's kernel.
-          bf16x8 yb[6];
-#pragma unroll
-          for (int kk = 0; kk < 6; ++kk)
-            yb[kk] = *reinterpret_cast<const bf16x8*>(&Y[(k * 32 + n + (kk >> 1)) * LB_LD + 16 * (kk & 1) + 8 * h]);
           const int f0 = ts / hop, fn = (ts + n) / hop;
-          for (int fr = f0; fr < f0 + 32 / hop && fr < Tc; ++fr) {
-            const __bf16* kq = P.Kf[l] + ((long long)b * Tc + fr) * KPERLAYER;
-            const bool mine = fn == fr;
+          const int nf = min(32 / hop, Tc - f0);
+          // the frames' kernel fragments in a 2-deep register pipeline: frame i + 1's loads are
+          // in flight under frame i's MFMAs (a load-then-use chain per frame made this block a
+          // series of L2 round trips: 79 us for one utterance vs 121 us for eight, r02)
+          const __bf16* kq0 = P.Kf[l] + ((long long)b * Tc + f0) * KPERLAYER;
+          bf16x8 ka[12], kb[12];
+          auto kld = [&](bf16x8 (&d)[12], int i) {   // unconditional: rows past the last frame clamp
+            const __bf16* kq = kq0 + (long long)min(i, nf - 1) * KPERLAYER;
+#pragma unroll
+            for (int kk = 0; kk < 12; ++kk) d[kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+            __builtin_amdgcn_sched_barrier(0);    // keep the loads here (the scheduler sinks them to their use)
+          };
+          auto kmm = [&](const bf16x8 (&kf)[12], int i) {
+            const bool mine = fn == f0 + i;
 #pragma unroll
             for (int kk = 0; kk < 6; ++kk) {
+              // B operand re-read from LDS per frame (registers go to the kernel pipeline)
+              const bf16x8 yv = *reinterpret_cast<const bf16x8*>(&Y[(k * 32 + n + (kk >> 1)) * LB_LD + 16 * (kk & 1) + 8 * h]);
               const bf16x8 z = {};
-              const bf16x8 ym = mine ? yb[kk] : z;
-              const bf16x8 kg = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
-              const bf16x8 kt = *reinterpret_cast<const bf16x8*>(kq + ((6 + kk) * 64 + lane) * 8);
-              g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kg, ym, g, 0, 0, 0);
-              f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, ym, f, 0, 0, 0);
+              const bf16x8 ym = mine ? yv : z;
+              g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk], ym, g, 0, 0, 0);
+              f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[6 + kk], ym, f, 0, 0, 0);
+            }
+          };
+          kld(ka, 0);
+          for (int i = 0; i < nf; i += 2) {
+            kld(kb, i + 1);
+            kmm(ka, i);
+            if (i + 1 < nf) {
+              kld(ka, i + 2);
+              kmm(kb, i + 1);
             }
           }
           bq = P.Bf + ((long long)b * Tc + (fn < Tc ? fn : Tc - 1)) * (2 * CI * NLY) + l * 2 * CI;
