@@ -1957,7 +1957,7 @@ int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B
                    bool prescale = false) {
   const int rows = B * Tc;
   const int fblocks = cdiv(rows, KP_FR);
-  int groups = 512 / fblocks;                 // 2 blocks per CU x 256 CUs, one wave of blocks
+  int groups = 512 / fblocks;                 // 2 blocks per CU x 256 CUs, one wave of blocks (r02: 256 / 1024 slower)
   groups = groups < 16 ? 16 : groups > KP_TILES ? KP_TILES : groups;   // >= 16: Bs holds a block's tiles
   ProfScope ps("fd_kp_kernel", st);
   hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(fblocks, groups), dim3(KP_THREADS), 0, st, hk, lookup_bf16(K.kk_w),
