@@ -118,9 +118,11 @@ def test_c3_slice_fastdiff_fp32(c3):
     np.testing.assert_allclose(wav.mean(1), c3["wav_mean"], rtol=0, atol=1e-6)
 
 
-def test_c3_full_bf16_vs_fp32():
-    """B=8 x 861 (the bench's C3 batch): bf16 sampler chain vs the fp32 HIP chain, same draws."""
-    B, T = 8, 861
+@pytest.mark.parametrize("B", [8, 32])
+def test_c3_full_bf16_vs_fp32(B):
+    """B=8 x 861 (the bench's C3 batch) and B=32 x 861 (C4's per-GPU batch: the 64-frame fused
+    WaveNet layer blocks, 4x the LVC grids): bf16 sampler chain vs the fp32 HIP chain, same draws."""
+    T = 861
     L = T * 256
     gen = torch.Generator(device=DEV).manual_seed(5)
     cond = torch.randn(B, T, 256, device=DEV, generator=gen)
@@ -128,13 +130,13 @@ def test_c3_full_bf16_vs_fp32():
     nz = torch.randn(2, B, 1, 80, T, device=DEV, generator=gen)
     mel32 = prodiff(0).sample(cond, x_T=xT, noise=nz)
     mel16 = prodiff(0, "bf16").sample(cond, x_T=xT, noise=nz)
-    assert_bf16_close(mel16.cpu().numpy(), mel32.cpu().numpy(), "C3 ProDiff bf16 vs fp32, B=8x861")
+    assert_bf16_close(mel16.cpu().numpy(), mel32.cpu().numpy(), f"C3 ProDiff bf16 vs fp32, B={B}x861")
     wT = torch.randn(B, 1, L, device=DEV, generator=gen)
     wn = torch.randn(3, B, 1, L, device=DEV, generator=gen)
     b, a, s, st = SCHED
     wav32 = fastdiff(1).sample(mel32, b, a, s, st, x_T=wT, noise=wn).cpu().numpy()
     wav16 = fastdiff(1, "bf16").sample(mel32, b, a, s, st, x_T=wT, noise=wn).cpu().numpy()
-    assert_bf16_close(wav16, wav32, "C3 FastDiff bf16 vs fp32, B=8x861")
+    assert_bf16_close(wav16, wav32, f"C3 FastDiff bf16 vs fp32, B={B}x861")
 
 
 def test_c5_full_bf16_vs_fp32():
