@@ -83,22 +83,46 @@ __device__ __forceinline__ float nsf_rad(float f0, int h, int f, float sr, const
   return r;
 }
 
-// P[b][f][h] = sum_{f' < f} rad[b][f'][h] in double (one thread per (b, h)).
-__global__ __launch_bounds__(64) void nsf_phase_prefix_kernel(const float* __restrict__ f0, int B, int T, int dim,
-                                                              float sr, const float* __restrict__ rand_ini,
-                                                              unsigned long long seed, double* __restrict__ P) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * dim) return;
-  int b = i / dim, h = i - b * dim;
+// P[b][f][h] = sum_{f' < f} rad[b][f'][h] in double, and Rd[b][f][h] = rad[b][f][h] (fp32, the
+// source kernel reads it instead of recomputing fmod/div per sample).  One block per (b, h):
+// each thread sums a contiguous run of frames, a block-wide exclusive scan of the run sums
+// (double, in LDS) gives every run its offset.  (r02: one serial thread per (b, h) took 181 us.)
+constexpr int NSF_PP_THREADS = 256;
+__global__ __launch_bounds__(NSF_PP_THREADS) void nsf_phase_prefix_kernel(const float* __restrict__ f0, int B, int T,
+                                                                        int dim, float sr,
+                                                                        const float* __restrict__ rand_ini,
+                                                                        unsigned long long seed,
+                                                                        double* __restrict__ P,
+                                                                        float* __restrict__ Rd) {
+  __shared__ double part[NSF_PP_THREADS];
+  const int i = blockIdx.x, b = i / dim, h = i - b * dim, tid = threadIdx.x;
+  const int run = (T + NSF_PP_THREADS - 1) / NSF_PP_THREADS, fa = tid * run, fb = min(fa + run, T);
   double acc = 0.0;
-  for (int f = 0; f < T; ++f) {
-    P[((long long)b * T + f) * dim + h] = acc;
-    acc += (double)nsf_rad(f0[(long long)b * T + f], h, f, sr, rand_ini, seed, b, dim);
+  for (int f = fa; f < fb; ++f) {
+    const float r = nsf_rad(f0[(long long)b * T + f], h, f, sr, rand_ini, seed, b, dim);
+    Rd[((long long)b * T + f) * dim + h] = r;
+    acc += (double)r;
+  }
+  part[tid] = acc;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over the 256 run sums
+  for (int o = 1; o < NSF_PP_THREADS; o <<= 1) {
+    const double v = tid >= o ? part[tid - o] : 0.0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  double run_off = tid > 0 ? part[tid - 1] : 0.0;
+  for (int f = fa; f < fb; ++f) {
+    const long long e = ((long long)b * T + f) * dim + h;
+    P[e] = run_off;
+    run_off += (double)Rd[e];
   }
 }
 
 // har[b][t] = tanh(l_linear(sine_waves)) (models.py:168-219), one thread per sample.
 __global__ __launch_bounds__(256) void nsf_source_kernel(const float* __restrict__ f0, const double* __restrict__ P,
+                                                         const float* __restrict__ Rd,
                                                          int B, int T, int upp, int dim, float sr,
                                                          const float* __restrict__ rand_ini,
                                                          const float* __restrict__ noise, unsigned long long seed,
@@ -115,8 +139,8 @@ __global__ __launch_bounds__(256) void nsf_source_kernel(const float* __restrict
   const float namp = uv * NSF_NOISE_STD + (1.f - uv) * NSF_SINE_AMP / 3.f;
   float acc = 0.f;
   for (int h = 0; h < dim; ++h) {
-    double ph = (double)upp * P[((long long)b * T + f) * dim + h] +
-                (double)(j + 1) * (double)nsf_rad(fv, h, f, sr, rand_ini, seed, b, dim);
+    const long long e = ((long long)b * T + f) * dim + h;
+    double ph = (double)upp * P[e] + (double)(j + 1) * (double)Rd[e];
     ph -= floor(ph);
     float s = (float)sin(ph * 6.283185307179586) * NSF_SINE_AMP;
     long long ni = i * dim + h;
@@ -806,7 +830,7 @@ __global__ __launch_bounds__(256) void nsf_accum_kernel(float4* __restrict__ xs,
 }
 
 struct NsfWs {
-  size_t P = 0, har = 0, X = 0, T1 = 0, R = 0, XS = 0, src = 0, total = 0;   // float offsets
+  size_t P = 0, Rd = 0, har = 0, X = 0, T1 = 0, R = 0, XS = 0, src = 0, total = 0;   // float offsets
 };
 
 NsfWs nsf_layout(const nsf_model* m, int B, int T) {
@@ -821,6 +845,7 @@ NsfWs nsf_layout(const nsf_model* m, int B, int T) {
   size_t act = al((size_t)B * T * per_frame);
   size_t off = 0;
   W.P = off; off += al((size_t)B * T * m->dim * 2);
+  W.Rd = off; off += al((size_t)B * T * m->dim);
   W.har = off; off += al((size_t)B * T * m->upp);
   W.X = off; off += act;
   W.T1 = off; off += act;
@@ -1088,9 +1113,10 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
   const float sr = (float)d.sampling_rate;
   {
     ProfScope ps("nsf_source", st);
-    hipLaunchKernelGGL(nsf_phase_prefix_kernel, dim3(cdiv((long long)B * dim, 64)), dim3(64), 0, st, f0, B, T, dim,
-                       sr, rand_ini, seed, P);
-    hipLaunchKernelGGL(nsf_source_kernel, dim3(cdiv((long long)B * L, 256)), dim3(256), 0, st, f0, P, B, T, m->upp,
+    float* Rd = ws + W.Rd;
+    hipLaunchKernelGGL(nsf_phase_prefix_kernel, dim3(B * dim), dim3(NSF_PP_THREADS), 0, st, f0, B, T, dim, sr,
+                       rand_ini, seed, P, Rd);
+    hipLaunchKernelGGL(nsf_source_kernel, dim3(cdiv((long long)B * L, 256)), dim3(256), 0, st, f0, P, Rd, B, T, m->upp,
                        dim, sr, rand_ini, noise, seed, m->lin_w, m->lin_b, har);
   }
   PD_LAUNCH_CHECK();
