@@ -166,3 +166,37 @@ def test_fastdiff_kp_chunk_bitexact(chunk):
         outs.append(wav.cpu().numpy())
     assert np.isfinite(outs[0]).all()
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cyc", [1, 5])
+def test_wavenet_two_kernel_vs_fused(cyc):
+    """PD_WN_OPT_LAYER=1 (GATE + RESSKIP) against the fused layer at a ragged size: B=5 x 203
+    frames puts utterance boundaries inside 128-frame GATE blocks (tap masks) and, with cyc=5,
+    dilations up to 16 (the 16-row-halo GATE variant).  Same bf16 roundings, only the fp32
+    summation order differs (measured: bit-identical outputs; the bf16 rounding of every layer's
+    inputs absorbs the reordering).  The launch tags prove which path ran."""
+    torch.manual_seed(3)
+    net = WaveNet(80, 256, 20, 256, cyc)
+    B, T = 5, 203
+    spec = torch.randn(B, 1, 80, T, device=DEV)
+    cond = torch.randn(B, 256, T, device=DEV)
+    steps = torch.full((B,), 7.0, device=DEV)
+    from prodiff_amd import _lib
+    outs, tags = {}, {}
+    for layer in (0, 1):
+        m = WaveNet(80, 256, 20, 256, cyc)
+        m.load_state_dict(net.state_dict())
+        m = m.to(DEV).set_compute_dtype("bf16").set_options(layer=layer)
+        m(spec, steps, cond)                      # pack the handle
+        torch.cuda.synchronize()
+        _lib.profile_enable(True)
+        outs[layer] = m(spec, steps, cond).float().cpu().numpy()
+        torch.cuda.synchronize()
+        tags[layer] = set(_lib.profile_summary())
+        _lib.profile_enable(False)
+    assert "wn_gate2" in tags[1] and "wn_resskip2" in tags[1] and "wn_layer" not in tags[1], tags[1]
+    assert "wn_layer" in tags[0], tags[0]
+    a, b = outs[1], outs[0]
+    rel = float(np.linalg.norm(a - b) / np.linalg.norm(b))
+    print(f"BF16ERR two-kernel vs fused WaveNet cyc={cyc} B={B}x{T} rel-L2={rel:.3e}")
+    assert np.isfinite(a).all() and rel <= 2e-3
