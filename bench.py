@@ -154,28 +154,38 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
     }
 
 
-# bench tag -> kernel symbol (the default tile sizes) for the PMC traffic lookup
+# bench tag -> kernel symbols that can serve it (the default kernel first) for the PMC
+# traffic lookup; the first one present in a summary is used
 TAG_KERNEL = {
-    "fd_lvc_block_final": "lvc_block_bf16_kernel<384, true, true, true, true, false>",
-    "fd_lvc_block_ups": "lvc_block_bf16_kernel<384, true, false, false, true, false>",
-    "fd_lvc_block_sub": "lvc_block_bf16_kernel<128, true, false, false, false, true>",
-    "fd_kp_kernel": "kp_kernel_bf16_kernel",
-    "wn_layer": "wn_layer_bf16_kernel",
-    "wn_gate2": "wn_gate_bf16_kernel",
-    "wn_resskip2": "wn_resskip_bf16_kernel",
-    "nsf_res": "nsf_wconv_kernel<",
+    "fd_lvc_block_final": ("lvc_skew_bf16_kernel<true, true>", "lvc_block_bf16_kernel<384, true, true, true, true, false>"),
+    "fd_lvc_block_ups": ("lvc_skew_bf16_kernel<false, false>", "lvc_block_bf16_kernel<384, true, false, false, true, false>"),
+    "fd_lvc_block_sub": ("lvc_block_bf16_kernel<128, true, false, false, false, true>",),
+    "fd_kp_kernel": ("kp_kernel_bf16_kernel",),
+    "wn_layer": ("wn_layer_bf16_kernel",),
+    "wn_gate2": ("wn_gate_bf16_kernel",),
+    "wn_resskip2": ("wn_resskip_bf16_kernel",),
+    "nsf_res": ("nsf_wconv_kernel<",),
 }
 
 
-def pmc_traffic(tag, path=None):
-    """HBM bytes per launch of `tag`'s kernel(s) from the newest committed PMC summary that
-    holds them (profiles/rNN_vMM_traffic.json, written by tools/pmc_traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of the bench command).  A tag served by several
-    template instantiations (nsf_res) gets the launch-weighted mean.  None if absent."""
+def traffic_workload(d, fname):
+    """(config, per-GPU batch, frames) a PMC summary was measured on.  Summaries written
+    before round 3 carry no workload: they are C5 (file name *c5*) or C3, 8 x 861."""
+    if "config" in d:
+        return d["config"], int(d["batch"]), int(d["frames"])
+    return ("C5" if "c5" in os.path.basename(fname) else "C3"), 8, 861
+
+
+def pmc_traffic(tag, config, batch, frames, path=None):
+    """HBM bytes per launch of `tag`'s kernel(s) from the newest committed PMC summary
+    measured on the SAME workload (config, per-GPU batch, frames) -- profiles/rNN_vMM_traffic.json,
+    written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
+    of the bench command.  A tag served by several template instantiations (nsf_res) gets the
+    launch-weighted mean.  (None, None) when no summary of this workload holds the kernel."""
     import glob
     import re
-    sym = TAG_KERNEL.get(tag)
-    if sym is None:
+    syms = TAG_KERNEL.get(tag)
+    if syms is None:
         return None, None
     if path is None:
         def ver(f):
@@ -188,12 +198,16 @@ def pmc_traffic(tag, path=None):
         if not os.path.exists(fpath):
             continue
         with open(fpath) as f:
-            kern = json.load(f)["kernels"]
-        hits = [v for name, v in kern.items() if sym in name]
-        if hits:
-            n = sum(v["launches"] for v in hits)
-            tb = sum(v["traffic_bytes_per_launch"] * v["launches"] for v in hits) / n
-            return float(tb), os.path.relpath(fpath, ROOT)
+            d = json.load(f)
+        if traffic_workload(d, fpath) != (config, batch, frames):
+            continue
+        kern = d["kernels"]
+        for sym in syms:
+            hits = [v for name, v in kern.items() if sym in name]
+            if hits:
+                n = sum(v["launches"] for v in hits)
+                tb = sum(v["traffic_bytes_per_launch"] * v["launches"] for v in hits) / n
+                return float(tb), os.path.relpath(fpath, ROOT)
     return None, None
 
 
@@ -541,7 +555,7 @@ def main():
             ach = fl[dom] * cnt / sec / 1e12
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
                         "frac": round(ach / peak_tf, 4)}
-        traffic, tsrc = pmc_traffic(dom, args.traffic)
+        traffic, tsrc = pmc_traffic(dom, cfg_name, B, T, args.traffic)
         roofline.update({"traffic": round(traffic) if traffic else None, "traffic_source": tsrc, "kernel": dom,
                          "flop_per_launch": fl[dom], "bytes_per_launch": by.get(dom),
                          "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(ridge, 1),

@@ -201,6 +201,8 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 #define FD_OPT_KP_SIDE 5      /* 1: kernel-predictor GEMMs of fd_sample on a low-priority side stream */
 #define FD_OPT_LVC_STREAM 6   /* 1: hop % 32 == 0 blocks on the streaming LVC pipeline kernel (default 0) */
 #define FD_OPT_KP_CHUNK 7     /* n > 0: kernel predictor + LVC block per chunk of n utterances (default 0 = whole batch) */
+#define FD_OPT_LVC_SKEW 8     /* 1: hop >= 64 blocks with r in {4,8} on the skewed persistent LVC kernel (default 0) */
+#define FD_OPT_LVC_SEG 9      /* n > 0: skewed-kernel segment length in 32-row tiles (default 0 = ~one workgroup per CU) */
 int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */

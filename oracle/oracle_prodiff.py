@@ -85,7 +85,10 @@ def mish(x):
 
 
 def sigmoid(x):
-    return 1.0 / (1.0 + np.exp(-x))
+    """Overflow-free logistic: exp is only taken of -|x| (the naive 1/(1+exp(-x)) warns for
+    x << 0 although its result, 0, is right)."""
+    e = np.exp(-np.abs(x))
+    return np.where(x >= 0, 1.0 / (1.0 + e), e / (1.0 + e))
 
 
 def sinusoidal_pos_emb(steps, dim):

@@ -11,7 +11,11 @@ modules re-pack whenever a parameter tensor changes).
 
 Difference from the reference: files load with ``torch.load(weights_only=True)``
 (tensors and plain containers only, nothing unpickled is executed); a checkpoint
-that needs arbitrary unpickling is refused with the loader's error.
+that needs arbitrary unpickling is refused with the loader's error.  The only
+non-container globals allowed are numpy's scalar reconstructor and dtypes: the
+reference trainer stores ``checkpoint_callback_best`` as a numpy scalar once it
+resumes (``np.load(best_valid.npy)[0]``, utils/pl_utils.py:321,751), and such a
+value is data, not code.
 The vocoder layouts live beside their vocoders: FastDiff ``config.yaml`` +
 ``['state_dict']['model']`` (prodiff_amd.vocoder.load_fastdiff_model, reference
 component/vocoder/fastdiff.py:17-41) and NSF-HiFiGAN ``config.json`` +
@@ -27,8 +31,20 @@ import re
 import torch
 
 
+def _numpy_safe_globals():
+    import numpy as np
+    try:
+        from numpy._core.multiarray import scalar
+    except ImportError:                     # numpy < 2
+        from numpy.core.multiarray import scalar
+    dtypes = [np.dtype] + [type(np.dtype(t)) for t in (np.float64, np.float32, np.float16, np.int64, np.int32,
+                                                         np.int16, np.int8, np.uint8, np.bool_)]
+    return [scalar] + dtypes
+
+
 def _load(path):
-    return torch.load(path, map_location="cpu", weights_only=True)
+    with torch.serialization.safe_globals(_numpy_safe_globals()):
+        return torch.load(path, map_location="cpu", weights_only=True)
 
 
 def get_all_ckpts(work_dir, steps=None):

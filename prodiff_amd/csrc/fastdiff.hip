@@ -73,6 +73,11 @@ struct fd_model {
   // saves (r01 ab_v16b: 7.41 vs 7.33 ms/step).
   bool kp_side = false;
   int kp_chunk = 0;   // FD_OPT_KP_CHUNK: utterances per kernel-predictor -> LVC chunk (0 = whole batch)
+  // hop >= 64 blocks with a fused upsample (r in {4, 8}) on the skewed persistent kernel
+  // (lvc_skew_bf16_kernel, FD_OPT_LVC_SKEW); lvc_seg overrides its segment length in tiles.
+  bool lvc_skew = false;
+  int lvc_seg = 0;
+  int ncu = 256;      // compute units of the device (one skewed-kernel workgroup each)
   mutable hipStream_t side = nullptr;
   mutable hipEvent_t ev_hidden = nullptr, ev_kp[4] = {}, ev_lvc[4] = {};
   float* pool = nullptr;
@@ -986,6 +991,505 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   }
   LB_STAMP(15);
 #undef TILE
+}
+
+// ------------------------------------------------------------------ skewed persistent LVC block (bf16)
+// All 4 layers of one TimeAware_LVCBlock (modules.py:205-217) with the ConvTranspose
+// upsample in front (always fused), audio_down recomputed from the audio (AUD) and the
+// final conv + sampler update behind (FIN), for hop % 32 == 0, hop >= 64, r in {4, 8}.
+//
+// Why: the whole-block kernel recomputes a 64-row halo on each side of every 384-row
+// tile (25% of its MFMA/VALU work) and each of its short-lived workgroups pays a cold
+// prologue (x_prev, audio, biases, kernel fragments: ~30% of its life) and an epilogue
+// that nothing overlaps.  Here ONE workgroup per CU walks a long time segment of one
+// utterance in steps of W tiles and carries every layer's state from step to step, so
+// no row is computed twice and the next step's operands load under this step.
+//
+// The stencil dependency of layer l on layer l-1 (rows +-(d_l + 1)) is met by a
+// tile-level skew: at step j, stage U (upsample + audio_down) covers local tiles
+// [Wj+1, Wj+W+1), layer l covers [Wj-l, Wj-l+W) and the final-conv stage [Wj-4, Wj).
+// Local tile i belongs to wave i mod W in every stage, so a tile's fp32 state
+// (z = x + a and a, 32 VGPRs) never leaves its wave.  Because the windows shift, a wave
+// holds two tiles for part of a step (slots `c` = the layers' tile, `nx` = the U tile),
+// switched by register moves at a wave-dependent layer.  W = 4 waves, one per SIMD:
+// the 256 architectural VGPRs of a wave hold both tiles' state, the kernel fragments
+// and the accumulators without spilling (8 waves of 256 registers in all cannot).
+// Waves meet only through LDS and 10 barriers per step:
+//   A1 final-conv combine of the previous step, upsample phase GEMMs -> XS, prefetches
+//   A2 x_0 + audio_down -> registers, u_0 = lrelu(z_0) -> ring
+//   B_l pre-conv of layer l (u_l ring -> y buffer)
+//   C_l location-variable conv + gate (y buffer, kernel fragments) -> z, u_{l+1} ring
+// LDS: u rings 4 x (W + 2) tiles (a tile's rows are read by both neighbours), the y
+// buffer, pre-conv weights, an LVC-bias ring, staged x_prev, an audio ring and the
+// final-conv partial sums; the fp32 upsample output XS lives in u-ring slots of layers
+// 1-2 that are dead during A1/A2.  bf16 rows are 64 B with the 16-B chunks XOR-swizzled
+// by (row >> 2) & 3 (conflict-free b128 reads at any row offset).
+// Results equal the whole-block kernel's roundings (same MFMA operands and epilogues)
+// except the final conv, which sums per-row partials (fp32 reassociation only).
+namespace lsw {
+constexpr int W = 4, NTH = 64 * W;                         // tiles per step = waves
+constexpr int RT = W + 2, RR = RT * 32;                    // u-ring tiles / rows per layer
+constexpr int U_LAYER = RR * 64;
+constexpr int U_OFF = 0;
+constexpr int YR = W * 32 + 2;                             // y buffer rows
+constexpr int Y_OFF = U_OFF + NLY * U_LAYER;
+constexpr int YC_OFF = Y_OFF + YR * 64;                    // carries [layer][step parity][2 rows]
+constexpr int WC_OFF = YC_OFF + NLY * 2 * 2 * 64;
+constexpr int BC_OFF = WC_OFF + NLY * 6 * 64 * 16;
+constexpr int BU_OFF = BC_OFF + NLY * CI * 4;
+constexpr int XP_OFF = BU_OFF + CI * 4;
+constexpr int XPR = 32 * W / 4 + 2;                        // staged x_prev rows (32 W / r + 2, r >= 4)
+constexpr int BF_OFF = XP_OFF + XPR * 64;
+constexpr int NF = 8;                                      // LVC-bias ring frames
+constexpr int AUR = 16;                                    // audio ring tiles (>= 2W + 6)
+template <bool AUD, bool FIN> struct Geo {
+  static constexpr int AU_OFF = BF_OFF + NF * NLY * 2 * CI * 4;
+  static constexpr int FW_OFF = AU_OFF + (AUD || FIN ? AUR * 32 * 4 : 0);
+  static constexpr int FF_OFF = FW_OFF + (AUD ? (7 + 1) * 32 * 4 : 0);   // first conv [tap][c] + bias
+  static constexpr int P_OFF = FF_OFF + (FIN ? 7 * 32 * 4 : 0);           // final conv [tap][c]
+  static constexpr int SMEM = P_OFF + (FIN ? RR * 7 * 4 : 0);             // partials, 7 per row
+};
+__device__ __forceinline__ int swz(int row, int chunk) { return ((chunk ^ (row >> 2)) & 3) * 16; }
+}  // namespace lsw
+
+template <bool AUD, bool FIN>
+__global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlockArgs P, int nseg, int seg_tiles) {
+  using namespace lsw;
+  using GG = Geo<AUD, FIN>;
+  static_assert(GG::SMEM <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char sm[GG::SMEM];
+  // the wave index in an SGPR: every tile index and slot decision below is wave-uniform
+  const int tid = threadIdx.x, lane = tid & 63, m = __builtin_amdgcn_readfirstlane(tid >> 6), n = lane & 31,
+            h = lane >> 5;
+  const int b = blockIdx.x / nseg, sg = blockIdx.x - b * nseg;
+  const int Tc = P.Tc, hop = P.hop, Lh = Tc * hop, NTu = Lh >> 5;
+  const int tau0 = sg * seg_tiles, tau1 = min(tau0 + seg_tiles, NTu);
+  if (tau0 >= tau1) return;                          // whole workgroup (uniform)
+  const int sigma = tau0 - 3;                        // global tile of local tile 0 (3 halo tiles)
+  const int nloc = tau1 - sigma;                     // outputs: local tiles [3, nloc)
+  const int J = (nloc + 3) / W + 1;                  // the last final-conv window [W(J-1)-4, W(J-1)+W-4) reaches nloc
+  const long long base = (long long)b * Lh;
+  const int r = P.r, pp = P.p, Tin = Lh / r, ntj = (32 * W / r + 1 + 31) / 32, nph = r / 4;
+  auto gt = [&](int i) { return sigma + i; };        // local -> global tile
+  auto inside = [&](int i) { return gt(i) >= 0 && gt(i) < NTu; };
+  auto frame_of = [&](int i) { return min(max(gt(i) * 32, 0) / hop, Tc - 1); };
+  // LDS addressing
+  auto uoff = [&](int l, int R, int chunk) {         // ring l, local row R (may be negative)
+    const int pr = (R + RR * 16) % RR;
+    return U_OFF + l * U_LAYER + pr * 64 + swz(pr, chunk);
+  };
+  auto yoff = [&](int br, int chunk) { return Y_OFF + br * 64 + swz(br, chunk); };
+  auto xpoff = [&](int row, int chunk) { return XP_OFF + row * 64 + swz(row, chunk); };
+  auto xsoff = [&](int j, int rr, int c4) {          // fp32 upsample output, window row rr, 16-B chunk c4
+    const int half = (rr >> 4) & 1, ring = 1 + half;
+    const int slot = (W * j - ring + 1 + (rr >> 5) + RT * 16) % RT;   // a tile rewritten later this step
+    return U_OFF + ring * U_LAYER + slot * 2048 + (rr & 15) * 128 + ((c4 ^ ((rr & 15) >> 1)) & 7) * 16;
+  };
+  auto aroff = [&](int R) { return GG::AU_OFF + ((R + AUR * 32 * 16) & (AUR * 32 - 1)) * 4; };
+  auto lds4 = [&](int off) -> float4& { return *reinterpret_cast<float4*>(sm + off); };
+  auto ldsb8 = [&](int off) -> bf16x8& { return *reinterpret_cast<bf16x8*>(sm + off); };
+  auto ldsf = [&](int off) -> float& { return *reinterpret_cast<float*>(sm + off); };
+
+  // ---- prologue: zero the state, stage the weights
+  for (int i = tid; i < GG::SMEM / 16; i += NTH) reinterpret_cast<uint4*>(sm)[i] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  for (int i = tid; i < NLY * 6 * 64; i += NTH) {
+    const int l = i / 384, kk = (i >> 6) % 6, ln = i & 63;
+    const __bf16* w = P.Wc[l] + (ln & 31) * 96 + (kk >> 1) * 32 + 16 * (ln >> 5) + 4 * (kk & 1);
+    const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(w), w1 = *reinterpret_cast<const bf16x4*>(w + 8);
+    ldsb8(WC_OFF + i * 16) = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+  }
+  if (tid < NLY * CI) ldsf(BC_OFF + tid * 4) = P.bc[tid / CI][tid % CI];
+  if (tid < CI) ldsf(BU_OFF + tid * 4) = P.bup[tid];
+  if constexpr (AUD) {
+    if (tid < 224) ldsf(GG::FW_OFF + tid * 4) = P.fw[(tid & 31) * 7 + (tid >> 5)];   // fw is [c][tap]
+    if (tid < 32) ldsf(GG::FW_OFF + (224 + tid) * 4) = P.fb[tid];
+  }
+  if constexpr (FIN) {
+    if (tid < 224) ldsf(GG::FF_OFF + tid * 4) = P.wfin[tid];                        // already [tap][c]
+  }
+  const float bfin = FIN ? P.bfin[0] : 0.f;
+  // upsample phase weights: this wave computes phases m and m + 4 (r = 8) on every column
+  // tile; re-loaded (L2-resident) at the end of each step, ahead of the kernel prefetch
+  bf16x8 wup[2][4];
+  auto wup_load = [&]() {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q >= nph) break;
+      const __bf16* wa = P.Wup + ((long long)(m + 4 * q) * 32 + n) * 64 + 8 * h;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wup[q][kk] = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
+    }
+  };
+  wup_load();
+  // per-step operand loads (issued one step ahead, stored to LDS at the end of the step)
+  const float* xprev = P.xin + (long long)b * Tin * CI;
+  const int xpn = 32 * W / r + 2;                    // x_prev rows per step
+  constexpr int IX = (XPR * 8 + NTH - 1) / NTH;      // float4 per thread
+  float4 xv[IX];
+  float av = 0.f;
+  constexpr int IB = (8 * 64 + NTH - 1) / NTH;       // bias float4 per thread (<= 8 frames)
+  float4 bfv[IB];
+  const int nfill = ((W + 4) * 32 + hop - 1) / hop + 1;   // LVC-bias frames a step can touch
+  auto flo = [&](int j) { return max(gt(W * j - 3) * 32, 0) / hop; };
+  auto issue_xprev = [&](int j) {                    // x_prev rows jb .. jb + xpn of step j
+    const int jb = 32 * gt(W * j + 1) / r - 1;
+#pragma unroll
+    for (int it = 0; it < IX; ++it) {
+      const int i = tid + it * NTH, q = (i & 7) * 4, jj = min(max(jb + (i >> 3), 0), Tin - 1);
+      xv[it] = *reinterpret_cast<const float4*>(xprev + (long long)jj * CI + q);
+    }
+  };
+  auto store_xprev = [&](int j) {
+    const int jb = 32 * gt(W * j + 1) / r - 1;
+#pragma unroll
+    for (int it = 0; it < IX; ++it) {
+      const int i = tid + it * NTH, rr = i >> 3, q = (i & 7) * 4, jj = jb + rr;
+      if (rr < xpn) {
+        const float mk = (jj >= 0 && jj < Tin) ? 1.f : 0.f;     // rows outside x_prev are zero
+        const f32x2 u0 = lrelu2(f32x2{xv[it].x, xv[it].y} * mk), u1 = lrelu2(f32x2{xv[it].z, xv[it].w} * mk);
+        *reinterpret_cast<bf16x4*>(sm + xpoff(rr, q >> 3) + (q & 7) * 2) =
+            bf16x4{(__bf16)u0.x, (__bf16)u0.y, (__bf16)u1.x, (__bf16)u1.y};
+      }
+    }
+  };
+  auto issue_audio = [&](int t0tile) {               // AUD / FIN: W tiles of samples from local tile t0tile
+    if (tid < 32 * W) {
+      const int t = gt(t0tile) * 32 + tid;
+      av = P.audio[base + min(max(t, 0), Lh - 1)];
+    }
+  };
+  auto store_audio = [&](int t0tile) {
+    if (tid < 32 * W) {
+      const int t = gt(t0tile) * 32 + tid;
+      ldsf(aroff(t0tile * 32 + tid)) = (t >= 0 && t < Lh) ? av : 0.f;
+    }
+  };
+  auto issue_bias = [&](int j) {                     // frames flo(j) .. + 8, 64 float4 each
+#pragma unroll
+    for (int q = 0; q < IB; ++q) {
+      const int i = tid + q * NTH, fr = flo(j) + (i >> 6), c = (i & 63) * 4;
+      bfv[q] = *reinterpret_cast<const float4*>(P.Bf + ((long long)b * Tc + min(fr, Tc - 1)) * (2 * CI * NLY) + c);
+    }
+  };
+  auto store_bias = [&](int j) {
+#pragma unroll
+    for (int q = 0; q < IB; ++q) {
+      const int i = tid + q * NTH, fr = flo(j) + (i >> 6), c = (i & 63) * 4;
+      if ((i >> 6) < nfill) {
+        // gate pre-scale (the accumulators are exp2 arguments); frames past the end are zero
+        const float sc = fr >= Tc ? 0.f : (c & 63) < 32 ? -LOG2E : 2.f * LOG2E;
+        lds4(BF_OFF + ((fr % NF) * 256 + c) * 4) = make_float4(bfv[q].x * sc, bfv[q].y * sc, bfv[q].z * sc, bfv[q].w * sc);
+      }
+    }
+  };
+  // kernel fragments of (layer, local tile), frame-major fragment order (kp_kernel_bf16_kernel)
+  bf16x8 kn[12];
+  auto kload = [&](int l, int i) {
+    const __bf16* kq = P.Kf[l] + ((long long)b * Tc + frame_of(i)) * KPERLAYER;
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk) kn[kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+  };
+  // audio_down of the U tile (non-AUD: loaded one step ahead, C layout)
+  float4 apf[4];
+  auto issue_a = [&](int i) {
+    const int t = min(max(gt(i) * 32 + n, 0), Lh - 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) apf[q] = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + 8 * q + 4 * h);
+  };
+  // this wave's tile in stage U / layer l at step j
+  auto iU = [&](int j) { return W * j + (m == 0 ? W : m); };
+  auto iL = [&](int j, int l) { return W * j + m - (m + l >= W ? W : 0); };
+
+  // step-0 operands
+  issue_xprev(0);
+  if constexpr (AUD || FIN) {
+    // tiles [-4, W + 2): step 0's final-conv window and audio_down taps
+    for (int i = tid; i < (W + 6) * 32; i += NTH) {
+      const int t = gt(-4) * 32 + i;
+      ldsf(aroff(-4 * 32 + i)) = (t >= 0 && t < Lh) ? P.audio[base + min(max(t, 0), Lh - 1)] : 0.f;
+    }
+  }
+  issue_bias(0);
+  if constexpr (!AUD) issue_a(iU(0));
+  kload(0, iL(0, 0));
+  store_xprev(0);
+  store_bias(0);
+  __syncthreads();
+
+  // fp32 state: the layers' tile (c) and the U tile (nx)
+  f32x2 cz[8], ca[8], nz[8], na[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) { cz[p] = ca[p] = nz[p] = na[p] = f32x2{0.f, 0.f}; }
+  auto swap_slots = [&]() {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const f32x2 tz = cz[p], ta = ca[p];
+      cz[p] = nz[p]; ca[p] = na[p]; nz[p] = tz; na[p] = ta;
+    }
+  };
+  auto take_next = [&]() {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) { cz[p] = nz[p]; ca[p] = na[p]; }
+  };
+
+  // final-conv combine of step jf's window: eps(t) = b + sum_tap P(t + tap - 3)[tap];
+  // audio_out = (x_t - ce eps) / den + sig z   (FastDiff_model.py:100, util.py:222-226)
+  auto fin_combine = [&](int jf) {
+    if (tid < 32 * W) {
+      const int R = 32 * (W * jf - 4) + tid, i = R >> 5, t = 32 * sigma + R;
+      if (i >= 3 && i < nloc && t >= 0 && t < Lh) {
+        float e = 0.f;
+#pragma unroll
+        for (int tap = 0; tap < 7; ++tap) e += ldsf(GG::P_OFF + (((R + tap - 3 + RR * 16) % RR) * 7 + tap) * 4);
+        e += bfin;
+        float v = (ldsf(aroff(R)) - P.ce * e) / P.den;
+        if (P.sig != 0.f)
+          v += P.sig * (P.noise ? P.noise[base + t]
+                                : philox_normal(P.seed, (unsigned long long)((long long)(b + P.b_off) * Lh + t), P.stream));
+        P.audio_out[base + t] = v;
+      }
+    }
+  };
+
+  for (int j = 0; j < J; ++j) {
+    // ================= A1: previous final conv, upsample phase GEMMs -> XS, next-step loads
+    if constexpr (FIN) {
+      if (j > 0) fin_combine(j - 1);
+    }
+    // C^T[co][col] = [W_k^T | W_{k+r}^T] . [xp(j0); xp(j0 - 1)],  t = r j0 + k - p  (modules.py:205-206)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q >= nph) break;
+      const int k = m + 4 * q;
+      for (int jt = 0; jt < ntj; ++jt) {
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int row = min(jt * 32 + n + (kk < 2 ? 1 : 0), XPR - 1);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wup[q][kk], ldsb8(xpoff(row, 2 * (kk & 1) + h)), acc, 0, 0, 0);
+        }
+        // column c' = jt*32 + n is input j0 = T0 / r + c' (XP row c' + 1): window row t - T0 = r c' + k - p
+        const int rw = r * (jt * 32 + n) + k - pp;
+        if (rw >= 0 && rw < 32 * W) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4 bv = lds4(BU_OFF + (8 * g + 4 * h) * 4);
+            lds4(xsoff(j, rw, 2 * g + h)) =
+                make_float4(acc[4 * g] + bv.x, acc[4 * g + 1] + bv.y, acc[4 * g + 2] + bv.z, acc[4 * g + 3] + bv.w);
+          }
+        }
+      }
+    }
+    if (j + 1 < J) {
+      issue_xprev(j + 1);
+      issue_bias(j + 1);
+      if constexpr (AUD || FIN) issue_audio(W * j + W + 2);
+    }
+    __syncthreads();
+    // ================= A2: z_0 = upsample + audio_down of the U tile, u_0 ring
+    {
+      const int iu = iU(j), q = iu - W * j - 1, R = 32 * iu + n;
+      f32x2 x0[8], a0[8];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 xv4 = lds4(xsoff(j, 32 * q + n, 2 * g + h));
+        float4 a4;
+        if constexpr (AUD) {
+          // a0[t][c] = b[c] + sum_tap w[c][tap] audio[t + tap - 3]  (first_conv_kernel's order)
+          float sa[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) sa[c] = ldsf(GG::FW_OFF + (224 + 8 * g + 4 * h + c) * 4);
+#pragma unroll
+          for (int tap = 0; tap < 7; ++tap) {
+            const float au = ldsf(aroff(R + tap - 3));
+            const float4 w = lds4(GG::FW_OFF + (tap * 32 + 8 * g + 4 * h) * 4);
+            sa[0] = fmaf(w.x, au, sa[0]); sa[1] = fmaf(w.y, au, sa[1]);
+            sa[2] = fmaf(w.z, au, sa[2]); sa[3] = fmaf(w.w, au, sa[3]);
+          }
+          a4 = make_float4(sa[0], sa[1], sa[2], sa[3]);
+        } else {
+          a4 = apf[g];
+        }
+        x0[2 * g] = f32x2{xv4.x + a4.x, xv4.y + a4.y}; x0[2 * g + 1] = f32x2{xv4.z + a4.z, xv4.w + a4.w};
+        a0[2 * g] = f32x2{a4.x, a4.y}; a0[2 * g + 1] = f32x2{a4.z, a4.w};
+      }
+      const bool in = inside(iu);
+      bf16x8 u0, u1;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const f32x2 v0 = in ? lrelu2(x0[p]) : f32x2{0.f, 0.f}, v1 = in ? lrelu2(x0[4 + p]) : f32x2{0.f, 0.f};
+        u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
+        u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
+      }
+      ldsb8(uoff(0, R, 2 * h)) = u0;
+      ldsb8(uoff(0, R, 2 * h + 1)) = u1;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) { nz[p] = x0[p]; na[p] = a0[p]; }
+      // wave 0's U tile is next step's; waves m >= 1 start this step's layers on it, and
+      // keep their older tile (layers >= W - m) in `nx` until then
+      if (m >= 1) swap_slots();
+    }
+    __syncthreads();
+    // ================= layers
+#pragma unroll 1
+    for (int l = 0; l < NLY; ++l) {
+      const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
+      const int i = iL(j, l), w = (m + l) % W;       // tile, window position (window at Wj - l)
+      if (l > 0 && m >= 1 && l == W - m) swap_slots();   // the older tile takes over
+      if constexpr (!AUD) {
+        if (l == 0 && j + 1 < J) issue_a(iU(j + 1));
+      }
+      // ---- B_l: y rows [32i+1, 32i+33) = lrelu(W_c . [u(t-d); u(t); u(t+d)] + b) -> y rows 32w+2..
+      {
+        f32x16 acc;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const int tap = kk >> 1;
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ldsb8(WC_OFF + ((l * 6 + kk) * 64 + lane) * 16),
+                                                        ldsb8(uoff(l, 32 * i + 1 + n + (tap - 1) * d, 2 * (kk & 1) + h)),
+                                                        acc, 0, 0, 0);
+        }
+        f32x2 v[8];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = lds4(BC_OFF + (l * CI + 8 * g + 4 * h) * 4);
+          v[2 * g] = lrelu2(f32x2{acc[4 * g], acc[4 * g + 1]} + f32x2{bv.x, bv.y});
+          v[2 * g + 1] = lrelu2(f32x2{acc[4 * g + 2], acc[4 * g + 3]} + f32x2{bv.z, bv.w});
+        }
+        const int tt = 32 * gt(i) + 1;                // global time of this preconv tile's row 0
+        if (tt < 0 || tt + 31 >= Lh) {                // utterance-edge tile: the LVC zero-pads y
+          const int t = tt + n;
+          const bool in = t >= 0 && t < Lh;
+#pragma unroll
+          for (int p = 0; p < 8; ++p) v[p] = in ? v[p] : f32x2{0.f, 0.f};
+        }
+        bf16x8 y0, y1;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          y0[2 * p] = (__bf16)v[p].x; y0[2 * p + 1] = (__bf16)v[p].y;
+          y1[2 * p] = (__bf16)v[4 + p].x; y1[2 * p + 1] = (__bf16)v[4 + p].y;
+        }
+        const int br = 32 * w + 2 + n;
+        ldsb8(yoff(br, 2 * h)) = y0;
+        ldsb8(yoff(br, 2 * h + 1)) = y1;
+        if (w == W - 1 && n >= 30) {                  // rows 32W, 32W + 1: the next step's rows 0, 1
+          const int co = YC_OFF + ((l * 2 + (j & 1)) * 2 + (n - 30)) * 64;
+          *reinterpret_cast<bf16x8*>(sm + co + swz(br, 2 * h)) = y0;
+          *reinterpret_cast<bf16x8*>(sm + co + swz(br, 2 * h + 1)) = y1;
+        }
+        if (w == 0 && lane < 8) {                     // rows 0, 1 from the previous step
+          const int ci = YC_OFF + ((l * 2 + ((j + 1) & 1)) * 2) * 64 + lane * 16;
+          *reinterpret_cast<uint4*>(sm + Y_OFF + lane * 16) = *reinterpret_cast<const uint4*>(sm + ci);
+        }
+      }
+      __syncthreads();
+      // ---- C_l: o^T = K_frame . [y(t-1); y(t); y(t+1)]^T + Bf;  z += gate(o) (+ a)
+      {
+        f32x16 g, f;
+        {
+          const float* bq = reinterpret_cast<const float*>(sm + BF_OFF) + ((frame_of(i) % NF) * NLY + l) * 2 * CI;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * q + 4 * h);
+            const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * q + 4 * h);
+            g[4 * q] = bg.x; g[4 * q + 1] = bg.y; g[4 * q + 2] = bg.z; g[4 * q + 3] = bg.w;
+            f[4 * q] = bl.x; f[4 * q + 1] = bl.y; f[4 * q + 2] = bl.z; f[4 * q + 3] = bl.w;
+          }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const bf16x8 yb = ldsb8(yoff(32 * w + (kk >> 1) + n, 2 * (kk & 1) + h));
+          g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g, 0, 0, 0);
+          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f, 0, 0, 0);
+        }
+        // next LVC's kernel fragments, in flight under the gate, the next pre-conv and barriers
+        // (issued once these chains have read their fragments)
+        __builtin_amdgcn_sched_barrier(0);
+        if (l + 1 < NLY) {
+          kload(l + 1, iL(j, l + 1));
+        } else if (j + 1 < J) {
+          wup_load();
+          kload(0, iL(j + 1, 0));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 o0 = gate2s(f32x2{g[4 * q], g[4 * q + 1]}, f32x2{f[4 * q], f[4 * q + 1]});
+          const f32x2 o1 = gate2s(f32x2{g[4 * q + 2], g[4 * q + 3]}, f32x2{f[4 * q + 2], f[4 * q + 3]});
+          if (l + 1 < NLY) {
+            cz[2 * q] += ca[2 * q] + o0;
+            cz[2 * q + 1] += ca[2 * q + 1] + o1;
+          } else {
+            cz[2 * q] += o0;
+            cz[2 * q + 1] += o1;
+          }
+        }
+        const bool in = inside(i);
+        if (l + 1 < NLY) {
+          bf16x8 u0, u1;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const f32x2 v0 = in ? lrelu2(cz[p]) : f32x2{0.f, 0.f}, v1 = in ? lrelu2(cz[4 + p]) : f32x2{0.f, 0.f};
+            u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
+            u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
+          }
+          ldsb8(uoff(l + 1, 32 * i + n, 2 * h)) = u0;
+          ldsb8(uoff(l + 1, 32 * i + n, 2 * h + 1)) = u1;
+        } else if constexpr (FIN) {
+          // per-row partial sums of the final conv: P[t][tap] = sum_c w[tap][c] x4[t][c]
+          float sv[7];
+#pragma unroll
+          for (int tap = 0; tap < 7; ++tap) {
+            float acc = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 wf = lds4(GG::FF_OFF + (tap * 32 + 8 * q + 4 * h) * 4);
+              acc = fmaf(wf.x, cz[2 * q].x, fmaf(wf.y, cz[2 * q].y, fmaf(wf.z, cz[2 * q + 1].x, fmaf(wf.w, cz[2 * q + 1].y, acc))));
+            }
+            acc += __shfl_xor(acc, 32);
+            sv[tap] = in ? acc : 0.f;                 // the final conv zero-pads x outside the utterance
+          }
+          const int po = GG::P_OFF + (((32 * i + n + RR * 16) % RR) * 7) * 4;
+          if (h == 0) {
+#pragma unroll
+            for (int tap = 0; tap < 4; ++tap) ldsf(po + tap * 4) = sv[tap];
+          } else {
+#pragma unroll
+            for (int tap = 4; tap < 7; ++tap) ldsf(po + tap * 4) = sv[tap];
+          }
+        } else {
+          const int t = 32 * gt(i) + n;
+          if (i >= 3 && i < nloc && in) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              *reinterpret_cast<float4*>(P.xout + (base + t) * CI + 8 * q + 4 * h) =
+                  make_float4(cz[2 * q].x, cz[2 * q].y, cz[2 * q + 1].x, cz[2 * q + 1].y);
+          }
+        }
+        if (l == NLY - 1 && j + 1 < J) {             // the next step's staged operands
+          store_xprev(j + 1);
+          store_bias(j + 1);
+          if constexpr (AUD || FIN) store_audio(W * j + W + 2);
+        }
+      }
+      __syncthreads();
+    }
+    take_next();                                     // the U tile becomes the layers' tile
+  }
+  if constexpr (FIN) fin_combine(J - 1);
+}
+
+// Workgroups per utterance for the skewed kernel: about one per CU over the batch, at
+// least 8 tiles each.
+void lvc_skew_segments(int NTu, int B, int ncu, int seg_override, int* nseg, int* seg_tiles) {
+  const int s = seg_override > 0 ? cdiv(NTu, seg_override) : std::max(1, std::min((ncu + B - 1) / B, NTu / 8));
+  *seg_tiles = cdiv(NTu, s);
+  *nseg = cdiv(NTu, *seg_tiles);
 }
 
 // ------------------------------------------------------------------ streaming LVC block (bf16)
@@ -2359,7 +2863,20 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream;
       }
       // (the LDS image holds upsample weights for r <= 4 with the audio fusions, r <= 8 without)
-      if (stream_path) {
+      const bool skew_path = !stream_path && m->lvc_skew && ups && hop % 32 == 0 && hop >= 64 && (r == 4 || r == 8);
+      if (skew_path) {
+        ProfScope ps(fuse_fin ? "fd_lvc_block_final" : "fd_lvc_block_ups", st);
+        int nseg = 1, seg_tiles = 1;
+        lvc_skew_segments((int)(Tout / 32), nbk, m->ncu, m->lvc_seg, &nseg, &seg_tiles);
+        const dim3 grid(nbk * nseg);
+        if (last && aud && fuse_fin)
+          hipLaunchKernelGGL((lvc_skew_bf16_kernel<true, true>), grid, dim3(lsw::NTH), 0, st, la, nseg, seg_tiles);
+        else if (last && aud)
+          hipLaunchKernelGGL((lvc_skew_bf16_kernel<true, false>), grid, dim3(lsw::NTH), 0, st, la, nseg, seg_tiles);
+        else
+          hipLaunchKernelGGL((lvc_skew_bf16_kernel<false, false>), grid, dim3(lsw::NTH), 0, st, la, nseg, seg_tiles);
+        PD_LAUNCH_CHECK();
+      } else if (stream_path) {
         // streaming pipeline: one long time range per workgroup (lvc_stream_bf16_kernel)
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : "fd_lvc_block_ups", st);
         const int Lh = (int)Tout, seg = lvc_stream_seg(Lh, nbk);
@@ -2467,6 +2984,12 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   PD_CHECK_ARG(dims->num_blocks >= 1 && dims->num_blocks <= 4, "num_blocks in [1,4]");
   hipStream_t st = (hipStream_t)stream;
   fd_model* m = new fd_model();
+  {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+      m->ncu = ncu;
+  }
   m->nblocks = dims->num_blocks;
   m->dtype = dtype;
   int hop = 1;
@@ -2640,6 +3163,11 @@ int fd_set_option(fd_model* m, int option, int value) {
     case FD_OPT_KP_CHUNK:
       PD_CHECK_ARG(value >= 0, "FD_OPT_KP_CHUNK >= 0");
       m->kp_chunk = value;
+      return PD_OK;
+    case FD_OPT_LVC_SKEW: m->lvc_skew = value != 0; return PD_OK;
+    case FD_OPT_LVC_SEG:
+      PD_CHECK_ARG(value >= 0, "FD_OPT_LVC_SEG >= 0");
+      m->lvc_seg = value;
       return PD_OK;
     default: break;
   }

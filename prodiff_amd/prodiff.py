@@ -91,10 +91,16 @@ class WaveNet(nn.Module):
                 self.output_projection.weight, self.output_projection.bias]
         return out
 
+    def param_signature(self):
+        """What the packed handle depends on: dtype, options and every parameter's storage
+        and version (load_state_dict / in-place updates change it)."""
+        ps = self.ordered_params()
+        return (self.compute_dtype, tuple(sorted(self._options.items()))) + tuple((p.data_ptr(), p._version) for p in ps)
+
     def handle(self):
         """The packed C handle; re-packed whenever a parameter is replaced or modified."""
         ps = self.ordered_params()
-        sig = (self.compute_dtype, tuple(sorted(self._options.items()))) + tuple((p.data_ptr(), p._version) for p in ps)
+        sig = self.param_signature()
         if self._h is not None and sig == self._sig:
             return self._h
         L = _lib.lib()
@@ -152,13 +158,25 @@ class WaveNet(nn.Module):
 
 
 class SampleGraph:
-    """A captured sampler (``GaussianDiffusion.capture``): static input, static output."""
+    """A captured sampler (``GaussianDiffusion.capture``): static input, static output.
 
-    def __init__(self, graph, cond, mel, keep=()):
+    The graph bakes in device addresses: its own workspace and the draw buffers (held
+    here), and the WaveNet handle's packed weight pool.  The handle is owned by the
+    denoiser and re-packed (the old pool freed) when its parameters, dtype or options
+    change, so ``replay`` refuses to run once the denoiser no longer matches the capture."""
+
+    def __init__(self, graph, cond, mel, denoiser, keep=()):
         self.graph, self.cond, self.mel = graph, cond, mel
-        self._keep = keep        # captured draw buffers stay alive with the graph
+        self._denoiser = denoiser
+        self._handle = denoiser._h.value
+        self._sig = denoiser.param_signature()
+        self._keep = keep        # workspace and captured draw buffers stay alive with the graph
 
     def replay(self):
+        d = self._denoiser
+        if d._h is None or d._h.value != self._handle or d.param_signature() != self._sig:
+            raise RuntimeError("SampleGraph: the denoiser was re-packed or its parameters changed "
+                               "since capture; capture again")
         self.graph.replay()
         return self.mel
 
@@ -211,13 +229,14 @@ class GaussianDiffusion(nn.Module):
         return self._coef_cache[1:]
 
     @torch.no_grad()
-    def sample(self, cond, infer_step=4, x_T=None, noise=None, seed=None):
+    def sample(self, cond, infer_step=4, x_T=None, noise=None, seed=None, workspace=None):
         """cond [B,T,H] -> mel [B,T,M].
 
         x_T: [B,1,M,T] draw (reference layout, prodiff.py:147) or None;
         noise: [S,B,1,M,T] per-step draws in sampling order, or None.
         Missing draws come from the on-device Philox generator keyed by ``seed``
-        (default: drawn from torch's CPU generator, so torch.manual_seed applies)."""
+        (default: drawn from torch's CPU generator, so torch.manual_seed applies).
+        ``workspace``: a ``_lib.Workspace`` to use instead of the module's own (capture)."""
         if not isinstance(self.denoise_fn, WaveNet):
             raise TypeError("GaussianDiffusion needs a prodiff_amd.WaveNet denoise_fn")
         B, T, H = cond.shape
@@ -236,7 +255,7 @@ class GaussianDiffusion(nn.Module):
         mel = torch.empty(B, T, M, device=dev, dtype=torch.float32)
         L = _lib.lib()
         nbytes = L.pd_wavenet_workspace_size(h, B, T, S)
-        ws, wsb = self._ws.get(nbytes, dev)
+        ws, wsb = (workspace or self._ws).get(nbytes, dev)
         _lib.check(L.pd_prodiff_sample(h, _lib.fptr(cond), _lib.farr(c1), _lib.farr(c2), _lib.farr(sg), S,
                                        _lib.fptr(xT), _lib.fptr(nz), seed, _lib.fptr(mel), B, T, ws, wsb,
                                        _lib.stream_ptr(dev)))
@@ -257,13 +276,14 @@ class GaussianDiffusion(nn.Module):
         cond = cond.float().contiguous()
         xT = None if x_T is None else x_T.float().contiguous().clone()
         nz = None if noise is None else noise.float().contiguous().clone()
-        self.sample(cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz)   # packs weights, sizes the workspace
+        ws = _lib.Workspace()    # the graph's own: later eager calls may grow (reallocate) self._ws
+        self.sample(cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz, workspace=ws)   # packs, sizes ws
         torch.cuda.synchronize()
         static_cond = cond.clone()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            mel = self.sample(static_cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz)
-        return SampleGraph(g, static_cond, mel, keep=(xT, nz))
+            mel = self.sample(static_cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz, workspace=ws)
+        return SampleGraph(g, static_cond, mel, self.denoise_fn, keep=(ws, xT, nz))
 
     def forward(self, cond, src_spec=None, gt_spec=None, infer_step=4, infer=False):
         if not infer:

@@ -98,6 +98,19 @@ class _Opaque:
     pass
 
 
+def test_load_ckpt_numpy_scalar_metadata(tmp_path):
+    """A resumed reference training checkpoint stores checkpoint_callback_best as a numpy
+    scalar (np.load(best_valid.npy)[0], utils/pl_utils.py:321,751; dumped by
+    handler/train/handler.py:389-402): the weights-only loader accepts numpy scalars/dtypes."""
+    sd = _wn_sd(6)
+    _save(tmp_path / "model_ckpt_steps_9.ckpt",
+          {"epoch": 3, "global_step": 9, "checkpoint_callback_best": np.float64(0.1234),
+           "best_int": np.int64(7), "optimizer_states": [{}], "state_dict": {"model." + k: v for k, v in sd.items()}})
+    net = WaveNet(80, 32, 4, 64, 2)
+    load_ckpt(net, str(tmp_path), "model")
+    assert all(torch.equal(net.state_dict()[k], v) for k, v in sd.items())
+
+
 # ---------------------------------------------------------------- vocoder layouts
 FASTDIFF_CONFIG = dict(audio_channels=1, inner_channels=32, cond_channels=80, upsample_ratios=[8, 8, 4],
                        lvc_layers_each_block=4, lvc_kernel_size=3, kpnet_hidden_channels=64, kpnet_conv_size=3,

@@ -161,3 +161,23 @@ def test_cond_create_rejects_bad_dims():
     assert lib.pd_cond_create(_lib.C.byref(d), None, 0, None, _lib.C.byref(h)) != 0
     d = _lib.pd_cond_dims(40, 256, 4, 9, 2, 1, 0, 1, 1, 1, 0, 0, 0)   # gender without lang_embed
     assert lib.pd_cond_num_params(_lib.C.byref(d)) > 0
+
+
+def test_bench_traffic_keyed_by_workload(tmp_path):
+    """bench.py takes `roofline.traffic` only from a PMC summary of the same workload: a C4
+    line (32 utterances per GPU) must not carry a C3 (8 per GPU) measurement."""
+    import json
+    import bench
+    f = tmp_path / "r09_v1_traffic.json"
+    sym = "void (anonymous namespace)::lvc_skew_bf16_kernel<true, true>((anonymous namespace)::LvcBlockArgs, int, int)"
+    json.dump({"bench_tag": "fd_lvc_block_final", "config": "C3", "batch": 8, "frames": 861,
+               "kernels": {sym: {"traffic_bytes_per_launch": 1.0e8, "launches": 4}}}, open(f, "w"))
+    assert bench.pmc_traffic("fd_lvc_block_final", "C3", 8, 861, str(f))[0] == 1.0e8
+    assert bench.pmc_traffic("fd_lvc_block_final", "C4", 32, 861, str(f)) == (None, None)
+    assert bench.pmc_traffic("fd_lvc_block_final", "C3", 8, 100, str(f)) == (None, None)
+    # legacy (pre-r03) summaries are C3 8 x 861 unless named *c5*
+    assert bench.traffic_workload({}, "profiles/r02_v4_traffic.json") == ("C3", 8, 861)
+    assert bench.traffic_workload({}, "profiles/r02_v4c5_traffic.json") == ("C5", 8, 861)
+    # the committed summaries never serve a C4 line
+    for tag in bench.TAG_KERNEL:
+        assert bench.pmc_traffic(tag, "C4", 32, 861) == (None, None)

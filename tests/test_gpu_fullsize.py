@@ -86,6 +86,27 @@ def test_c2_prodiff_fullsize_fp32():
     np.testing.assert_allclose(g.replay().cpu().numpy(), ref2.cpu().numpy(), rtol=0, atol=1e-6)
 
 
+def test_sample_graph_owns_its_workspace():
+    """A captured sampler keeps its own workspace: an eager sample() at a larger shape grows
+    (reallocates) the module's workspace but leaves the graph's buffers alone, so the replay
+    still reproduces the capture; once the denoiser's parameters change (re-pack frees the
+    old weight pool) replay() refuses to run (prodiff.py SampleGraph)."""
+    gd = prodiff(11)
+    B, T = 1, 64
+    cond = tt(synth.synth_inputs(501, (B, T, 256)))
+    xT, nz = prodiff_draws(11, B, T)
+    g = gd.capture(cond, x_T=tt(xT), noise=tt(nz))
+    first = g.replay().clone()
+    big = tt(synth.synth_inputs(502, (4, 3 * T, 256)))
+    gd.sample(big, seed=3)                               # grows gd._ws past the captured size
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(g.replay().cpu().numpy(), first.cpu().numpy())
+    with torch.no_grad():
+        gd.denoise_fn.input_projection.bias.add_(0.01)   # parameters change -> handle re-pack
+    with pytest.raises(RuntimeError):
+        g.replay()
+
+
 @pytest.fixture(scope="module")
 def c3():
     return G.load("fullsize_c3_b2")

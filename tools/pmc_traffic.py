@@ -1,6 +1,10 @@
 """Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM traffic.
 
-    python tools/pmc_traffic.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <out.json> <bench-tag>
+    python tools/pmc_traffic.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <out.json> <bench-tag> \
+        [<config> <per-GPU batch> <frames>]          (default C3 8 861)
+
+The workload is recorded in the summary: bench.py only takes `traffic` from a summary
+of the same config, batch and frames as the line it prints.
 
 Units and corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
 counters are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B per
@@ -27,6 +31,7 @@ def load(path):
 
 def main():
     src, out, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    config, batch, frames = (sys.argv[4], int(sys.argv[5]), int(sys.argv[6])) if len(sys.argv) > 6 else ("C3", 8, 861)
     fetch = load(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"))
     write = load(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"))
     per_grid, tot = [], defaultdict(lambda: [0.0, 0])
@@ -39,7 +44,7 @@ def main():
         t = tot[name]
         t[0] += (f + w) * len(fetch[key])
         t[1] += len(fetch[key])
-    res = {"bench_tag": tag, "units": "bytes per launch (FETCH_SIZE KiB x1024 x2 + WRITE_SIZE KiB x1024)",
+    res = {"bench_tag": tag, "config": config, "batch": batch, "frames": frames, "units": "bytes per launch (FETCH_SIZE KiB x1024 x2 + WRITE_SIZE KiB x1024)",
            "per_grid": per_grid,
            "kernels": {k: {"traffic_bytes_per_launch": v[0] / v[1], "launches": v[1]} for k, v in tot.items()}}
     with open(out, "w") as f:
