@@ -996,7 +996,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
 // ------------------------------------------------------------------ skewed persistent LVC block (bf16)
 // All 4 layers of one TimeAware_LVCBlock (modules.py:205-217) with the ConvTranspose
 // upsample in front (always fused), audio_down recomputed from the audio (AUD) and the
-// final conv + sampler update behind (FIN), for hop % 32 == 0, hop >= 64, r in {4, 8}.
+// final conv + sampler update behind (FIN), for hop a power of 2 >= 64, r in {4, 8}.
 //
 // Why: the whole-block kernel recomputes a 64-row halo on each side of every 384-row
 // tile (25% of its MFMA/VALU work) and each of its short-lived workgroups pays a cold
@@ -1008,12 +1008,16 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
 // The stencil dependency of layer l on layer l-1 (rows +-(d_l + 1)) is met by a
 // tile-level skew: at step j, stage U (upsample + audio_down) covers local tiles
 // [Wj+1, Wj+W+1), layer l covers [Wj-l, Wj-l+W) and the final-conv stage [Wj-4, Wj).
-// Local tile i belongs to wave i mod W in every stage, so a tile's fp32 state
-// (z = x + a and a, 32 VGPRs) never leaves its wave.  Because the windows shift, a wave
-// holds two tiles for part of a step (slots `c` = the layers' tile, `nx` = the U tile),
-// switched by register moves at a wave-dependent layer.  W = 4 waves, one per SIMD:
-// the 256 architectural VGPRs of a wave hold both tiles' state, the kernel fragments
-// and the accumulators without spilling (8 waves of 256 registers in all cannot).
+// Local tile i belongs to wave pair i mod W in every stage; the pair splits the 32
+// residual channels (wave 2p + c owns channels 16c .. 16c+15), so a tile's fp32 state
+// (z = x + a and a) never leaves its waves.  The split is free for the location-variable
+// conv: a channel half's gate and filter rows of the frame kernel form one 32-row MFMA
+// operand (6 fragments per wave, no kernel byte loaded twice), and its accumulator holds
+// matching gate/filter pairs.  The pre-conv output (all 32 channels feed every LVC) is
+// split the same way on 16x16x32 MFMAs.  8 waves = 2 per SIMD, so one wave's MFMAs
+// overlap its partner's gate VALU and each one's LDS/barrier waits.
+// Because the windows shift, a pair holds two tiles for part of a step (slots `c` = the
+// layers' tile, `nx` = the U tile), switched by register moves at a pair-dependent layer.
 // Waves meet only through LDS and 10 barriers per step:
 //   A1 final-conv combine of the previous step, upsample phase GEMMs -> XS, prefetches
 //   A2 x_0 + audio_down -> registers, u_0 = lrelu(z_0) -> ring
@@ -1021,46 +1025,71 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
 //   C_l location-variable conv + gate (y buffer, kernel fragments) -> z, u_{l+1} ring
 // LDS: u rings 4 x (W + 2) tiles (a tile's rows are read by both neighbours), the y
 // buffer, pre-conv weights, an LVC-bias ring, staged x_prev, an audio ring and the
-// final-conv partial sums; the fp32 upsample output XS lives in u-ring slots of layers
-// 1-2 that are dead during A1/A2.  bf16 rows are 64 B with the 16-B chunks XOR-swizzled
-// by (row >> 2) & 3 (conflict-free b128 reads at any row offset).
-// Results equal the whole-block kernel's roundings (same MFMA operands and epilogues)
-// except the final conv, which sums per-row partials (fp32 reassociation only).
+// final-conv partial sums (one plane per channel half); the fp32 upsample output XS lives
+// in u-ring slots of layers 1-2 that are dead during A1/A2.  bf16 rows are 64 B with the
+// 16-B chunks XOR-swizzled by (row >> 2) & 3 (conflict-free b128 reads at any row offset).
+// Results equal the whole-block kernel's roundings up to fp32 summation order (the
+// accumulators start from the LVC bias as in its prefetch variant; the final conv sums
+// per-row partials).
 namespace lsw {
-constexpr int W = 4, NTH = 64 * W;                         // tiles per step = waves
-constexpr int RT = W + 2, RR = RT * 32;                    // u-ring tiles / rows per layer
-constexpr int U_LAYER = RR * 64;
+constexpr int W = 4, NWV = 2 * W, NTH = 64 * NWV;          // tiles per step; a wave pair per tile
+constexpr int RT = W + 2;                                  // u-ring tiles per layer
+// Every ring is stored with a mirror tile at each end (physical slots 0 .. RT + 1: slot
+// (i mod RT) + 1 holds tile i, slot 0 repeats slot RT, slot RT + 1 repeats slot 1), so the
+// rows a tile's pre-conv reads (-28 .. +60 around it) are contiguous: one address per
+// lane plus immediate offsets, no per-lane wrap.
+constexpr int RP = RT + 2;
+constexpr int LDB = 80;                                    // bytes per bf16 row: 32 channels + 16 B pad
+constexpr int TB = 32 * LDB;                               // bytes per tile
+constexpr int U_LAYER = RP * TB;
 constexpr int U_OFF = 0;
 constexpr int YR = W * 32 + 2;                             // y buffer rows
 constexpr int Y_OFF = U_OFF + NLY * U_LAYER;
-constexpr int YC_OFF = Y_OFF + YR * 64;                    // carries [layer][step parity][2 rows]
-constexpr int WC_OFF = YC_OFF + NLY * 2 * 2 * 64;
+constexpr int YC_OFF = Y_OFF + YR * LDB;                   // carries [layer][step parity][2 rows]
+constexpr int WC_OFF = YC_OFF + NLY * 2 * 2 * LDB;
 constexpr int BC_OFF = WC_OFF + NLY * 6 * 64 * 16;
 constexpr int BU_OFF = BC_OFF + NLY * CI * 4;
 constexpr int XP_OFF = BU_OFF + CI * 4;
-constexpr int XPR = 32 * W / 4 + 2;                        // staged x_prev rows (32 W / r + 2, r >= 4)
-constexpr int BF_OFF = XP_OFF + XPR * 64;
+constexpr int XPR = 66;                                    // staged x_prev rows (32 W / r + 2 used; + the
+                                                           // unused columns' reads, so no clamp)
+constexpr int BF_OFF = XP_OFF + XPR * LDB;
+constexpr int XLD = 144;                                   // bytes per fp32 XS row (32 channels + pad)
 constexpr int NF = 8;                                      // LVC-bias ring frames
-constexpr int AUR = 16;                                    // audio ring tiles (>= 2W + 6)
+constexpr int AUR = 16;                                    // audio ring tiles (>= 2W + 6, a power of 2)
+constexpr int PR = 256;                                    // final-conv partial rows (>= 6 tiles, a power of 2)
 template <bool AUD, bool FIN> struct Geo {
   static constexpr int AU_OFF = BF_OFF + NF * NLY * 2 * CI * 4;
   static constexpr int FW_OFF = AU_OFF + (AUD || FIN ? AUR * 32 * 4 : 0);
   static constexpr int FF_OFF = FW_OFF + (AUD ? (7 + 1) * 32 * 4 : 0);   // first conv [tap][c] + bias
   static constexpr int P_OFF = FF_OFF + (FIN ? 7 * 32 * 4 : 0);           // final conv [tap][c]
-  static constexpr int SMEM = P_OFF + (FIN ? RR * 7 * 4 : 0);             // partials, 7 per row
+  static constexpr int SMEM = P_OFF + (FIN ? 2 * PR * 7 * 4 : 0);         // partials [half][row][tap]
 };
-__device__ __forceinline__ int swz(int row, int chunk) { return ((chunk ^ (row >> 2)) & 3) * 16; }
 }  // namespace lsw
+#ifdef LB_TRACE
+// tools/skew_probe.hip: s_memtime stamps of workgroup 37, steps 8..15, [step][wave][20]
+#define SK_STAMP(jj, idx)                                                                    \
+  do {                                                                                       \
+    if (lane == 0 && blockIdx.x == 37 && (jj) >= 8 && (jj) < 16)                             \
+      P.trace[(((jj) - 8) * lsw::NWV + wv) * 20 + (idx)] = __builtin_readcyclecounter();    \
+  } while (0)
+#else
+#define SK_STAMP(jj, idx) \
+  do {                    \
+  } while (0)
+#endif
 
 template <bool AUD, bool FIN>
-__global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlockArgs P, int nseg, int seg_tiles) {
+__global__ __launch_bounds__(lsw::NTH, 2) void lvc_skew_bf16_kernel(const LvcBlockArgs P, int nseg, int seg_tiles) {
   using namespace lsw;
   using GG = Geo<AUD, FIN>;
   static_assert(GG::SMEM <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char sm[GG::SMEM];
-  // the wave index in an SGPR: every tile index and slot decision below is wave-uniform
-  const int tid = threadIdx.x, lane = tid & 63, m = __builtin_amdgcn_readfirstlane(tid >> 6), n = lane & 31,
-            h = lane >> 5;
+  // wave index in an SGPR: every tile index and slot decision below is wave-uniform.
+  // m = the pair's tile group (local tile i = m mod W), ch = channel half.
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = wv >> 1, ch = wv & 1;
+  const int n = lane & 31, h = lane >> 5;            // 32x32 MFMA lane coordinates
+  const int m16 = lane & 15, q16 = lane >> 4;        // 16x16 MFMA lane coordinates
   const int b = blockIdx.x / nseg, sg = blockIdx.x - b * nseg;
   const int Tc = P.Tc, hop = P.hop, Lh = Tc * hop, NTu = Lh >> 5;
   const int tau0 = sg * seg_tiles, tau1 = min(tau0 + seg_tiles, NTu);
@@ -1069,26 +1098,25 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
   const int nloc = tau1 - sigma;                     // outputs: local tiles [3, nloc)
   const int J = (nloc + 3) / W + 1;                  // the last final-conv window [W(J-1)-4, W(J-1)+W-4) reaches nloc
   const long long base = (long long)b * Lh;
-  const int r = P.r, pp = P.p, Tin = Lh / r, ntj = (32 * W / r + 1 + 31) / 32, nph = r / 4;
+  const int r = P.r, pp = P.p, Tin = Lh / r;
+  const int fsh = __builtin_ctz(hop >> 5);           // tiles per frame = hop / 32, a power of 2
   auto gt = [&](int i) { return sigma + i; };        // local -> global tile
   auto inside = [&](int i) { return gt(i) >= 0 && gt(i) < NTu; };
-  auto frame_of = [&](int i) { return min(max(gt(i) * 32, 0) / hop, Tc - 1); };
-  // LDS addressing
-  auto uoff = [&](int l, int R, int chunk) {         // ring l, local row R (may be negative)
-    const int pr = (R + RR * 16) % RR;
-    return U_OFF + l * U_LAYER + pr * 64 + swz(pr, chunk);
-  };
-  auto yoff = [&](int br, int chunk) { return Y_OFF + br * 64 + swz(br, chunk); };
-  auto xpoff = [&](int row, int chunk) { return XP_OFF + row * 64 + swz(row, chunk); };
-  auto xsoff = [&](int j, int rr, int c4) {          // fp32 upsample output, window row rr, 16-B chunk c4
-    const int half = (rr >> 4) & 1, ring = 1 + half;
-    const int slot = (W * j - ring + 1 + (rr >> 5) + RT * 16) % RT;   // a tile rewritten later this step
-    return U_OFF + ring * U_LAYER + slot * 2048 + (rr & 15) * 128 + ((c4 ^ ((rr & 15) >> 1)) & 7) * 16;
-  };
-  auto aroff = [&](int R) { return GG::AU_OFF + ((R + AUR * 32 * 16) & (AUR * 32 - 1)) * 4; };
+  auto frame_of = [&](int i) { return min(max(gt(i), 0) >> fsh, Tc - 1); };
+  auto pslot = [&](int i) { return (i % RT + RT) % RT + 1; };   // physical ring slot of local tile i
   auto lds4 = [&](int off) -> float4& { return *reinterpret_cast<float4*>(sm + off); };
   auto ldsb8 = [&](int off) -> bf16x8& { return *reinterpret_cast<bf16x8*>(sm + off); };
   auto ldsf = [&](int off) -> float& { return *reinterpret_cast<float*>(sm + off); };
+  // this wave's channels in the 32x32 C layout: element e <-> channel 16ch + 4h + (e & 3) + 8(e >> 2)
+  const int cb0 = 16 * ch + 4 * h, cb1 = cb0 + 8;
+  // per-lane LDS address parts (constant for the whole kernel)
+  const int lc_ub = m16 * LDB + q16 * 16;                                        // pre-conv B (u rows)
+  const int lc_wc = WC_OFF + ((q16 >> 1) * 64 + 32 * (q16 & 1) + 16 * ch + m16) * 16;   // pre-conv A
+  const int lc_bc = BC_OFF + (16 * ch + 4 * q16) * 4;                            // pre-conv bias
+  const int lc_yw = Y_OFF + (2 + m16) * LDB + (2 * (q16 & 1) + ch) * 16 + 8 * (q16 >> 1);   // y write
+  const int lc_yr = Y_OFF + n * LDB + h * 16;                                    // LVC B (y rows)
+  const int lc_uw = n * LDB + (2 * h + ch) * 16;                                 // u write (lvc_pos 16h+8ch..)
+  const int lc_bf = BF_OFF + cb0 * 4;                                            // LVC bias
 
   // ---- prologue: zero the state, stage the weights
   for (int i = tid; i < GG::SMEM / 16; i += NTH) reinterpret_cast<uint4*>(sm)[i] = uint4{0u, 0u, 0u, 0u};
@@ -1109,29 +1137,35 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
     if (tid < 224) ldsf(GG::FF_OFF + tid * 4) = P.wfin[tid];                        // already [tap][c]
   }
   const float bfin = FIN ? P.bfin[0] : 0.f;
-  // upsample phase weights: this wave computes phases m and m + 4 (r = 8) on every column
-  // tile; re-loaded (L2-resident) at the end of each step, ahead of the kernel prefetch
-  bf16x8 wup[2][4];
+  // upsample phase GEMM job of this wave: phase wv % r on column tile wv / r (r * tiles = 8);
+  // its weights are re-loaded (L2-resident) at the end of each step, ahead of the kernel prefetch
+  const int uk = wv % r, ujt = wv / r;
+  const int rw = r * (ujt * 32 + n) + uk - pp;       // the window row this lane's column writes (t - T0)
+  const bool rw_ok = rw >= 0 && rw < 32 * W;
+  bf16x8 wup[4];
   auto wup_load = [&]() {
+    const __bf16* wa = P.Wup + ((long long)uk * 32 + n) * 64 + 8 * h;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (q >= nph) break;
-      const __bf16* wa = P.Wup + ((long long)(m + 4 * q) * 32 + n) * 64 + 8 * h;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) wup[q][kk] = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
-    }
+    for (int kk = 0; kk < 4; ++kk) wup[kk] = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
   };
   wup_load();
+  // XS (fp32 upsample output) in ring 1 (rows 0-15 of a window tile) / ring 2 (rows 16-31):
+  // window tile q of step j lives in the slot of local tile Wj - ring + 1 + q, which that
+  // ring's writer (layer ring - 1) rewrites later in the same step
+  auto xsoff = [&](int j, int rr) {
+    const int ring = 1 + ((rr >> 4) & 1);
+    const int ps = pslot(W * j - ring + 1 + (rr >> 5));
+    return U_OFF + ring * U_LAYER + ps * TB + (rr & 15) * XLD;
+  };
   // per-step operand loads (issued one step ahead, stored to LDS at the end of the step)
   const float* xprev = P.xin + (long long)b * Tin * CI;
   const int xpn = 32 * W / r + 2;                    // x_prev rows per step
-  constexpr int IX = (XPR * 8 + NTH - 1) / NTH;      // float4 per thread
+  constexpr int IX = ((32 * W / 4 + 2) * 8 + NTH - 1) / NTH;   // float4 per thread
   float4 xv[IX];
   float av = 0.f;
-  constexpr int IB = (8 * 64 + NTH - 1) / NTH;       // bias float4 per thread (<= 8 frames)
-  float4 bfv[IB];
-  const int nfill = ((W + 4) * 32 + hop - 1) / hop + 1;   // LVC-bias frames a step can touch
-  auto flo = [&](int j) { return max(gt(W * j - 3) * 32, 0) / hop; };
+  float4 bfv;
+  const int nfill = ((W + 4) * 32 + hop - 1) / hop + 1;   // LVC-bias frames a step can touch (<= 8)
+  auto flo = [&](int j) { return max(gt(W * j - 3), 0) >> fsh; };
   auto issue_xprev = [&](int j) {                    // x_prev rows jb .. jb + xpn of step j
     const int jb = 32 * gt(W * j + 1) / r - 1;
 #pragma unroll
@@ -1148,11 +1182,12 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
       if (rr < xpn) {
         const float mk = (jj >= 0 && jj < Tin) ? 1.f : 0.f;     // rows outside x_prev are zero
         const f32x2 u0 = lrelu2(f32x2{xv[it].x, xv[it].y} * mk), u1 = lrelu2(f32x2{xv[it].z, xv[it].w} * mk);
-        *reinterpret_cast<bf16x4*>(sm + xpoff(rr, q >> 3) + (q & 7) * 2) =
+        *reinterpret_cast<bf16x4*>(sm + XP_OFF + rr * LDB + q * 2) =
             bf16x4{(__bf16)u0.x, (__bf16)u0.y, (__bf16)u1.x, (__bf16)u1.y};
       }
     }
   };
+  auto aroff = [&](int R) { return GG::AU_OFF + (R & (AUR * 32 - 1)) * 4; };
   auto issue_audio = [&](int t0tile) {               // AUD / FIN: W tiles of samples from local tile t0tile
     if (tid < 32 * W) {
       const int t = gt(t0tile) * 32 + tid;
@@ -1166,40 +1201,44 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
     }
   };
   auto issue_bias = [&](int j) {                     // frames flo(j) .. + 8, 64 float4 each
-#pragma unroll
-    for (int q = 0; q < IB; ++q) {
-      const int i = tid + q * NTH, fr = flo(j) + (i >> 6), c = (i & 63) * 4;
-      bfv[q] = *reinterpret_cast<const float4*>(P.Bf + ((long long)b * Tc + min(fr, Tc - 1)) * (2 * CI * NLY) + c);
-    }
+    const int fr = flo(j) + (tid >> 6), c = (tid & 63) * 4;
+    bfv = *reinterpret_cast<const float4*>(P.Bf + ((long long)b * Tc + min(fr, Tc - 1)) * (2 * CI * NLY) + c);
   };
   auto store_bias = [&](int j) {
-#pragma unroll
-    for (int q = 0; q < IB; ++q) {
-      const int i = tid + q * NTH, fr = flo(j) + (i >> 6), c = (i & 63) * 4;
-      if ((i >> 6) < nfill) {
-        // gate pre-scale (the accumulators are exp2 arguments); frames past the end are zero
-        const float sc = fr >= Tc ? 0.f : (c & 63) < 32 ? -LOG2E : 2.f * LOG2E;
-        lds4(BF_OFF + ((fr % NF) * 256 + c) * 4) = make_float4(bfv[q].x * sc, bfv[q].y * sc, bfv[q].z * sc, bfv[q].w * sc);
-      }
+    const int fr = flo(j) + (tid >> 6), c = (tid & 63) * 4;
+    if ((tid >> 6) < nfill) {
+      // gate pre-scale (the accumulators are exp2 arguments); frames past the end are zero
+      const float sc = fr >= Tc ? 0.f : (c & 63) < 32 ? -LOG2E : 2.f * LOG2E;
+      lds4(BF_OFF + ((fr % NF) * 256 + c) * 4) = make_float4(bfv.x * sc, bfv.y * sc, bfv.z * sc, bfv.w * sc);
     }
   };
-  // kernel fragments of (layer, local tile), frame-major fragment order (kp_kernel_bf16_kernel)
-  bf16x8 kn[12];
+  // kernel fragments of (layer, local tile): this half's gate rows 16ch.. and filter rows
+  // 32+16ch.. as ONE 32-row A operand (A-row n < 16: gate 16ch + n; n >= 16: filter 16ch + n-16),
+  // picked from the frame-major fragment order (kp_kernel_bf16_kernel)
+  bf16x8 kn[6];
+  const int kofs = ((n >= 16 ? 6 * 64 : 0) + 32 * h + 16 * ch + (n & 15)) * 16;   // bytes
   auto kload = [&](int l, int i) {
-    const __bf16* kq = P.Kf[l] + ((long long)b * Tc + frame_of(i)) * KPERLAYER;
+    const char* kq = reinterpret_cast<const char*>(P.Kf[l] + ((long long)b * Tc + frame_of(i)) * KPERLAYER);
 #pragma unroll
-    for (int kk = 0; kk < 12; ++kk) kn[kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+    for (int kk = 0; kk < 6; ++kk) kn[kk] = *reinterpret_cast<const bf16x8*>(kq + kofs + kk * 1024);
   };
-  // audio_down of the U tile (non-AUD: loaded one step ahead, C layout)
-  float4 apf[4];
+  // audio_down of the U tile (non-AUD: loaded one step ahead, this wave's 8 channels per lane)
+  float4 apf[2];
   auto issue_a = [&](int i) {
     const int t = min(max(gt(i) * 32 + n, 0), Lh - 1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) apf[q] = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + 8 * q + 4 * h);
+    apf[0] = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + cb0);
+    apf[1] = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + cb1);
   };
-  // this wave's tile in stage U / layer l at step j
+  // this pair's tile in stage U / layer l at step j
   auto iU = [&](int j) { return W * j + (m == 0 ? W : m); };
   auto iL = [&](int j, int l) { return W * j + m - (m + l >= W ? W : 0); };
+  // bf16 row of tile i (this lane's row n, its 8 channels) into ring l, and the mirror copy
+  auto uwrite = [&](int l, int i, const bf16x8& v) {
+    const int ps = pslot(i);
+    ldsb8(lc_uw + U_OFF + l * U_LAYER + ps * TB) = v;
+    if (ps == RT) ldsb8(lc_uw + U_OFF + l * U_LAYER) = v;
+    if (ps == 1) ldsb8(lc_uw + U_OFF + l * U_LAYER + (RT + 1) * TB) = v;
+  };
 
   // step-0 operands
   issue_xprev(0);
@@ -1217,21 +1256,18 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
   store_bias(0);
   __syncthreads();
 
-  // fp32 state: the layers' tile (c) and the U tile (nx)
-  f32x2 cz[8], ca[8], nz[8], na[8];
+  // fp32 state (this wave's 8 channels per lane): the layers' tile (c) and the U tile (nx)
+  f32x2 cz[4], ca[4], nz[4], na[4];
 #pragma unroll
-  for (int p = 0; p < 8; ++p) { cz[p] = ca[p] = nz[p] = na[p] = f32x2{0.f, 0.f}; }
+  for (int p = 0; p < 4; ++p) { cz[p] = ca[p] = nz[p] = na[p] = f32x2{0.f, 0.f}; }
   auto swap_slots = [&]() {
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
+    for (int p = 0; p < 4; ++p) {
       const f32x2 tz = cz[p], ta = ca[p];
       cz[p] = nz[p]; ca[p] = na[p]; nz[p] = tz; na[p] = ta;
     }
   };
-  auto take_next = [&]() {
-#pragma unroll
-    for (int p = 0; p < 8; ++p) { cz[p] = nz[p]; ca[p] = na[p]; }
-  };
+  auto pofs = [&](int half, int R, int tap) { return GG::P_OFF + ((half * PR + (R & (PR - 1))) * 7 + tap) * 4; };
 
   // final-conv combine of step jf's window: eps(t) = b + sum_tap P(t + tap - 3)[tap];
   // audio_out = (x_t - ce eps) / den + sig z   (FastDiff_model.py:100, util.py:222-226)
@@ -1241,7 +1277,7 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
       if (i >= 3 && i < nloc && t >= 0 && t < Lh) {
         float e = 0.f;
 #pragma unroll
-        for (int tap = 0; tap < 7; ++tap) e += ldsf(GG::P_OFF + (((R + tap - 3 + RR * 16) % RR) * 7 + tap) * 4);
+        for (int tap = 0; tap < 7; ++tap) e += ldsf(pofs(0, R + tap - 3, tap)) + ldsf(pofs(1, R + tap - 3, tap));
         e += bfin;
         float v = (ldsf(aroff(R)) - P.ce * e) / P.den;
         if (P.sig != 0.f)
@@ -1253,33 +1289,30 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
   };
 
   for (int j = 0; j < J; ++j) {
-    // ================= A1: previous final conv, upsample phase GEMMs -> XS, next-step loads
+    SK_STAMP(j, 0);
+    // ================= A1: previous final conv, upsample phase GEMM -> XS, next-step loads
     if constexpr (FIN) {
       if (j > 0) fin_combine(j - 1);
     }
-    // C^T[co][col] = [W_k^T | W_{k+r}^T] . [xp(j0); xp(j0 - 1)],  t = r j0 + k - p  (modules.py:205-206)
+    {
+      // C^T[co][col] = [W_k^T | W_{k+r}^T] . [xp(j0); xp(j0 - 1)],  t = r j0 + k - p  (modules.py:205-206)
+      // column c' = ujt*32 + n is input j0 = T0 / r + c' (XP row c' + 1): window row rw = r c' + k - p
+      f32x16 acc;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (q >= nph) break;
-      const int k = m + 4 * q;
-      for (int jt = 0; jt < ntj; ++jt) {
-        f32x16 acc;
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      const int xo = XP_OFF + (ujt * 32 + n) * LDB + h * 16;
+      bf16x8 xb[4];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      for (int kk = 0; kk < 4; ++kk) xb[kk] = ldsb8(xo + (kk < 2 ? LDB : 0) + 32 * (kk & 1));
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int row = min(jt * 32 + n + (kk < 2 ? 1 : 0), XPR - 1);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wup[q][kk], ldsb8(xpoff(row, 2 * (kk & 1) + h)), acc, 0, 0, 0);
-        }
-        // column c' = jt*32 + n is input j0 = T0 / r + c' (XP row c' + 1): window row t - T0 = r c' + k - p
-        const int rw = r * (jt * 32 + n) + k - pp;
-        if (rw >= 0 && rw < 32 * W) {
+      for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wup[kk], xb[kk], acc, 0, 0, 0);
+      if (rw_ok) {
+        const int xs = xsoff(j, rw);
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const float4 bv = lds4(BU_OFF + (8 * g + 4 * h) * 4);
-            lds4(xsoff(j, rw, 2 * g + h)) =
-                make_float4(acc[4 * g] + bv.x, acc[4 * g + 1] + bv.y, acc[4 * g + 2] + bv.z, acc[4 * g + 3] + bv.w);
-          }
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = lds4(BU_OFF + (8 * g + 4 * h) * 4);
+          lds4(xs + (2 * g + h) * 16) =
+              make_float4(acc[4 * g] + bv.x, acc[4 * g + 1] + bv.y, acc[4 * g + 2] + bv.z, acc[4 * g + 3] + bv.w);
         }
       }
     }
@@ -1288,24 +1321,28 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
       issue_bias(j + 1);
       if constexpr (AUD || FIN) issue_audio(W * j + W + 2);
     }
+    SK_STAMP(j, 1);
     __syncthreads();
+    SK_STAMP(j, 2);
     // ================= A2: z_0 = upsample + audio_down of the U tile, u_0 ring
     {
       const int iu = iU(j), q = iu - W * j - 1, R = 32 * iu + n;
-      f32x2 x0[8], a0[8];
+      const int xs = xsoff(j, 32 * q + n);
+      f32x2 x0[4], a0[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 xv4 = lds4(xsoff(j, 32 * q + n, 2 * g + h));
+      for (int g = 0; g < 2; ++g) {
+        const int cb = g ? cb1 : cb0;
+        const float4 xv4 = lds4(xs + cb * 4);
         float4 a4;
         if constexpr (AUD) {
           // a0[t][c] = b[c] + sum_tap w[c][tap] audio[t + tap - 3]  (first_conv_kernel's order)
           float sa[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) sa[c] = ldsf(GG::FW_OFF + (224 + 8 * g + 4 * h + c) * 4);
+          for (int c = 0; c < 4; ++c) sa[c] = ldsf(GG::FW_OFF + (224 + cb + c) * 4);
 #pragma unroll
           for (int tap = 0; tap < 7; ++tap) {
             const float au = ldsf(aroff(R + tap - 3));
-            const float4 w = lds4(GG::FW_OFF + (tap * 32 + 8 * g + 4 * h) * 4);
+            const float4 w = lds4(GG::FW_OFF + (tap * 32 + cb) * 4);
             sa[0] = fmaf(w.x, au, sa[0]); sa[1] = fmaf(w.y, au, sa[1]);
             sa[2] = fmaf(w.z, au, sa[2]); sa[3] = fmaf(w.w, au, sa[3]);
           }
@@ -1316,99 +1353,107 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
         x0[2 * g] = f32x2{xv4.x + a4.x, xv4.y + a4.y}; x0[2 * g + 1] = f32x2{xv4.z + a4.z, xv4.w + a4.w};
         a0[2 * g] = f32x2{a4.x, a4.y}; a0[2 * g + 1] = f32x2{a4.z, a4.w};
       }
-      const bool in = inside(iu);
-      bf16x8 u0, u1;
+      bf16x8 u0 = {};
+      if (inside(iu)) {                              // rows outside the utterance stay zero (conv padding)
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const f32x2 v0 = in ? lrelu2(x0[p]) : f32x2{0.f, 0.f}, v1 = in ? lrelu2(x0[4 + p]) : f32x2{0.f, 0.f};
-        u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
-        u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
+        for (int p = 0; p < 4; ++p) {
+          const f32x2 v = lrelu2(x0[p]);
+          u0[2 * p] = (__bf16)v.x; u0[2 * p + 1] = (__bf16)v.y;
+        }
       }
-      ldsb8(uoff(0, R, 2 * h)) = u0;
-      ldsb8(uoff(0, R, 2 * h + 1)) = u1;
+      uwrite(0, iu, u0);                             // positions 16h + 8ch + e (lvc_pos of the channels)
 #pragma unroll
-      for (int p = 0; p < 8; ++p) { nz[p] = x0[p]; na[p] = a0[p]; }
-      // wave 0's U tile is next step's; waves m >= 1 start this step's layers on it, and
+      for (int p = 0; p < 4; ++p) { nz[p] = x0[p]; na[p] = a0[p]; }
+      // pair 0's U tile is next step's; pairs m >= 1 start this step's layers on it, and
       // keep their older tile (layers >= W - m) in `nx` until then
       if (m >= 1) swap_slots();
     }
+    SK_STAMP(j, 3);
     __syncthreads();
-    // ================= layers
-#pragma unroll 1
+    // ================= layers (unrolled: the slot switch and the last layer's epilogue are
+    // static per layer, so the state registers are not shuffled through loop phis)
+#pragma unroll
     for (int l = 0; l < NLY; ++l) {
       const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
       const int i = iL(j, l), w = (m + l) % W;       // tile, window position (window at Wj - l)
-      if (l > 0 && m >= 1 && l == W - m) swap_slots();   // the older tile takes over
+      if (l > 0 && m == W - l) swap_slots();         // the older tile takes over
       if constexpr (!AUD) {
         if (l == 0 && j + 1 < J) issue_a(iU(j + 1));
       }
-      // ---- B_l: y rows [32i+1, 32i+33) = lrelu(W_c . [u(t-d); u(t); u(t+d)] + b) -> y rows 32w+2..
+      SK_STAMP(j, 4 + 4 * l);
+      // ---- B_l: y rows [32i+1, 32i+33) = lrelu(W_c . [u(t-d); u(t); u(t+d)] + b) -> y rows 32w+2..,
+      //      this wave's 16 output channels 16ch.. on 16x16x32 MFMAs (2 row blocks x 3 taps)
       {
-        f32x16 acc;
+        // every operand of the 6 MFMAs is read before the first one issues (one LDS latency)
+        const int ub = lc_ub + U_OFF + l * U_LAYER + (32 * pslot(i) + 1 - d) * LDB;
+        bf16x8 wa[3], uv[2][3];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+        for (int ks = 0; ks < 3; ++ks) {   // the 32x32x16 fragment (k-step 2ks + q/2, lane 32(q&1) + 16ch + m16)
+          wa[ks] = ldsb8(lc_wc + (l * 6 + 2 * ks) * 1024);
 #pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
-          const int tap = kk >> 1;
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ldsb8(WC_OFF + ((l * 6 + kk) * 64 + lane) * 16),
-                                                        ldsb8(uoff(l, 32 * i + 1 + n + (tap - 1) * d, 2 * (kk & 1) + h)),
-                                                        acc, 0, 0, 0);
+          for (int rb = 0; rb < 2; ++rb) uv[rb][ks] = ldsb8(ub + (ks * d + 16 * rb) * LDB);
         }
-        f32x2 v[8];
+        const float4 bv = lds4(lc_bc + l * CI * 4);
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 acc[2];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 bv = lds4(BC_OFF + (l * CI + 8 * g + 4 * h) * 4);
-          v[2 * g] = lrelu2(f32x2{acc[4 * g], acc[4 * g + 1]} + f32x2{bv.x, bv.y});
-          v[2 * g + 1] = lrelu2(f32x2{acc[4 * g + 2], acc[4 * g + 3]} + f32x2{bv.z, bv.w});
+        for (int rb = 0; rb < 2; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+            acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks], uv[rb][ks], acc[rb], 0, 0, 0);
+        f32x2 v[2][2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          v[rb][0] = lrelu2(f32x2{acc[rb][0], acc[rb][1]} + f32x2{bv.x, bv.y});
+          v[rb][1] = lrelu2(f32x2{acc[rb][2], acc[rb][3]} + f32x2{bv.z, bv.w});
         }
-        const int tt = 32 * gt(i) + 1;                // global time of this preconv tile's row 0
+        const int tt = 32 * gt(i) + 1;                // global time of this pre-conv tile's row 0
         if (tt < 0 || tt + 31 >= Lh) {                // utterance-edge tile: the LVC zero-pads y
-          const int t = tt + n;
-          const bool in = t >= 0 && t < Lh;
 #pragma unroll
-          for (int p = 0; p < 8; ++p) v[p] = in ? v[p] : f32x2{0.f, 0.f};
+          for (int rb = 0; rb < 2; ++rb) {
+            const int t = tt + 16 * rb + m16;
+            if (t < 0 || t >= Lh) { v[rb][0] = f32x2{0.f, 0.f}; v[rb][1] = f32x2{0.f, 0.f}; }
+          }
         }
-        bf16x8 y0, y1;
+        // lvc_pos(co + e) = 16(q&1) + 8ch + 4(q>>1) + e: 4 contiguous positions (8 bytes)
+        const int yw = lc_yw + 32 * w * LDB;
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          y0[2 * p] = (__bf16)v[p].x; y0[2 * p + 1] = (__bf16)v[p].y;
-          y1[2 * p] = (__bf16)v[4 + p].x; y1[2 * p + 1] = (__bf16)v[4 + p].y;
+        for (int rb = 0; rb < 2; ++rb) {
+          const bf16x4 y4 = {(__bf16)v[rb][0].x, (__bf16)v[rb][0].y, (__bf16)v[rb][1].x, (__bf16)v[rb][1].y};
+          *reinterpret_cast<bf16x4*>(sm + yw + 16 * rb * LDB) = y4;
+          if (w == W - 1 && rb == 1 && m16 >= 14)    // rows 32W, 32W + 1: the next step's rows 0, 1
+            *reinterpret_cast<bf16x4*>(sm + yw + 16 * LDB - Y_OFF - (32 * W) * LDB + YC_OFF + (l * 2 + (j & 1)) * 2 * LDB) = y4;
         }
-        const int br = 32 * w + 2 + n;
-        ldsb8(yoff(br, 2 * h)) = y0;
-        ldsb8(yoff(br, 2 * h + 1)) = y1;
-        if (w == W - 1 && n >= 30) {                  // rows 32W, 32W + 1: the next step's rows 0, 1
-          const int co = YC_OFF + ((l * 2 + (j & 1)) * 2 + (n - 30)) * 64;
-          *reinterpret_cast<bf16x8*>(sm + co + swz(br, 2 * h)) = y0;
-          *reinterpret_cast<bf16x8*>(sm + co + swz(br, 2 * h + 1)) = y1;
-        }
-        if (w == 0 && lane < 8) {                     // rows 0, 1 from the previous step
-          const int ci = YC_OFF + ((l * 2 + ((j + 1) & 1)) * 2) * 64 + lane * 16;
+        if (w == 0 && ch == 0 && lane < 10) {        // rows 0, 1 from the previous step (2 x 80 B)
+          const int ci = YC_OFF + ((l * 2 + ((j + 1) & 1)) * 2) * LDB + lane * 16;
           *reinterpret_cast<uint4*>(sm + Y_OFF + lane * 16) = *reinterpret_cast<const uint4*>(sm + ci);
         }
       }
+      SK_STAMP(j, 5 + 4 * l);
       __syncthreads();
+      SK_STAMP(j, 6 + 4 * l);
       // ---- C_l: o^T = K_frame . [y(t-1); y(t); y(t+1)]^T + Bf;  z += gate(o) (+ a)
       {
-        f32x16 g, f;
+        f32x16 acc;
+        bf16x8 yb[6];
         {
-          const float* bq = reinterpret_cast<const float*>(sm + BF_OFF) + ((frame_of(i) % NF) * NLY + l) * 2 * CI;
+          const int bo = lc_bf + ((frame_of(i) % NF) * NLY + l) * 2 * CI * 4;
+          const float4 g0 = lds4(bo), g1 = lds4(bo + 32), f0 = lds4(bo + 128), f1 = lds4(bo + 160);
+          acc[0] = g0.x; acc[1] = g0.y; acc[2] = g0.z; acc[3] = g0.w;
+          acc[4] = g1.x; acc[5] = g1.y; acc[6] = g1.z; acc[7] = g1.w;
+          acc[8] = f0.x; acc[9] = f0.y; acc[10] = f0.z; acc[11] = f0.w;
+          acc[12] = f1.x; acc[13] = f1.y; acc[14] = f1.z; acc[15] = f1.w;
+          const int yr = lc_yr + 32 * w * LDB;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * q + 4 * h);
-            const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * q + 4 * h);
-            g[4 * q] = bg.x; g[4 * q + 1] = bg.y; g[4 * q + 2] = bg.z; g[4 * q + 3] = bg.w;
-            f[4 * q] = bl.x; f[4 * q + 1] = bl.y; f[4 * q + 2] = bl.z; f[4 * q + 3] = bl.w;
-          }
+          for (int kk = 0; kk < 6; ++kk) yb[kk] = ldsb8(yr + (kk >> 1) * LDB + 32 * (kk & 1));
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
-          const bf16x8 yb = ldsb8(yoff(32 * w + (kk >> 1) + n, 2 * (kk & 1) + h));
-          g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g, 0, 0, 0);
-          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f, 0, 0, 0);
-        }
+        for (int kk = 0; kk < 6; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb[kk], acc, 0, 0, 0);
         // next LVC's kernel fragments, in flight under the gate, the next pre-conv and barriers
-        // (issued once these chains have read their fragments)
+        // (issued once this chain has read its fragments)
         __builtin_amdgcn_sched_barrier(0);
         if (l + 1 < NLY) {
           kload(l + 1, iL(j, l + 1));
@@ -1418,43 +1463,36 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x2 o0 = gate2s(f32x2{g[4 * q], g[4 * q + 1]}, f32x2{f[4 * q], f[4 * q + 1]});
-          const f32x2 o1 = gate2s(f32x2{g[4 * q + 2], g[4 * q + 3]}, f32x2{f[4 * q + 2], f[4 * q + 3]});
-          if (l + 1 < NLY) {
-            cz[2 * q] += ca[2 * q] + o0;
-            cz[2 * q + 1] += ca[2 * q + 1] + o1;
-          } else {
-            cz[2 * q] += o0;
-            cz[2 * q + 1] += o1;
-          }
+        for (int p = 0; p < 4; ++p) {
+          const f32x2 o = gate2s(f32x2{acc[2 * p], acc[2 * p + 1]}, f32x2{acc[8 + 2 * p], acc[8 + 2 * p + 1]});
+          if (l + 1 < NLY) cz[p] += ca[p] + o;
+          else cz[p] += o;
         }
-        const bool in = inside(i);
         if (l + 1 < NLY) {
-          bf16x8 u0, u1;
+          bf16x8 u0 = {};
+          if (inside(i)) {
 #pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            const f32x2 v0 = in ? lrelu2(cz[p]) : f32x2{0.f, 0.f}, v1 = in ? lrelu2(cz[4 + p]) : f32x2{0.f, 0.f};
-            u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
-            u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
+            for (int p = 0; p < 4; ++p) {
+              const f32x2 v = lrelu2(cz[p]);
+              u0[2 * p] = (__bf16)v.x; u0[2 * p + 1] = (__bf16)v.y;
+            }
           }
-          ldsb8(uoff(l + 1, 32 * i + n, 2 * h)) = u0;
-          ldsb8(uoff(l + 1, 32 * i + n, 2 * h + 1)) = u1;
+          uwrite(l + 1, i, u0);
         } else if constexpr (FIN) {
-          // per-row partial sums of the final conv: P[t][tap] = sum_c w[tap][c] x4[t][c]
+          // per-row partial sums of the final conv over this half's channels: P[t][tap] = sum_c w[tap][c] x4[t][c]
           float sv[7];
 #pragma unroll
           for (int tap = 0; tap < 7; ++tap) {
-            float acc = 0.f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float4 wf = lds4(GG::FF_OFF + (tap * 32 + 8 * q + 4 * h) * 4);
-              acc = fmaf(wf.x, cz[2 * q].x, fmaf(wf.y, cz[2 * q].y, fmaf(wf.z, cz[2 * q + 1].x, fmaf(wf.w, cz[2 * q + 1].y, acc))));
-            }
-            acc += __shfl_xor(acc, 32);
-            sv[tap] = in ? acc : 0.f;                 // the final conv zero-pads x outside the utterance
+            const float4 w0 = lds4(GG::FF_OFF + (tap * 32 + cb0) * 4), w1 = lds4(GG::FF_OFF + (tap * 32 + cb1) * 4);
+            float s = fmaf(w0.x, cz[0].x, fmaf(w0.y, cz[0].y, fmaf(w0.z, cz[1].x, w0.w * cz[1].y)));
+            s = fmaf(w1.x, cz[2].x, fmaf(w1.y, cz[2].y, fmaf(w1.z, cz[3].x, fmaf(w1.w, cz[3].y, s))));
+            sv[tap] = s + __shfl_xor(s, 32);
           }
-          const int po = GG::P_OFF + (((32 * i + n + RR * 16) % RR) * 7) * 4;
+          if (!inside(i)) {                           // the final conv zero-pads x outside the utterance
+#pragma unroll
+            for (int tap = 0; tap < 7; ++tap) sv[tap] = 0.f;
+          }
+          const int po = pofs(ch, 32 * i + n, 0);
           if (h == 0) {
 #pragma unroll
             for (int tap = 0; tap < 4; ++tap) ldsf(po + tap * 4) = sv[tap];
@@ -1464,11 +1502,9 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
           }
         } else {
           const int t = 32 * gt(i) + n;
-          if (i >= 3 && i < nloc && in) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              *reinterpret_cast<float4*>(P.xout + (base + t) * CI + 8 * q + 4 * h) =
-                  make_float4(cz[2 * q].x, cz[2 * q].y, cz[2 * q + 1].x, cz[2 * q + 1].y);
+          if (i >= 3 && i < nloc && inside(i)) {
+            *reinterpret_cast<float4*>(P.xout + (base + t) * CI + cb0) = make_float4(cz[0].x, cz[0].y, cz[1].x, cz[1].y);
+            *reinterpret_cast<float4*>(P.xout + (base + t) * CI + cb1) = make_float4(cz[2].x, cz[2].y, cz[3].x, cz[3].y);
           }
         }
         if (l == NLY - 1 && j + 1 < J) {             // the next step's staged operands
@@ -1477,9 +1513,11 @@ __global__ __launch_bounds__(lsw::NTH, 1) void lvc_skew_bf16_kernel(const LvcBlo
           if constexpr (AUD || FIN) store_audio(W * j + W + 2);
         }
       }
+      SK_STAMP(j, 7 + 4 * l);
       __syncthreads();
     }
-    take_next();                                     // the U tile becomes the layers' tile
+#pragma unroll
+    for (int p = 0; p < 4; ++p) { cz[p] = nz[p]; ca[p] = na[p]; }   // the U tile becomes the layers' tile
   }
   if constexpr (FIN) fin_combine(J - 1);
 }
@@ -2034,10 +2072,29 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   __shared__ __attribute__((aligned(16))) __bf16 R0[DB_ROWS * DB_LD];   // x[f i] (residual input)
   __shared__ __attribute__((aligned(16))) __bf16 H1[DB_ROWS * DB_LD];
   __shared__ __attribute__((aligned(16))) __bf16 H2[DB_ROWS * DB_LD];
+  // audio input (the first DBlock): the block's samples t = f i + k - 3 of its rows, staged once
+  constexpr int DB_AUM = (DB_TS + 14) * 16 + 8;      // f <= 16 (fd_create's ratio bound)
+  __shared__ float AU[DB_AUM];
+  __shared__ float FWS[8 * 32];                       // first conv [tap][c] (+ bias row 7)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, i0 = blockIdx.x * DB_TS, ib = i0 - 7;
   const long long Lin = (long long)Lout * f;
   const float* src = in + (long long)b * Lin * CI;
+  if (audio) {
+    // input = first_conv(audio) at t = f ii (FastDiff_model.py:90), recomputed: no a0 tensor.
+    // One coalesced load of the samples [f ib - 3, f (ib + DB_TS + 14) + 4) (r02: 7 strided
+    // global loads per staged item made this block a chain of round trips, ~9x its siblings)
+    const long long t0 = (long long)ib * f - 3;
+    const float* au = audio + (long long)b * Lin;
+    const int na = (DB_TS + 14) * f + 8;
+    for (int i = tid; i < na; i += 256) {
+      const long long t = t0 + i;
+      AU[i] = (t >= 0 && t < Lin) ? au[t] : 0.f;
+    }
+    if (tid < 224) FWS[(tid % 7) * 32 + tid / 7] = fw[tid];   // fw is [c][tap]
+    if (tid < 32) FWS[224 + tid] = fb[tid];
+    __syncthreads();
+  }
   // staging: every thread's (<= DB_NI) items are loaded before any is converted, so their
   // strided HBM reads are in flight together (one round trip per block, not one per item)
   constexpr int DB_NI = (DB_ROWS * 8 + 255) / 256;
@@ -2048,18 +2105,15 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
     const int p = i >> 3, q = (i & 7) * 4, ii = ib + p;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < DB_ROWS * 8 && p < DB_TS + 14 && ii >= 0 && ii < Lout) {
-      if (audio) {   // input = first_conv(audio) (FastDiff_model.py:90), recomputed: no a0 tensor
-        const long long t = (long long)ii * f;
-        const float* au = audio + (long long)b * Lin;
-        float a7[7], o[4];
+      if (audio) {
+        float o[4];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) a7[k] = (t + k - 3 >= 0 && t + k - 3 < Lin) ? au[t + k - 3] : 0.f;
+        for (int e = 0; e < 4; ++e) o[e] = FWS[224 + q + e];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float acc = fb[q + e];
+        for (int k = 0; k < 7; ++k) {                // first_conv_kernel's order
+          const float a = AU[p * f + k];             // t = f ii + k - 3
 #pragma unroll
-          for (int k = 0; k < 7; ++k) acc = fmaf(fw[(q + e) * 7 + k], a7[k], acc);   // first_conv_kernel's order
-          o[e] = acc;
+          for (int e = 0; e < 4; ++e) o[e] = fmaf(FWS[k * 32 + q + e], a, o[e]);
         }
         v = make_float4(o[0], o[1], o[2], o[3]);
       } else {
@@ -2863,7 +2917,8 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream;
       }
       // (the LDS image holds upsample weights for r <= 4 with the audio fusions, r <= 8 without)
-      const bool skew_path = !stream_path && m->lvc_skew && ups && hop % 32 == 0 && hop >= 64 && (r == 4 || r == 8);
+      const bool skew_path = !stream_path && m->lvc_skew && ups && hop >= 64 && (hop & (hop - 1)) == 0 &&
+                             (r == 4 || r == 8);
       if (skew_path) {
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : "fd_lvc_block_ups", st);
         int nseg = 1, seg_tiles = 1;
