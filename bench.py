@@ -332,7 +332,7 @@ def free_port():
     return p
 
 
-def stub_synth(cond, seed):
+def stub_synth(cond, seed, utt_ids=None):
     """--dry-run stand-in for the Synthesizer (CPU, no compute worth timing)."""
     B, T, _ = cond.shape
     return cond[..., :80].clone(), torch.zeros(B, T * HOP)
@@ -434,9 +434,17 @@ def main():
             syn.diffusion.denoise_fn.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.wn_opt)})
         synth_fn = syn
 
+    phase = {"compute_ms": 0.0, "gather_ms": 0.0, "n": 0}    # N > 1: where each timed step went
+
     if cfg["vocoder"]:
-        def step(i):
-            return distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop)
+        def step(i, timed=False):
+            st = {} if (timed and world > 1) else None
+            out = distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop, stats=st)
+            if st:
+                phase["compute_ms"] += st["compute_ms"]
+                phase["gather_ms"] += st["gather_ms"]
+                phase["n"] += 1
+            return out
     else:
         # C2: the ProDiff sampler alone on one utterance (B=1), mel only
         gd = syn.diffusion
@@ -445,7 +453,7 @@ def main():
         if not args.no_graph:
             graph = gd.capture(cond_b, seed=1)             # hipGraph of the whole 2-step sampler
 
-        def step(i):
+        def step(i, timed=False):
             if graph is not None:
                 return graph.replay()
             return gd.sample(cond_b, seed=10_000 * i)
@@ -488,7 +496,7 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        out = step(args.warmup + nprof + i)
+        out = step(args.warmup + nprof + i, timed=True)
     if not dry:
         torch.cuda.synchronize()
     if world > 1:
@@ -520,10 +528,24 @@ def main():
         kern = _lib.profile_summary()
         _lib.profile_enable(False)
         _lib.profile_filter(None)
+    phases = None
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        if phase["n"]:
+            # per-step compute (own shard, device-synchronized) and gather of every rank
+            v = torch.tensor([phase["compute_ms"] / phase["n"], phase["gather_ms"] / phase["n"]],
+                             device=dev, dtype=torch.float64)
+            allv = [torch.empty_like(v) for _ in range(world)]
+            dist.all_gather(allv, v)
+            c = [float(x[0]) for x in allv]
+            g = [float(x[1]) for x in allv]
+            phases = {"compute_ms_per_step_slowest_rank": round(max(c), 3),
+                      "compute_ms_per_step_fastest_rank": round(min(c), 3),
+                      "gather_ms_per_step_max": round(max(g), 3),
+                      "gather_ms_per_step_rank0": round(g[0], 3),
+                      "note": "per rank: its shard's synthesis (synchronized) then the ragged RCCL gather to rank 0"}
     if rank == 0 and not dry:
         if cfg["vocoder"]:
             mels, wavs = out
@@ -593,6 +615,7 @@ def main():
         "model_tflops": round(step_fl * args.steps / dt / 1e12, 2),
         "roofline": roofline,
         "kernels": kernels,
+        "phases": phases,
         "kernels_source": (f"untimed {'eager ' if graph_prof else ''}pass of {nprof} steps, every launch bracketed by "
                            f"HIP events") if kernels else None,
         "cpu_baseline": None,

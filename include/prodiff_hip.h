@@ -104,6 +104,11 @@ int pd_wavenet_forward(const pd_wavenet* h, const float* spec, const float* step
                        const float* cond, float* out, int B, int T, void* workspace,
                        size_t ws_bytes, void* stream);
 
+/* Random draws (every sampler below).  When the caller passes no explicit draws they come
+ * from an on-device Philox4x32-10 generator keyed by (seed, utterance id, element index
+ * within the utterance, stream): `utt_ids` is a device array of B ints (one id per batch
+ * row) or NULL (ids 0..B-1).  An utterance's output therefore depends on (seed, its id) only,
+ * not on its row in the batch or on how a job is sharded over GPUs. */
 /* The whole x0-predict reverse sampler, GaussianDiffusion.forward(cond, infer=True)
  * (prodiff.py:136-153) for S = clip(infer_step, 1, timesteps) steps:
  *   x ~ U[0,1); for i = S-1..0: x0 = WaveNet(x, i, cond);
@@ -116,8 +121,8 @@ int pd_wavenet_forward(const pd_wavenet* h, const float* spec, const float* step
  *   mel   [B,T,M] output (the reference's x[:,0].transpose(1,2), prodiff.py:151). */
 int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1,
                       const float* coef2, const float* sigma, int S, const float* x_T,
-                      const float* noise, unsigned long long seed, float* mel, int B, int T,
-                      void* workspace, size_t ws_bytes, void* stream);
+                      const float* noise, unsigned long long seed, const int* utt_ids, float* mel,
+                      int B, int T, void* workspace, size_t ws_bytes, void* stream);
 
 /* ============================================================= rectified flow
  * RectifiedFlow / PitchRectifiedFlow inference (modules/diffusion/reflow.py:5-144) with
@@ -139,8 +144,8 @@ size_t pd_reflow_workspace_size(const pd_wavenet* h, int B, int T, int S, int al
  *   x_T  [B,T,M] time-major draw, or NULL -> Philox N(0,1) from `seed`
  *   x    [B,T,M] output: the reference's x.transpose(2,3).squeeze(1) before denorm_spec. */
 int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, float time_scale,
-                     const float* x_T, unsigned long long seed, float* x, int B, int T,
-                     void* workspace, size_t ws_bytes, void* stream);
+                     const float* x_T, unsigned long long seed, const int* utt_ids, float* x, int B,
+                     int T, void* workspace, size_t ws_bytes, void* stream);
 
 /* denorm_spec (reflow.py:106-107): y = (x+1)/2 * (spec_max - spec_min) + spec_min with
  * spec_min/spec_max device arrays of length nspec (1, broadcast, or M);  x [rows,M].
@@ -224,8 +229,8 @@ int fd_forward(const fd_model* m, const float* audio, const float* cond, const f
  *   or NULL -> Philox;  wav [B,L] output. */
 int fd_sample(const fd_model* m, const float* mel, const float* beta, const float* alpha,
               const float* sigma, const float* steps, int N, const float* x_T,
-              const float* noise, unsigned long long seed, float* wav, int B, int Tc,
-              void* workspace, size_t ws_bytes, void* stream);
+              const float* noise, unsigned long long seed, const int* utt_ids, float* wav, int B,
+              int Tc, void* workspace, size_t ws_bytes, void* stream);
 
 
 /* ==================================================================== NSF-HiFiGAN
@@ -280,8 +285,8 @@ int nsf_set_option(nsf_model* m, int option, int value);
  *   noise [B, T*hop, harmonic_num+1] (randn_like, models.py:182), or NULL -> Philox from seed
  *   wav [B, T*hop] output in [-1, 1]. */
 int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const float* f0, const float* rand_ini,
-                const float* noise, unsigned long long seed, float* wav, int B, int T,
-                void* workspace, size_t ws_bytes, void* stream);
+                const float* noise, unsigned long long seed, const int* utt_ids, float* wav, int B,
+                int T, void* workspace, size_t ws_bytes, void* stream);
 
 /* ============================================================ condition encoder
  * SVS teacher condition -- replaces ProDiffTeacher.forward_condition

@@ -75,10 +75,10 @@ _SIGS = {
     "pd_wavenet_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
     "pd_wavenet_forward": (C.c_int, [_VP, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "pd_prodiff_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),
-                                    C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP,
+                                    C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, _VP,
                                     C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "pd_reflow_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int, C.c_int]),
-    "pd_reflow_sample": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_float, _VP, C.c_ulonglong, _VP, C.c_int,
+    "pd_reflow_sample": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_float, _VP, C.c_ulonglong, _VP, _VP, C.c_int,
                                    C.c_int, _VP, C.c_size_t, _VP]),
     "pd_reflow_denorm": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
                                    _VP, _VP]),
@@ -90,7 +90,7 @@ _SIGS = {
     "fd_fold_weight_norm": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, _VP]),
     "fd_forward": (C.c_int, [_VP, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "fd_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
-                            C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, C.c_int,
+                            C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, _VP, C.c_int,
                             C.c_int, _VP, C.c_size_t, _VP]),
     "pd_cond_num_params": (C.c_int, [C.POINTER(pd_cond_dims)]),
     "pd_cond_create": (C.c_int, [C.POINTER(pd_cond_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
@@ -104,7 +104,8 @@ _SIGS = {
     "nsf_hop": (C.c_int, [_VP]),
     "nsf_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int]),
     "nsf_set_option": (C.c_int, [_VP, C.c_int, C.c_int]),
-    "nsf_forward": (C.c_int, [_VP, _VP, C.c_float, _VP, _VP, _VP, C.c_ulonglong, _VP, C.c_int, C.c_int, _VP, C.c_size_t,
+    "nsf_forward": (C.c_int, [_VP, _VP, C.c_float, _VP, _VP, _VP, C.c_ulonglong, _VP, _VP, C.c_int, C.c_int, _VP,
+                              C.c_size_t,
                               _VP]),
 }
 EXPORTS = tuple(_SIGS)
@@ -155,6 +156,28 @@ def lptr(t):
         raise HipError("libprodiff_hip needs device tensors (got a CPU tensor)")
     if t.dtype != torch.int64 or not t.is_contiguous():
         raise HipError(f"expected contiguous int64 tensor, got {t.dtype} contiguous={t.is_contiguous()}")
+    return C.c_void_p(t.data_ptr())
+
+
+def utt_ids(ids, B, device):
+    """Per-row utterance ids for the samplers' Philox draws (include/prodiff_hip.h): None
+    (ids 0..B-1) or B ints -> (device int32 tensor or None).  Keep the tensor alive until
+    the call's stream work is done (a captured graph keeps it)."""
+    if ids is None:
+        return None
+    import torch
+    t = torch.as_tensor(ids).reshape(-1)
+    if t.numel() != B:
+        raise HipError(f"utt_ids holds {t.numel()} ids for a batch of {B}")
+    if t.numel() and (int(t.min()) < 0 or int(t.max()) >= 2 ** 31):
+        raise HipError("utt_ids must lie in [0, 2**31)")
+    return t.to(device=device, dtype=torch.int32).contiguous()
+
+
+def iptr(t):
+    """Device pointer of a contiguous int32 tensor, or None."""
+    if t is None:
+        return None
     return C.c_void_p(t.data_ptr())
 
 

@@ -98,7 +98,7 @@ __device__ __forceinline__ float gate_fast(float g, float f) {
 
 // ---------------------------------------------------------------------------
 // Counter-based normal/uniform draws (Philox4x32-10), used when the caller does
-// not hand in explicit noise.  key = seed, counter = (index, stream id).
+// not hand in explicit noise.  key = seed.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
@@ -117,17 +117,20 @@ __device__ __forceinline__ float u01_from(uint32_t x) {
   return (float)((x >> 8) + 1u) * (1.0f / 16777216.0f);
 }
 
-// One standard-normal draw per (idx, stream) under `seed`.
-__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t idx, uint32_t stream) {
-  uint32_t c[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), stream, 0x5EEDu};
+// Per-utterance draws (what every sampler uses): counter = (element within the utterance,
+// utterance id, stream).  An utterance's noise depends on its id, never on its row in a
+// batch or on how a job is sharded over ranks, so batched, length-grouped and multi-GPU
+// runs of the same utterance produce the same output.  Ids come from the caller
+// (`utt_ids`, one per batch row) or default to the row index.
+__device__ __forceinline__ unsigned utt_id(const int* ids, int b) { return ids ? (unsigned)ids[b] : (unsigned)b; }
+__device__ __forceinline__ float philox_normal_u(uint64_t seed, unsigned uid, unsigned elem, uint32_t stream) {
+  uint32_t c[4] = {elem, uid, stream, 0x5EEDu};
   philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   float u1 = u01_from(c[0]), u2 = u01_from(c[1]);
   return sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
 }
-
-// One U[0,1) draw per (idx, stream).
-__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t idx, uint32_t stream) {
-  uint32_t c[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), stream, 0x0F00u};
+__device__ __forceinline__ float philox_uniform_u(uint64_t seed, unsigned uid, unsigned elem, uint32_t stream) {
+  uint32_t c[4] = {elem, uid, stream, 0x0F00u};
   philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
 }

@@ -366,6 +366,7 @@ struct LvcBlockArgs {
   float ce, den, sig;
   unsigned long long seed;
   unsigned stream;
+  const int* uid;           // FIN: utterance id per batch row (null -> row index)
   int Tc, hop;
   int b_off;                // utterance index of blockIdx.y = 0 in the whole batch (Philox draws)
 #ifdef LB_TRACE
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
       zr[it] = 0.f;
       if (s2 < 2 * TS && (s2 & 1) == 0 && t < Lh && P.sig != 0.f)
         zr[it] = P.noise ? P.noise[base + t]
-                         : philox_normal(P.seed, (unsigned long long)((long long)(b + P.b_off) * Lh + t), P.stream);
+                         : philox_normal_u(P.seed, utt_id(P.uid, b + P.b_off), (unsigned)t, P.stream);
     }
   }
   // ---- LDS stores of the staged operands
@@ -1282,7 +1283,7 @@ __global__ __launch_bounds__(lsw::NTH, 2) void lvc_skew_bf16_kernel(const LvcBlo
         float v = (ldsf(aroff(R)) - P.ce * e) / P.den;
         if (P.sig != 0.f)
           v += P.sig * (P.noise ? P.noise[base + t]
-                                : philox_normal(P.seed, (unsigned long long)((long long)(b + P.b_off) * Lh + t), P.stream));
+                                : philox_normal_u(P.seed, utt_id(P.uid, b + P.b_off), (unsigned)t, P.stream));
         P.audio_out[base + t] = v;
       }
     }
@@ -2031,8 +2032,7 @@ __global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockA
             float v = (FS[AU_OFF + ((32 * j + sm) & (NAU - 1))] - P.ce * e) / P.den;
             if (P.sig != 0.f)
               v += P.sig * (P.noise ? P.noise[base + t]
-                                    : philox_normal(P.seed, (unsigned long long)((long long)(b + P.b_off) * Lh + t),
-                                                    P.stream));
+                                    : philox_normal_u(P.seed, utt_id(P.uid, b + P.b_off), (unsigned)t, P.stream));
             P.audio_out[base + t] = v;
           }
         }
@@ -2068,31 +2068,55 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
                                                           const __bf16* __restrict__ W2, const float* __restrict__ b2,
                                                           int Lout, int f, const float* __restrict__ audio,
                                                           const float* __restrict__ fw, const float* __restrict__ fb) {
-  __shared__ __attribute__((aligned(16))) __bf16 U0[DB_ROWS * DB_LD];   // lrelu(x[f i])
+  // U0 = lrelu(x[f i]) is dead after the first conv, so h2 reuses its rows: 3 x 13 KB of
+  // bf16 images (+ the audio window) let 3 blocks share a CU
+  __shared__ __attribute__((aligned(16))) __bf16 U0[DB_ROWS * DB_LD];   // lrelu(x[f i]), then h2
   __shared__ __attribute__((aligned(16))) __bf16 R0[DB_ROWS * DB_LD];   // x[f i] (residual input)
   __shared__ __attribute__((aligned(16))) __bf16 H1[DB_ROWS * DB_LD];
-  __shared__ __attribute__((aligned(16))) __bf16 H2[DB_ROWS * DB_LD];
+  __bf16* H2 = U0;
   // audio input (the first DBlock): the block's samples t = f i + k - 3 of its rows, staged once
   constexpr int DB_AUM = (DB_TS + 14) * 16 + 8;      // f <= 16 (fd_create's ratio bound)
+  constexpr int DB_AUI = (DB_AUM + 255) / 256;
   __shared__ float AU[DB_AUM];
   __shared__ float FWS[8 * 32];                       // first conv [tap][c] (+ bias row 7)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, i0 = blockIdx.x * DB_TS, ib = i0 - 7;
   const long long Lin = (long long)Lout * f;
   const float* src = in + (long long)b * Lin * CI;
+  // every stage's weight fragments first: their L2 round trip overlaps the staging's
+  bf16x8 wf0[6], wf1[6], wf2[8];
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) {
+    wf0[kk] = *reinterpret_cast<const bf16x8*>(W0 + r32 * 96 + kk * 16 + h * 8);
+    wf1[kk] = *reinterpret_cast<const bf16x8*>(W1 + r32 * 96 + kk * 16 + h * 8);
+  }
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) wf2[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
+  const float bv0 = b0[r32], bv1 = b1[r32], bv2 = b2[r32];
   if (audio) {
     // input = first_conv(audio) at t = f ii (FastDiff_model.py:90), recomputed: no a0 tensor.
-    // One coalesced load of the samples [f ib - 3, f (ib + DB_TS + 14) + 4) (r02: 7 strided
-    // global loads per staged item made this block a chain of round trips, ~9x its siblings)
+    // The window [f ib - 3, f (ib + DB_TS + 14) + 4) arrives in ONE round trip: every thread's
+    // loads are unconditional (clamped address) and issued before any LDS store (r03: a
+    // branch-guarded load per loop trip made the first DBlock a chain of 3 round trips,
+    // ~10x the time of its sibling blocks per row).
     const long long t0 = (long long)ib * f - 3;
     const float* au = audio + (long long)b * Lin;
     const int na = (DB_TS + 14) * f + 8;
-    for (int i = tid; i < na; i += 256) {
-      const long long t = t0 + i;
-      AU[i] = (t >= 0 && t < Lin) ? au[t] : 0.f;
+    float av[DB_AUI];
+#pragma unroll
+    for (int it = 0; it < DB_AUI; ++it) {
+      const long long t = t0 + tid + 256 * it;
+      av[it] = au[t < 0 ? 0 : t >= Lin ? Lin - 1 : t];
     }
-    if (tid < 224) FWS[(tid % 7) * 32 + tid / 7] = fw[tid];   // fw is [c][tap]
-    if (tid < 32) FWS[224 + tid] = fb[tid];
+    const float fwv = tid < 224 ? fw[tid] : 0.f, fbv = tid < 32 ? fb[tid] : 0.f;
+#pragma unroll
+    for (int it = 0; it < DB_AUI; ++it) {
+      const int i = tid + 256 * it;
+      const long long t = t0 + i;
+      if (i < na) AU[i] = (t >= 0 && t < Lin) ? av[it] : 0.f;
+    }
+    if (tid < 224) FWS[(tid % 7) * 32 + tid / 7] = fwv;   // fw is [c][tap]
+    if (tid < 32) FWS[224 + tid] = fbv;
     __syncthreads();
   }
   // staging: every thread's (<= DB_NI) items are loaded before any is converted, so their
@@ -2122,17 +2146,6 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
     }
     sv[u] = v;
   }
-  // every stage's weight fragments, issued behind the staging loads (vmcnt retires in order: the
-  // staging stores below wait only for the staging loads) -- no L2 round trip per conv stage
-  bf16x8 wf0[6], wf1[6], wf2[8];
-#pragma unroll
-  for (int kk = 0; kk < 6; ++kk) {
-    wf0[kk] = *reinterpret_cast<const bf16x8*>(W0 + r32 * 96 + kk * 16 + h * 8);
-    wf1[kk] = *reinterpret_cast<const bf16x8*>(W1 + r32 * 96 + kk * 16 + h * 8);
-  }
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) wf2[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
-  const float bv0 = b0[r32], bv1 = b1[r32], bv2 = b2[r32];
 #pragma unroll
   for (int u = 0; u < DB_NI; ++u) {
     const int i = tid + 256 * u;
@@ -2532,7 +2545,7 @@ __global__ __launch_bounds__(256) void final_conv_kernel(const float* __restrict
                                                          float* eps_out, float* xa, float ce, float den,
                                                          float sig, const float* noise,
                                                          unsigned long long seed, unsigned stream,
-                                                         long long L) {
+                                                         const int* uid, long long L) {
   // rows of 36 floats (144 B): 16-B reads, slot 9*row mod 16 -> conflict-free across lanes
   __shared__ __attribute__((aligned(16))) float xs[262 * 36];
   __shared__ __attribute__((aligned(16))) float wsh[7 * 32];
@@ -2564,7 +2577,7 @@ __global__ __launch_bounds__(256) void final_conv_kernel(const float* __restrict
   if (eps_out) eps_out[idx] = e;
   if (xa) {
     float v = (xa[idx] - ce * e) / den;
-    if (sig != 0.f) v += sig * (noise ? noise[idx] : philox_normal(seed, (unsigned long long)idx, stream));
+    if (sig != 0.f) v += sig * (noise ? noise[idx] : philox_normal_u(seed, utt_id(uid, b), (unsigned)t, stream));
     xa[idx] = v;
   }
 }
@@ -2754,6 +2767,7 @@ struct FdFinal {
   float ce, den, sig;
   unsigned long long seed;
   unsigned stream;
+  const int* uid;
 };
 
 template <int TS, bool UPS, bool AUD, bool FIN, bool PF, bool SUB = false>
@@ -2914,7 +2928,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       if (fuse_fin) {
         la.audio_out = fin->audio_out + (size_t)b0 * L; la.noise = fin->noise ? fin->noise + (size_t)b0 * L : nullptr;
         la.ce = fin->ce; la.den = fin->den;
-        la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream;
+        la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream; la.uid = fin->uid;
       }
       // (the LDS image holds upsample weights for r <= 4 with the audio fusions, r <= 8 without)
       const bool skew_path = !stream_path && m->lvc_skew && ups && hop >= 64 && (hop & (hop - 1)) == 0 &&
@@ -3246,14 +3260,14 @@ int fd_forward(const fd_model* m, const float* audio, const float* cond, const f
   if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, ws + W.condT, ws + W.nz, 1, B, Tc, st));
   PD_TRY(fd_net(m, ws, W, audio, ws + W.condT, ws + W.nz, 0, B, Tc, &x, st));
   hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w, m->final_b,
-                     eps, (float*)nullptr, 0.f, 0.f, 0.f, (const float*)nullptr, 0ull, 0u, L);
+                     eps, (float*)nullptr, 0.f, 0.f, 0.f, (const float*)nullptr, 0ull, 0u, (const int*)nullptr, L);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
 
 int fd_sample(const fd_model* m, const float* mel, const float* beta, const float* alpha, const float* sigma,
               const float* steps, int N, const float* x_T, const float* noise, unsigned long long seed,
-              float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream) {
+              const int* utt_ids, float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream) {
   PD_CHECK_ARG(m && mel && beta && alpha && sigma && steps && wav && workspace, "null pointer");
   PD_CHECK_ARG(B > 0 && Tc > 0 && N >= 1, "bad B/T'/N");
   // Long schedules (the 200- and 1000-step ones, fastdiff.py:58-61) run in chunks of
@@ -3275,7 +3289,7 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
   if (x_T) {
     PD_HIP(hipMemcpyAsync(cur, x_T, sizeof(float) * B * L, hipMemcpyDeviceToDevice, st));
   } else {
-    PD_TRY(fill_normal(cur, B * L, seed, 0xFFFF0001u, st));
+    PD_TRY(fill_normal_utt(cur, B, L, seed, 0xFFFF0001u, utt_ids, st));
   }
   const bool side = fd_kp_side(m);
   if (side && !m->side) {
@@ -3319,7 +3333,7 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
       const float den = sqrtf(1.f - beta[n]);
       const float sg = n > 0 ? sigma[n] : 0.f;
       const FdFinal fin{other, noise ? noise + (size_t)j * B * L : (const float*)nullptr, ce, den, sg, seed,
-                        0x10000u + j};
+                        0x10000u + j, utt_ids};
       PD_TRY(fd_net(m, ws, W, cur, mel, ws + W.nz + (size_t)jl * B * nb * CC, jl, B, Tc, &x, st,
                     fused ? &fin : nullptr, side));
       if (x == nullptr) {   // updated inside the last LVC block
@@ -3329,7 +3343,7 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
       {
         ProfScope ps("fd_final_update", st);
         hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w,
-                           m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + j, L);
+                           m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + j, utt_ids, L);
       }
       PD_LAUNCH_CHECK();
     }

@@ -76,6 +76,7 @@ struct GemmArgs {
   int noise_ld;
   unsigned long long seed;
   unsigned int stream_id;
+  const int* uid;           // POSTERIOR: utterance id per batch row (null -> row index)
   int ksplit;               // STORE, > 1: split-K -- blockIdx.z sums one K range into `part`,
   float* part;              //   [ksplit][B*T][N] fp32, and gemm_splitk_reduce applies the epilogue
 };
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
             float x = a.c1 * v + a.c2 * xt;
             if (a.sigma != 0.f) {
               float z = a.noise ? a.noise[(long long)b * a.noise_bs + (long long)t * a.noise_ld + n]
-                                : philox_normal(a.seed, ((unsigned long long)R) * a.N + n, a.stream_id);
+                                : philox_normal_u(a.seed, utt_id(a.uid, b), (unsigned)(t * a.N + n), a.stream_id);
               x += a.sigma * z;
             }
             a.out[oi] = x;

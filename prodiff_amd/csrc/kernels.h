@@ -56,8 +56,10 @@ void register_bf16_pool(const float* base, size_t n, const __bf16* bf);
 void unregister_bf16_pool(const float* base);
 const __bf16* lookup_bf16(const float* p);
 
-// Philox fills: U[0,1) or N(0,1), element i of stream `stream` under `seed`.
-int fill_uniform(float* out, long long n, unsigned long long seed, unsigned stream, hipStream_t st);
-int fill_normal(float* out, long long n, unsigned long long seed, unsigned stream, hipStream_t st);
+// Philox fills, U[0,1) or N(0,1), per utterance (common.h philox_*_u): out[b][e], e < per, keyed by utt_id(ids, b).
+int fill_uniform_utt(float* out, int B, long long per, unsigned long long seed, unsigned stream, const int* ids,
+                     hipStream_t st);
+int fill_normal_utt(float* out, int B, long long per, unsigned long long seed, unsigned stream, const int* ids,
+                    hipStream_t st);
 
 }  // namespace pd

@@ -391,26 +391,30 @@ const __bf16* lookup_bf16(const float* p) {
 }
 
 // ---------------------------------------------------------------- RNG fills
-__global__ void fill_uniform_kernel(float* out, long long n, unsigned long long seed, unsigned stream) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = philox_uniform(seed, (unsigned long long)i, stream);
+__global__ void fill_utt_kernel(float* out, long long per, unsigned long long seed, unsigned stream, const int* ids,
+                                bool normal) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (e >= per) return;
+  const unsigned u = utt_id(ids, b);
+  out[(long long)b * per + e] =
+      normal ? philox_normal_u(seed, u, (unsigned)e, stream) : philox_uniform_u(seed, u, (unsigned)e, stream);
 }
-__global__ void fill_normal_kernel(float* out, long long n, unsigned long long seed, unsigned stream) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = philox_normal(seed, (unsigned long long)i, stream);
-}
-
-int fill_uniform(float* out, long long n, unsigned long long seed, unsigned stream, hipStream_t st) {
-  if (n == 0) return PD_OK;
-  hipLaunchKernelGGL(fill_uniform_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, out, n, seed, stream);
+static int fill_utt(float* out, int B, long long per, unsigned long long seed, unsigned stream, const int* ids,
+                    bool normal, hipStream_t st) {
+  if (B == 0 || per == 0) return PD_OK;
+  PD_CHECK_ARG(per < (1ll << 32), "per-utterance draw index exceeds 32 bits");
+  hipLaunchKernelGGL(fill_utt_kernel, dim3(cdiv(per, 256), B), dim3(256), 0, st, out, per, seed, stream, ids, normal);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
-int fill_normal(float* out, long long n, unsigned long long seed, unsigned stream, hipStream_t st) {
-  if (n == 0) return PD_OK;
-  hipLaunchKernelGGL(fill_normal_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, out, n, seed, stream);
-  PD_LAUNCH_CHECK();
-  return PD_OK;
+int fill_uniform_utt(float* out, int B, long long per, unsigned long long seed, unsigned stream, const int* ids,
+                     hipStream_t st) {
+  return fill_utt(out, B, per, seed, stream, ids, false, st);
+}
+int fill_normal_utt(float* out, int B, long long per, unsigned long long seed, unsigned stream, const int* ids,
+                    hipStream_t st) {
+  return fill_utt(out, B, per, seed, stream, ids, true, st);
 }
 
 // ---------------------------------------------------------------- profiling

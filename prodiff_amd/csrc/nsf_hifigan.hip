@@ -73,11 +73,11 @@ constexpr unsigned NSF_STREAM_INI = 0x4e534600u, NSF_STREAM_NOISE = 0x4e534601u;
 // rad_values of SineGen._f02sine (models.py:137-141), bit-for-bit in fp32:
 // fn = f0 * (h+1); rad = fmod(fn / sr, 1); frame 0 adds rand_ini[h] (rand_ini[0] = 0).
 __device__ __forceinline__ float nsf_rad(float f0, int h, int f, float sr, const float* rand_ini,
-                                         unsigned long long seed, int b, int dim) {
+                                         unsigned long long seed, const int* uid, int b) {
   float fn = __fmul_rn(f0, (float)(h + 1));
   float r = fmodf(__fdiv_rn(fn, sr), 1.0f);
   if (f == 0 && h > 0) {
-    float ini = rand_ini ? rand_ini[h] : philox_uniform(seed, (unsigned long long)b * dim + h, NSF_STREAM_INI);
+    float ini = rand_ini ? rand_ini[h] : philox_uniform_u(seed, utt_id(uid, b), (unsigned)h, NSF_STREAM_INI);
     r = __fadd_rn(r, ini);
   }
   return r;
@@ -92,6 +92,7 @@ __global__ __launch_bounds__(NSF_PP_THREADS) void nsf_phase_prefix_kernel(const 
                                                                         int dim, float sr,
                                                                         const float* __restrict__ rand_ini,
                                                                         unsigned long long seed,
+                                                                        const int* __restrict__ uid,
                                                                         double* __restrict__ P,
                                                                         float* __restrict__ Rd) {
   __shared__ double part[NSF_PP_THREADS];
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(NSF_PP_THREADS) void nsf_phase_prefix_kernel(const 
   const int run = (T + NSF_PP_THREADS - 1) / NSF_PP_THREADS, fa = tid * run, fb = min(fa + run, T);
   double acc = 0.0;
   for (int f = fa; f < fb; ++f) {
-    const float r = nsf_rad(f0[(long long)b * T + f], h, f, sr, rand_ini, seed, b, dim);
+    const float r = nsf_rad(f0[(long long)b * T + f], h, f, sr, rand_ini, seed, uid, b);
     Rd[((long long)b * T + f) * dim + h] = r;
     acc += (double)r;
   }
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(256) void nsf_source_kernel(const float* __restrict
                                                          int B, int T, int upp, int dim, float sr,
                                                          const float* __restrict__ rand_ini,
                                                          const float* __restrict__ noise, unsigned long long seed,
-                                                         const float* __restrict__ lw, const float* __restrict__ lb,
+                                                         const int* __restrict__ uid, const float* __restrict__ lw, const float* __restrict__ lb,
                                                          float* __restrict__ har) {
   const long long L = (long long)T * upp;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(256) void nsf_source_kernel(const float* __restrict
     ph -= floor(ph);
     float s = (float)sin(ph * 6.283185307179586) * NSF_SINE_AMP;
     long long ni = i * dim + h;
-    float z = noise ? noise[ni] : philox_normal(seed, (unsigned long long)ni, NSF_STREAM_NOISE);
+    float z = noise ? noise[ni] : philox_normal_u(seed, utt_id(uid, b), (unsigned)(t * dim + h), NSF_STREAM_NOISE);
     acc = fmaf(lw[h], s * uv + namp * z, acc);
   }
   har[i] = tanhf(acc + lb[0]);
@@ -1096,7 +1097,8 @@ size_t nsf_workspace_size(const nsf_model* m, int B, int T) {
 }
 
 int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const float* f0, const float* rand_ini, const float* noise,
-                unsigned long long seed, float* wav, int B, int T, void* workspace, size_t ws_bytes, void* stream) {
+                unsigned long long seed, const int* utt_ids, float* wav, int B, int T, void* workspace, size_t ws_bytes,
+                void* stream) {
   PD_CHECK_ARG(m && mel && f0 && wav && B >= 0 && T >= 0, "null argument");
   if (B == 0 || T == 0) return PD_OK;
   const NsfWs W = nsf_layout(m, B, T);
@@ -1115,9 +1117,9 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
     ProfScope ps("nsf_source", st);
     float* Rd = ws + W.Rd;
     hipLaunchKernelGGL(nsf_phase_prefix_kernel, dim3(B * dim), dim3(NSF_PP_THREADS), 0, st, f0, B, T, dim, sr,
-                       rand_ini, seed, P, Rd);
+                       rand_ini, seed, utt_ids, P, Rd);
     hipLaunchKernelGGL(nsf_source_kernel, dim3(cdiv((long long)B * L, 256)), dim3(256), 0, st, f0, P, Rd, B, T, m->upp,
-                       dim, sr, rand_ini, noise, seed, m->lin_w, m->lin_b, har);
+                       dim, sr, rand_ini, noise, seed, utt_ids, m->lin_w, m->lin_b, har);
   }
   PD_LAUNCH_CHECK();
   // conv_pre(mel_scale * mel^T) (nsf_hifigan.py:53, models.py:267)

@@ -923,7 +923,7 @@ int pd_wavenet_forward(const pd_wavenet* h, const float* spec, const float* step
 
 int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1, const float* coef2,
                       const float* sigma, int S, const float* x_T, const float* noise,
-                      unsigned long long seed, float* mel, int B, int T, void* workspace,
+                      unsigned long long seed, const int* utt_ids, float* mel, int B, int T, void* workspace,
                       size_t ws_bytes, void* stream) {
   PD_CHECK_ARG(h && cond && coef1 && coef2 && sigma && mel && workspace, "null pointer");
   PD_CHECK_ARG(B > 0 && T > 0 && S >= 1 && S <= 64, "bad B/T/S");
@@ -937,7 +937,7 @@ int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1
   if (x_T) {
     PD_HIP(hipMemcpyAsync(mel, x_T, sizeof(float) * BTM, hipMemcpyDeviceToDevice, st));
   } else {
-    PD_TRY(fill_uniform(mel, BTM, seed, 0xFFFF0000u, st));
+    PD_TRY(fill_uniform_utt(mel, B, (long long)T * M, seed, 0xFFFF0000u, utt_ids, st));
   }
   // all S steps' embeddings at once: step index i = S-1-j for the j-th pass
   PD_TRY(fill_reverse_steps(ws + Lw.steps, S, B, S - 1, st));
@@ -954,7 +954,7 @@ int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1
     a.sigma = (i == 0) ? 0.f : sigma[i];
     a.noise = noise ? noise + (size_t)j * BTM : nullptr;
     a.noise_bs = BTs * M; a.noise_ld = M;
-    a.seed = seed; a.stream_id = (unsigned)j;
+    a.seed = seed; a.stream_id = (unsigned)j; a.uid = utt_ids;
     PD_TRY((launch_small_gemm<EPI_POSTERIOR, U_WN_POSTERIOR>(a, st, "wn_outproj_posterior")));
   }
   return PD_OK;
@@ -1011,7 +1011,8 @@ size_t pd_reflow_workspace_size(const pd_wavenet* h, int B, int T, int S, int al
 }
 
 int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, float time_scale,
-                     const float* x_T, unsigned long long seed, float* x, int B, int T, void* workspace,
+                     const float* x_T, unsigned long long seed, const int* utt_ids, float* x, int B, int T,
+                     void* workspace,
                      size_t ws_bytes, void* stream) {
   PD_CHECK_ARG(h && cond && x && workspace, "null pointer");
   RkTableau tb;
@@ -1031,7 +1032,7 @@ int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, fl
   if (x_T) {
     PD_HIP(hipMemcpyAsync(x, x_T, sizeof(float) * BTM, hipMemcpyDeviceToDevice, st));
   } else {
-    PD_TRY(fill_normal(x, BTM, seed, 0xFFFF0002u, st));
+    PD_TRY(fill_normal_utt(x, B, (long long)T * M, seed, 0xFFFF0002u, utt_ids, st));
   }
   // every evaluation's step value, float32 as the reference forms it (reflow.py:89-98):
   // t = i * float32(dt), a stage at t + float32(c dt), then time_scale * (.)

@@ -261,10 +261,11 @@ class FastDiff(nn.Module):
         return eps
 
     @torch.no_grad()
-    def sample(self, mel, beta, alpha, sigma, steps, x_T=None, noise=None, seed=None):
+    def sample(self, mel, beta, alpha, sigma, steps, x_T=None, noise=None, seed=None, utt_ids=None):
         """Fused reverse process.  mel [B,T',80] TIME-major (the ProDiff output);
         beta/alpha/sigma/steps: float32 arrays of the reverse schedule;
-        x_T [B,1,L] / noise [N-1,B,1,L] optional explicit draws -> wav [B,1,L]."""
+        x_T [B,1,L] / noise [N-1,B,1,L] optional explicit draws -> wav [B,1,L].
+        Missing draws: on-device Philox keyed by ``seed`` and each row's ``utt_ids``."""
         h = self.handle()
         B, Tc, _ = mel.shape
         N = len(steps)
@@ -278,10 +279,11 @@ class FastDiff(nn.Module):
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         wav = torch.empty(B, 1, L, device=dev, dtype=torch.float32)
+        uid = _lib.utt_ids(utt_ids, B, dev)
         lib = _lib.lib()
         ws, wsb = self._ws.get(lib.fd_workspace_size(h, B, Tc, N), dev)
         _lib.check(lib.fd_sample(h, _lib.fptr(mel), _lib.farr(beta), _lib.farr(alpha), _lib.farr(sigma),
-                                 _lib.farr(steps), N, _lib.fptr(xT), _lib.fptr(nz), seed, _lib.fptr(wav),
+                                 _lib.farr(steps), N, _lib.fptr(xT), _lib.fptr(nz), seed, _lib.iptr(uid), _lib.fptr(wav),
                                  B, Tc, ws, wsb, _lib.stream_ptr(dev)))
         return wav
 

@@ -200,10 +200,11 @@ class Generator(nn.Module):
 
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
-    def synthesize(self, mel, f0, mel_scale=1.0, rand_ini=None, noise=None, seed=None):
+    def synthesize(self, mel, f0, mel_scale=1.0, rand_ini=None, noise=None, seed=None, utt_ids=None):
         """mel [B,T,M] time-major, f0 [B,T] -> wav [B, T*hop].  rand_ini [dim] / noise
         [B, T*hop, dim] replay the reference's torch.rand / randn_like draws
-        (models.py:139,182); None draws them on the device (Philox, `seed`)."""
+        (models.py:139,182); None draws them on the device (Philox, `seed` and each row's
+        ``utt_ids``)."""
         h = self.handle()
         dev = mel.device
         mel = mel.float().contiguous()
@@ -216,10 +217,11 @@ class Generator(nn.Module):
         ri = None if rand_ini is None else rand_ini.to(dev).float().contiguous().reshape(-1)
         nz = None if noise is None else noise.to(dev).float().contiguous()
         wav = torch.empty(B, T * self.upp, device=dev, dtype=torch.float32)
+        uid = _lib.utt_ids(utt_ids, B, dev)
         L = _lib.lib()
         ws, wsb = self._ws.get(L.nsf_workspace_size(h, B, T), dev)
         _lib.check(L.nsf_forward(h, _lib.fptr(mel), float(mel_scale), _lib.fptr(f0), _lib.fptr(ri), _lib.fptr(nz),
-                                 int(seed), _lib.fptr(wav), B, T, ws, wsb, _lib.stream_ptr(dev)))
+                                 int(seed), _lib.iptr(uid), _lib.fptr(wav), B, T, ws, wsb, _lib.stream_ptr(dev)))
         return wav
 
     def forward(self, x, f0, **kw):
@@ -277,7 +279,8 @@ class NsfHifiGAN(BaseVocoder):
         if f0 is None:
             raise TypeError("NSF-HiFiGAN needs f0 (Generator.forward(x, f0), models.py:265)")
         wav = self.model.synthesize(mel, f0, LOG10_TO_LN, rand_ini=kwargs.get("rand_ini"),
-                                    noise=kwargs.get("noise"), seed=kwargs.get("seed"))
+                                    noise=kwargs.get("noise"), seed=kwargs.get("seed"),
+                                    utt_ids=kwargs.get("utt_ids"))
         return wav.view(-1)
 
     def spec2wav(self, mel, **kwargs):

@@ -59,10 +59,12 @@ class Synthesizer:
         return cls(gd, voc)
 
     @torch.no_grad()
-    def __call__(self, cond, seed=None):
+    def __call__(self, cond, seed=None, utt_ids=None):
+        """Random draws are keyed by (seed, utterance id): row i of the batch is utterance
+        ``utt_ids[i]`` (default i), and its output does not depend on the other rows."""
         g = None if seed is None else 2 * seed
-        mel = self.diffusion.sample(cond, seed=g)
-        wav = self.vocoder.spec2wav_torch(mel, seed=None if seed is None else g + 1)
+        mel = self.diffusion.sample(cond, seed=g, utt_ids=utt_ids)
+        wav = self.vocoder.spec2wav_batch(mel, seed=None if seed is None else g + 1, utt_ids=utt_ids)
         return mel, wav
 
 
@@ -152,11 +154,12 @@ class SvsSynthesizer:
         return cond
 
     @torch.no_grad()
-    def __call__(self, batch, seed=None):
+    def __call__(self, batch, seed=None, utt_ids=None):
         g = None if seed is None else 3 * seed
         cond = self.condition(batch)
-        mel = self.diffusion.sample(cond, infer_step=self.infer_step, seed=g)
-        wav = self.generator.synthesize(mel, batch["f0"], LOG10_TO_LN, seed=None if seed is None else g + 1)
+        mel = self.diffusion.sample(cond, infer_step=self.infer_step, seed=g, utt_ids=utt_ids)
+        wav = self.generator.synthesize(mel, batch["f0"], LOG10_TO_LN, seed=None if seed is None else g + 1,
+                                        utt_ids=utt_ids)
         return mel, wav
 
 
@@ -230,14 +233,17 @@ def length_groups(lengths, idx):
     return sorted(groups.items(), key=lambda kv: -kv[0])
 
 
-def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None):
+def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None):
     """Synthesize utterances sharded over the ranks of the default process group
     (SURVEY §8(e)); the reference runs them one by one, B=1 per segment
     (handler/infer/handler.py:373-388).
 
-    synth_fn(cond [B,T,H], seed) -> (mel [B,T,M], wav [B,T*hop]): one rank's
+    synth_fn(cond [B,T,H], seed, utt_ids) -> (mel [B,T,M], wav [B,T*hop]): one rank's
       batched synthesis (a ``Synthesizer``; an ``SvsSynthesizer`` takes per-utterance
-      input dicts, batched by its ``collate``).
+      input dicts, batched by its ``collate``).  Every batch gets the same ``seed`` and
+      the global indices of its utterances as ``utt_ids``, and the samplers key their
+      random draws by (seed, utterance id): an utterance's mel and waveform are the same
+      at any world size and in any batch position.
     conds: list over ALL utterances (same order on every rank) of [T_i,H] tensors
       on this rank's device, or (T_i, callable returning one) pairs, so that only
       this rank's shard is materialized.
@@ -245,7 +251,10 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     shard in equal-length batches, flattens its outputs, and one ragged gather
     per output kind brings them to the root, which un-permutes them.  The plan is
     deterministic, so no shape exchange is needed.  Returns on the root the lists
-    [mel_i [T_i,M]], [wav_i [T_i*hop]] in input order; (None, None) elsewhere."""
+    [mel_i [T_i,M]], [wav_i [T_i*hop]] in input order; (None, None) elsewhere.
+    ``stats`` (a dict, optional) receives this rank's ``compute_ms`` (its shard's
+    synthesis, device-synchronized) and ``gather_ms`` (the collectives after it)."""
+    import time
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     lengths = [int(c.shape[0]) if torch.is_tensor(c) else int(c[0]) for c in conds]
@@ -253,9 +262,15 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     mel_parts, wav_parts, order = [], [], []
     M = None
     collate = getattr(synth_fn, "collate", torch.stack)
-    for g, (T, idx) in enumerate(length_groups(lengths, shards[rank])):
+
+    def sync():
+        if stats is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+    t0 = time.perf_counter()
+    for T, idx in length_groups(lengths, shards[rank]):
         cb = collate([conds[i] if torch.is_tensor(conds[i]) else conds[i][1]() for i in idx])
-        mel, wav = synth_fn(cb, seed + 7919 * g + 104729 * rank)
+        mel, wav = synth_fn(cb, seed, utt_ids=idx)
         M = mel.shape[-1]
         mel_parts.append(mel.reshape(-1))
         wav_parts.append(wav.reshape(-1))
@@ -269,6 +284,8 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         wav_flat = torch.zeros(0, device=dev)
     else:
         mel_flat, wav_flat = torch.cat(mel_parts), torch.cat(wav_parts)
+    sync()
+    t1 = time.perf_counter()
     if world == 1:
         mels_all, wavs_all = [mel_flat], [wav_flat]
     else:
@@ -280,6 +297,10 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         wav_shapes = [(sum(lengths[i] for i in s) * hop,) for s in shards]
         mels_all = gather_to_root(mel_flat, root, mel_shapes)
         wavs_all = gather_to_root(wav_flat, root, wav_shapes)
+    sync()
+    if stats is not None:
+        stats["compute_ms"] = (t1 - t0) * 1e3
+        stats["gather_ms"] = (time.perf_counter() - t1) * 1e3
     if rank != root:
         return None, None
     mels, wavs = [None] * len(lengths), [None] * len(lengths)

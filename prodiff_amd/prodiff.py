@@ -229,13 +229,15 @@ class GaussianDiffusion(nn.Module):
         return self._coef_cache[1:]
 
     @torch.no_grad()
-    def sample(self, cond, infer_step=4, x_T=None, noise=None, seed=None, workspace=None):
+    def sample(self, cond, infer_step=4, x_T=None, noise=None, seed=None, workspace=None, utt_ids=None):
         """cond [B,T,H] -> mel [B,T,M].
 
         x_T: [B,1,M,T] draw (reference layout, prodiff.py:147) or None;
         noise: [S,B,1,M,T] per-step draws in sampling order, or None.
         Missing draws come from the on-device Philox generator keyed by ``seed``
-        (default: drawn from torch's CPU generator, so torch.manual_seed applies).
+        (default: drawn from torch's CPU generator, so torch.manual_seed applies) and
+        by each row's utterance id (``utt_ids``, default 0..B-1): a row's draws do not
+        depend on the rest of the batch.
         ``workspace``: a ``_lib.Workspace`` to use instead of the module's own (capture)."""
         if not isinstance(self.denoise_fn, WaveNet):
             raise TypeError("GaussianDiffusion needs a prodiff_amd.WaveNet denoise_fn")
@@ -253,16 +255,17 @@ class GaussianDiffusion(nn.Module):
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         c1, c2, sg = self._step_scalars()
         mel = torch.empty(B, T, M, device=dev, dtype=torch.float32)
+        uid = _lib.utt_ids(utt_ids, B, dev)
         L = _lib.lib()
         nbytes = L.pd_wavenet_workspace_size(h, B, T, S)
         ws, wsb = (workspace or self._ws).get(nbytes, dev)
         _lib.check(L.pd_prodiff_sample(h, _lib.fptr(cond), _lib.farr(c1), _lib.farr(c2), _lib.farr(sg), S,
-                                       _lib.fptr(xT), _lib.fptr(nz), seed, _lib.fptr(mel), B, T, ws, wsb,
+                                       _lib.fptr(xT), _lib.fptr(nz), seed, _lib.iptr(uid), _lib.fptr(mel), B, T, ws, wsb,
                                        _lib.stream_ptr(dev)))
         return mel
 
     @torch.no_grad()
-    def capture(self, cond, infer_step=4, seed=0, x_T=None, noise=None):
+    def capture(self, cond, infer_step=4, seed=0, x_T=None, noise=None, utt_ids=None):
         """Record the whole reverse process for cond's shape as ONE hipGraph.
 
         The library's calls are stream-ordered and allocation-free, so
@@ -277,13 +280,15 @@ class GaussianDiffusion(nn.Module):
         xT = None if x_T is None else x_T.float().contiguous().clone()
         nz = None if noise is None else noise.float().contiguous().clone()
         ws = _lib.Workspace()    # the graph's own: later eager calls may grow (reallocate) self._ws
-        self.sample(cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz, workspace=ws)   # packs, sizes ws
+        uid = _lib.utt_ids(utt_ids, cond.shape[0], cond.device)
+        self.sample(cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz, workspace=ws, utt_ids=uid)   # packs, sizes ws
         torch.cuda.synchronize()
         static_cond = cond.clone()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            mel = self.sample(static_cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz, workspace=ws)
-        return SampleGraph(g, static_cond, mel, self.denoise_fn, keep=(ws, xT, nz))
+            mel = self.sample(static_cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz, workspace=ws,
+                              utt_ids=uid)
+        return SampleGraph(g, static_cond, mel, self.denoise_fn, keep=(ws, xT, nz, uid))
 
     def forward(self, cond, src_spec=None, gt_spec=None, infer_step=4, infer=False):
         if not infer:

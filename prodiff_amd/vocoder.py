@@ -111,17 +111,24 @@ class FastDiff(BaseVocoder):
         return self
 
     @torch.no_grad()
-    def spec2wav_torch(self, mel, f0=None, x_T=None, noise=None, seed=None, **kwargs):
-        """mel [B,T,80] (or [T,80]) on the device -> wav [B, T*hop] (f0 unused: FastDiff is not NSF)."""
-        squeeze = mel.dim() == 2
-        if squeeze:
-            mel = mel[None]
+    def spec2wav_batch(self, mel, x_T=None, noise=None, seed=None, utt_ids=None):
+        """mel [B,T,80] on the device -> wav [B, T*hop], one row per utterance."""
         b, a, s, st = self.sched
-        wav = self.model.sample(mel.to(self.device), b, a, s, st, x_T=x_T, noise=noise, seed=seed)[:, 0]
-        return wav[0] if squeeze else wav
+        return self.model.sample(mel.to(self.device), b, a, s, st, x_T=x_T, noise=noise, seed=seed,
+                                 utt_ids=utt_ids)[:, 0]
+
+    @torch.no_grad()
+    def spec2wav_torch(self, mel, f0=None, x_T=None, noise=None, seed=None, **kwargs):
+        """mel [B,T,80] (or [T,80]) on the device -> wav flattened to [B*T*hop], the vocoder
+        contract InferHandler consumes (component/vocoder/nsf_hifigan.py:55-57 `view(-1)`,
+        handler/infer/handler.py:157,351); f0 is unused (FastDiff is not NSF).  Batched
+        callers that want one row per utterance use ``spec2wav_batch``."""
+        if mel.dim() == 2:
+            mel = mel[None]
+        return self.spec2wav_batch(mel, x_T=x_T, noise=noise, seed=seed, utt_ids=kwargs.get("utt_ids")).reshape(-1)
 
     def spec2wav(self, mel, **kwargs):
         """fastdiff.py:117-126: mel np [T,80] -> np [1,1,T*hop]."""
         c = torch.as_tensor(np.asarray(mel), dtype=torch.float32, device=self.device)[None]
-        wav = self.spec2wav_torch(c, **kwargs)
+        wav = self.spec2wav_batch(c, x_T=kwargs.get("x_T"), noise=kwargs.get("noise"), seed=kwargs.get("seed"))
         return wav[:, None].cpu().numpy()

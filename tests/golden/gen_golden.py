@@ -169,6 +169,14 @@ def gen_schedules():
                                    spec_min=[-12], spec_max=[0])
             for k, v in gd.state_dict().items():
                 out[f"t{ts}_mb{mb}_{k}"] = v.numpy()
+    # the other ProDiff schedule types (prodiff.py:27-46); logsnr yields betas outside
+    # (0, 1) and NaN buffers in the reference -- recorded as they are
+    for st in ("linear", "cosine", "logsnr"):
+        for ts in (4, 100):
+            gd = GaussianDiffusion(out_dims=4, denoise_fn=None, timesteps=ts, max_beta=0.06,
+                                   schedule_type=st, spec_min=[-12], spec_max=[0])
+            for k, v in gd.state_dict().items():
+                out[f"{st}_t{ts}_{k}"] = v.numpy()
     # FastDiff: training linear schedule (fastdiff.py:44-51) and the reverse
     # schedules (fastdiff.py:62-73) mapped to fractional steps (util.py:187-206)
     beta = torch.linspace(1e-6, 0.01, 1000)
@@ -239,12 +247,23 @@ def gen_fastdiff():
     save("fastdiff_fwd", seed=seed, audio=audio, c=c, steps=steps, eps=eps,
          **{"cap_" + k: v for k, v in keep.items()})
 
-    # sampler, 4-iter and 3-iter schedules
-    for n_iter, (B, Tc, seed_s) in {4: (2, 6, 41), 3: (1, 5, 42)}.items():
+    gen_fastdiff_samples({4: (2, 6, 41), 3: (1, 5, 42)})
+
+
+def gen_fastdiff_samples(cases=None):
+    """Sampler goldens.  Default (`gen_golden.py fastdiff_samples`): the 6- and 8-step
+    noise-predictor tables (fastdiff.py:64-70) and the 200-step linspace schedule
+    and the 1000-step one (fastdiff.py:60-63), which run through fd_sample's 16-step chunk loop."""
+    seed = 31
+    m, _ = build_fastdiff(seed)
+    cases = cases or {6: (2, 3, 43), 8: (1, 4, 44), 200: (1, 2, 45), 1000: (1, 1, 46)}
+    for n_iter, (B, Tc, seed_s) in cases.items():
         L = Tc * 256
         c = synth.synth_inputs(seed_s + 2, (B, 80, Tc), loc=-5.0, scale=2.0)
         dh = fd_util.compute_hyperparams_given_schedule(torch.linspace(1e-6, 0.01, 1000))
-        sched = torch.FloatTensor(FASTDIFF_SCHEDULES[n_iter])
+        sched = (torch.FloatTensor(FASTDIFF_SCHEDULES[n_iter]) if n_iter in FASTDIFF_SCHEDULES
+                 else torch.linspace(0.0001, 0.02, 200) if n_iter == 200
+                 else torch.linspace(0.000001, 0.01, 1000))
         draws, seen_steps = [], []
         cnt = [0]
 

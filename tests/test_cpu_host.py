@@ -35,7 +35,7 @@ def test_null_arguments_fail_loudly():
     lib = _lib.lib()
     rc = lib.pd_wavenet_forward(None, None, None, None, None, 1, 1, None, 0, None)
     assert rc == 1 and b"null" in lib.pd_last_error()
-    assert lib.fd_sample(None, None, None, None, None, None, 4, None, None, 0, None, 1, 1, None, 0, None) == 1
+    assert lib.fd_sample(None, None, None, None, None, None, 4, None, None, 0, None, None, 1, 1, None, 0, None) == 1
 
 
 def test_wavenet_state_dict_matches_reference_names():
@@ -77,6 +77,20 @@ def test_prodiff_schedules_match_reference():
             betas = S.get_noise_schedule_list("vpsde", ts + 1, min_beta=0.1, max_beta=mb)
             for k, v in S.diffusion_buffers(betas).items():
                 np.testing.assert_allclose(v, s[f"t{ts}_mb{mb}_{k}"], rtol=1e-6, atol=0, err_msg=k)
+
+
+def test_prodiff_schedule_types_match_reference():
+    """linear / cosine / logsnr (prodiff.py:27-46) at max_beta 0.06.  logsnr returns
+    log-SNR values, not betas: the reference's buffers hold NaN/inf there, and so do ours."""
+    s = G.load("schedules")
+    for st in ("linear", "cosine", "logsnr"):
+        for ts in (4, 100):
+            betas = S.get_noise_schedule_list(st, ts + 1, min_beta=0.1, max_beta=0.06)
+            with np.errstate(all="ignore"):
+                bufs = S.diffusion_buffers(betas)
+            for k, v in bufs.items():
+                np.testing.assert_allclose(v, s[f"{st}_t{ts}_{k}"], rtol=1e-6, atol=0, equal_nan=True,
+                                           err_msg=f"{st} t{ts} {k}")
 
 
 def test_fastdiff_schedules_match_reference():

@@ -152,8 +152,12 @@ def test_fastdiff_forward_oracle_shapes(fdnet, B, Tc, step):
     assert_close(eps, OF.fastdiff_forward(pf, audio, c, st))
 
 
-@pytest.mark.parametrize("n_iter", [4, 3])
+@pytest.mark.parametrize("n_iter", [4, 3, 6, 8, 200, 1000])
 def test_fastdiff_sample_golden(fdnet, n_iter):
+    """Every reverse schedule of component/vocoder/fastdiff.py:58-73 against the reference
+    sampler (util.py:158-232) with its recorded draws.  200 and 1000 steps run through
+    fd_sample's 16-step chunk loop (13 and 63 chunks: step-embedding / kernel-predictor
+    batching per chunk, workspace reuse)."""
     m, _ = fdnet
     d = G.load(f"fastdiff_sample_n{n_iter}")
     s = G.load("schedules")

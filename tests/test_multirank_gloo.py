@@ -42,10 +42,13 @@ def test_length_groups_exact():
     assert g == [(7, [3, 4]), (5, [0]), (2, [5])]
 
 
-def stub_synth(cond, seed):
-    """A deterministic stand-in for Synthesizer: per-utterance (independent of the
-    batch it runs in and of the seed), mel [B,T,M], wav [B,T*HOP]."""
-    mel = cond[..., :M] * 2.0 + 1.0
+def stub_synth(cond, seed, utt_ids=None):
+    """A deterministic stand-in for Synthesizer: per-utterance (independent of the batch
+    it runs in), mel [B,T,M], wav [B,T*HOP].  Like the real samplers' draws it depends on
+    (seed, utterance id), so the test sees that every batch gets the job's seed and the
+    utterances' GLOBAL indices."""
+    ids = torch.as_tensor(list(range(cond.shape[0])) if utt_ids is None else utt_ids, dtype=torch.float32)
+    mel = cond[..., :M] * 2.0 + 1.0 + 1000.0 * ids[:, None, None] + seed
     wav = torch.repeat_interleave(cond[..., 0], HOP, dim=1) - cond[..., 1].sum(1, keepdim=True)
     return mel, wav
 
@@ -100,7 +103,7 @@ def test_distributed_synthesize_ragged(world, lengths):
     conds = _conds(lengths)
     assert len(mels) == len(lengths) == len(wavs)
     for i, c in enumerate(conds):
-        em, ew = stub_synth(c[None], 0)
+        em, ew = stub_synth(c[None], 0, utt_ids=[i])
         np.testing.assert_array_equal(mels[i], em[0].numpy())
         np.testing.assert_array_equal(wavs[i], ew[0].numpy())
         assert mels[i].shape == (lengths[i], M) and wavs[i].shape == (lengths[i] * HOP,)
@@ -131,7 +134,7 @@ class StubSvs:
     from prodiff_amd.pipeline import SvsSynthesizer as _S
     collate = staticmethod(_S.collate)
 
-    def __call__(self, batch, seed):
+    def __call__(self, batch, seed, utt_ids=None):
         n = torch.tensor(batch["ntok"], dtype=torch.float32)[:, None]
         tok_sum = batch["txt_tokens"].float().sum(1, keepdim=True)        # pads are 0: neutral
         mel = batch["f0"][..., None].repeat(1, 1, M) + tok_sum[..., None] + n[..., None]

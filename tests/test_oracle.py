@@ -88,7 +88,7 @@ def test_fastdiff_ops_oracle(fd):
     np.testing.assert_allclose(up, d["cap_upsample0"], atol=2e-5, rtol=0)
 
 
-@pytest.mark.parametrize("n_iter", [4, 3])
+@pytest.mark.parametrize("n_iter", [4, 3, 6, 8])
 def test_fastdiff_sample_oracle(n_iter):
     d = G.load(f"fastdiff_sample_n{n_iter}")
     s = G.load("schedules")
