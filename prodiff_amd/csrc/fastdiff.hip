@@ -569,15 +569,15 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   };
   if constexpr (PF) kload(0);
   // FIN: the sampler noise of this thread's output samples, drawn while the loads fly
-  constexpr int IF = FIN ? (2 * TS + G::NT - 1) / G::NT : 1;
+  constexpr int IF = FIN ? (TS + G::NT - 1) / G::NT : 1;
   float zr[IF];
   const float bfin = FIN ? P.bfin[0] : 0.f;
   if constexpr (FIN) {
 #pragma unroll
     for (int it = 0; it < IF; ++it) {
-      const int s2 = tid + it * G::NT, t = t0 + (s2 >> 1);
+      const int s = tid + it * G::NT, t = t0 + s;
       zr[it] = 0.f;
-      if (s2 < 2 * TS && (s2 & 1) == 0 && t < Lh && P.sig != 0.f)
+      if (s < TS && t < Lh && P.sig != 0.f)
         zr[it] = P.noise ? P.noise[base + t]
                          : philox_normal_u(P.seed, utt_id(P.uid, b + P.b_off), (unsigned)t, P.stream);
     }
@@ -937,41 +937,48 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   }
   LB_STAMP(14);
   if constexpr (FIN) {
-    // eps(t) = b + sum_{tap, c} w[tap][c] x(t + tap - 3)[c] on the centre rows; x rows
-    // [61, 67 + TS) go through fp32 LDS (aliasing U/Y: every wave is past its Y reads).
+    // eps(t) = b + sum_tap E[t + tap - 3][tap],  E[r][tap] = sum_c w[tap][c] x(r)[c]: each lane
+    // forms the 7 per-tap partial sums of its row from the x it holds (16 channels; the two
+    // channel halves meet by one lane swap), so only 7 floats per row go through LDS
+    // (aliasing U/Y: every wave is past its Y reads).  r03: the final conv read 28 x 16 B of
+    // fp32 x rows plus 28 x 16 B of weights per output sample from LDS -- 12% of the block.
+    float* E = XS;                                   // [GR rows][8]
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int k = TILE(j), row = k * 32 + n;
       if (k >= 1 && k <= NG - 2) {
+        float st[7];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          *reinterpret_cast<float4*>(&XS[row * LB_XLD + 8 * i + 4 * h]) =
-              make_float4(xr[j][2 * i].x, xr[j][2 * i].y, xr[j][2 * i + 1].x, xr[j][2 * i + 1].y);
+        for (int tap = 0; tap < 7; ++tap) {
+          f32x2 acc = {0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {             // channels 8i + 4h .. +3 = regs 4i .. 4i+3
+            const float4 w = *reinterpret_cast<const float4*>(&FWF[tap * 32 + 8 * i + 4 * h]);
+            acc = __builtin_elementwise_fma(xr[j][2 * i], f32x2{w.x, w.y}, acc);
+            acc = __builtin_elementwise_fma(xr[j][2 * i + 1], f32x2{w.z, w.w}, acc);
+          }
+          st[tap] = acc.x + acc.y;
+        }
+#pragma unroll
+        for (int tap = 0; tap < 7; ++tap) st[tap] += __shfl_xor(st[tap], 32);
+        if (h == 0) {
+          *reinterpret_cast<float4*>(&E[row * 8]) = make_float4(st[0], st[1], st[2], st[3]);
+          *reinterpret_cast<float4*>(&E[row * 8 + 4]) = make_float4(st[4], st[5], st[6], 0.f);
+        }
       }
     }
     __syncthreads();
-    // two lanes per output sample (16 channels each), combined by one shuffle
+    // one thread per output sample: x_t from the staged audio (AS[i] is time tg - 3 + i,
+    // t = tg + 64 + s), the sampler update (util.py:222-226)
+    constexpr int IS = (TS + G::NT - 1) / G::NT;
 #pragma unroll
-    for (int it = 0; it < IF; ++it) {
-      const int s2 = tid + it * G::NT;                // wave-uniform bound (2 TS, NT: multiples of 64)
-      if (s2 >= 2 * TS) break;
-      const int s = s2 >> 1, c0 = (s2 & 1) * 16, t = t0 + s;
-      float e = 0.f;
+    for (int it = 0; it < IS; ++it) {
+      const int s = tid + it * G::NT, t = t0 + s;
+      if (s < TS && t < Lh) {
+        float e = bfin;
 #pragma unroll
-      for (int tap = 0; tap < 7; ++tap) {
-        const float* xrow = &XS[(64 + s + tap - 3) * LB_XLD + c0];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(xrow + 4 * q);
-          const float4 w = *reinterpret_cast<const float4*>(&FWF[tap * 32 + c0 + 4 * q]);
-          e = fmaf(w.x, v.x, fmaf(w.y, v.y, fmaf(w.z, v.z, fmaf(w.w, v.w, e))));
-        }
-      }
-      e += __shfl_xor(e, 1);
-      if ((s2 & 1) == 0 && t < Lh) {
-        e += bfin;
-        // x_t from the staged audio: AS[i] is time tg - 3 + i, t = tg + 64 + s
+        for (int tap = 0; tap < 7; ++tap) e += E[(64 + s + tap - 3) * 8 + tap];
         float v = (AS[67 + s] - P.ce * e) / P.den;
         if (P.sig != 0.f) v += P.sig * zr[it];
         P.audio_out[base + t] = v;
@@ -2395,131 +2402,141 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 
 // Location-variable kernels of ALL 4 layers of an LVC block, frame-major bf16
 // (modules.py:335-340):  Kf[l][f][n] = b[l][n] + W[l][n] . [h(f-1); h(f); h(f+1)],
-// n < 6144, K = 192.  One GEMM with 4 x 6144 rows (weights = MFMA A operand, staged in
-// LDS 64 rows at a time; the next tile's rows are loaded into registers under the MFMAs)
-// and one column per frame.  Block = 256 frames, 8 waves of 32 frames; a wave keeps the
-// bf16 h fragments of its frames in registers for the whole block (about 120 VGPRs, so
-// two blocks -- 16 waves -- share a CU and hide each other's LDS and store latency).
-// A lane of C holds 4 consecutive kernel values of one frame; a per-wave LDS transpose
-// turns them into full 128-B line stores.
-// Block (x, y) owns frames [256x, 256x + 256) and weight tiles [y T / G, (y+1) T / G).
-constexpr int KP_FR = 256, KP_NT = 64, KP_LDW = 200;   // 400-B LDS rows: conflict-free b128 reads
+// n < 6144, K = 192: one GEMM with N = 4 x 6144 rows (the MFMA A operand), a column per
+// frame, bound by its 340 MB of K stores at C3.  Work item = 512 rows n x 128 frames;
+// a persistent block (8 waves, one per CU) walks a contiguous run of items, n-group-major:
+//  * wave w holds its 64 rows of W (24 fragments, 96 VGPRs) and their biases in registers
+//    for as long as the n-group lasts, so the main loop reads only the frames' h from LDS,
+//    one 16-B fragment per TWO MFMAs;
+//  * the frames' [h(f-1); h(f); h(f+1)] rows (zero across utterance edges) are double-
+//    buffered in LDS: the next item's are loaded at the start of an item and written after
+//    its stores, one barrier per item, no barrier inside it;
+//  * K stores are unconditional buffer stores (rows past the end are dropped by the range
+//    check), so hipcc never drains them before the next LDS write.
+// r02's structure (W tile in LDS, one fragment read per MFMA, two barriers per 64-row tile)
+// ran ~77 us for its GEMM alone and ~86 us for its stores alone (profiles/r03_ab/kp_kernel_ab.txt).
+// A lane of C holds 4 consecutive kernel values of one frame; a per-wave LDS transpose turns
+// them into 128-B row segments (8 frames per 1-KiB store: 6.0 TB/s in tools/store_probe.hip).
+constexpr int KP_F = 128, KP_NG = 512, KP_LDH = 200;   // 400-B LDS rows: conflict-free b128 reads
 constexpr int KP_LDO = 72;                             // output transpose rows: 64 + 8 pad
-constexpr int KP_TILES = NLY * KPERLAYER / KP_NT;      // 384
+constexpr int KP_NGROUPS = NLY * KPERLAYER / KP_NG;    // 48
 constexpr int KP_THREADS = 512;
-__global__ __launch_bounds__(KP_THREADS, 2) void kp_kernel_bf16_kernel(const __bf16* __restrict__ hin,
+#ifndef KP_AUX
+#define KP_AUX 0   // plain K stores: the lines stay on-die for the LVC block that reads them next (r03 A/B: non-temporal (2) made kp ~4% and the next LVC launch ~4% slower)
+#endif
+__global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __bf16* __restrict__ hin,
                                                                        const __bf16* __restrict__ W,
                                                                        const float* __restrict__ bias,
                                                                        __bf16* __restrict__ Kf, int Tc, int rows,
-                                                                       int groups, float sg, float sf) {
-  __shared__ __attribute__((aligned(16))) __bf16 Ws[KP_NT * KP_LDW];
+                                                                       int nfg, float sg, float sf) {
+  __shared__ __attribute__((aligned(16))) __bf16 Hs[2][KP_F * KP_LDH];
   __shared__ __attribute__((aligned(16))) __bf16 Ot[8][32 * KP_LDO];
-  // the block's bias rows (tiles tb .. te - 1), staged once: a global bias load in the
-  // epilogue would wait behind the next tile's weight loads (vmcnt retires in order)
-  __shared__ __attribute__((aligned(16))) float Bs[(KP_TILES / 16 + 2) * KP_NT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
-  // XCD-aware order (as in lvc_block_bf16_kernel): each XCD walks a contiguous run of
-  // logical blocks, y-major, so a weight-tile group is read into one XCD's L2, not eight
-  int bx, by;
-  {
-    const int total = gridDim.x * gridDim.y, id = blockIdx.y * gridDim.x + blockIdx.x;
-    const int xcd = id & 7, slot = id >> 3, per = total >> 3, rem = total & 7;
-    const int logical = xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
-    by = logical / gridDim.x;
-    bx = logical - by * gridDim.x;
-  }
-  const int fw = bx * KP_FR + wave * 32;                    // first frame of this wave
-  const int tb = by * KP_TILES / groups, te = (by + 1) * KP_TILES / groups;
-  // W tile = 64 rows x 384 B = 1536 16-B pieces, 3 per thread (named registers: an
-  // indexed array here is demoted to scratch by hipcc)
-  uint4 s0, s1, s2;
-  int goff[3], loff[3];
+  __shared__ __attribute__((aligned(16))) float Bq[8][64];   // wave-private: its rows' biases
+  const int tid = threadIdx.x, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
+  // wave-uniform, and provably so: the K-store descriptor is built from it (a descriptor hipcc
+  // sees as divergent becomes a waterfall loop around every store)
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int items = KP_NGROUPS * nfg;
+  const int ib = (int)((long long)blockIdx.x * items / gridDim.x);
+  const int ie = (int)((long long)(blockIdx.x + 1) * items / gridDim.x);
+  typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+  // H staging: item frames [fg*128, +128) x 192 = 3072 16-B pieces, 6 per thread.  Piece c:
+  // frame c / 24, 8 values v = (c % 24) * 8 of [tap][ch] (tap = v / 64).
+  uint4 hv[6];
+  unsigned hz = 0;        // bit i: piece i is zero padding (applied at the LDS store, so the
+                          // load's wait is not pulled up to the load)
+  auto h_load = [&](int item) {
+    const int fg = item % nfg;
+    hz = 0;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int c = tid + KP_THREADS * i, row = c / 24, col = (c - row * 24) * 8;
-    goff[i] = row * 192 + col;
-    loff[i] = row * KP_LDW + col;
-  }
-#define KP_LD(t)                                                         \
-  do {                                                                   \
-    const __bf16* src_ = W + (long long)(t) * KP_NT * 192;               \
-    s0 = *reinterpret_cast<const uint4*>(src_ + goff[0]);                \
-    s1 = *reinterpret_cast<const uint4*>(src_ + goff[1]);                \
-    s2 = *reinterpret_cast<const uint4*>(src_ + goff[2]);                \
-  } while (0)
-#define KP_ST()                                                          \
-  do {                                                                   \
-    *reinterpret_cast<uint4*>(&Ws[loff[0]]) = s0;                        \
-    *reinterpret_cast<uint4*>(&Ws[loff[1]]) = s1;                        \
-    *reinterpret_cast<uint4*>(&Ws[loff[2]]) = s2;                        \
-  } while (0)
-  for (int i = tid; i < (te - tb) * KP_NT; i += KP_THREADS) Bs[i] = bias[(long long)tb * KP_NT + i];
-  KP_LD(tb);
-  // B fragments: k = tap*64 + ch (tap-major), lane half h holds 8 consecutive channels
-  bf16x8 af[12];
-  {
-    const int R = fw + r32;
-    const bool ok = R < rows;
-    const int b = ok ? R / Tc : 0, f = R - b * Tc;
-#pragma unroll
-    for (int kk = 0; kk < 12; ++kk) {
-      const int tap = kk >> 2, kc = kk & 3, ff = f + tap - 1;
-      bf16x8 v = {};
-      if (ok && ff >= 0 && ff < Tc) v = *reinterpret_cast<const bf16x8*>(hin + ((long long)b * Tc + ff) * HK + kc * 16 + h * 8);
-      af[kk] = v;
+    for (int i = 0; i < 6; ++i) {
+      const int c = tid + KP_THREADS * i, fl = c / 24, v = (c - fl * 24) * 8, tap = v >> 6, ch = v & 63;
+      const int R = fg * KP_F + fl, Rc = R < rows ? R : rows - 1;
+      const int b = Rc / Tc, f = Rc - b * Tc, ff = f + tap - 1;
+      const int ffc = ff < 0 ? 0 : ff >= Tc ? Tc - 1 : ff;     // clamped: unconditional load
+      hv[i] = *reinterpret_cast<const uint4*>(hin + ((long long)b * Tc + ffc) * HK + ch);
+      hz |= (R >= rows || ff < 0 || ff >= Tc) ? 1u << i : 0u;
     }
-  }
-  KP_ST();
+  };
+  auto h_store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int c = tid + KP_THREADS * i, fl = c / 24, v = (c - fl * 24) * 8;
+      // masked with AND: a uint4 ternary here made hipcc select through a scratch array
+      const unsigned m = (hz >> i) & 1 ? 0u : ~0u;
+      *reinterpret_cast<uint4*>(&Hs[buf][fl * KP_LDH + v]) = make_uint4(hv[i].x & m, hv[i].y & m, hv[i].z & m, hv[i].w & m);
+    }
+  };
+  bf16x8 wa[24];          // A fragments: (j, kk) = rows nb + 32 j + r32, k = 16 kk + 8 h
+  float* bw = Bq[wave];
+  int ng_cur = -1;
+  auto w_load = [&](int ng) {
+    const int nb = ng * KP_NG + wave * 64;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk)
+        wa[j * 12 + kk] = *reinterpret_cast<const bf16x8*>(W + (long long)(nb + 32 * j + r32) * 192 + kk * 16 + h * 8);
+    bw[lane] = bias[nb + lane];   // wave-private: no block barrier (read after this wave's lgkmcnt wait)
+  };
+  h_load(ib);
+  h_store(0);
   __syncthreads();
   __bf16* ot = Ot[wave];
-  for (int t = tb; t < te; ++t) {
-    if (t + 1 < te) KP_LD(t + 1);
-    f32x16 acc[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < 12; ++kk) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&Ws[(j * 32 + r32) * KP_LDW + kk * 16 + h * 8]);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, af[kk], acc[j], 0, 0, 0);
-      }
+  for (int item = ib; item < ie; ++item) {
+    const int buf = (item - ib) & 1, ng = item / nfg, fg = item - ng * nfg;
+    if (ng != ng_cur) {   // wave-uniform; once or twice per block
+      w_load(ng);
+      ng_cur = ng;
     }
-    // C[n][frame]: lane owns frame r32, rows n = 32j + 8g + 4h + (0..3)
-    const int layer = t / (KPERLAYER / KP_NT), n0 = (t - layer * (KPERLAYER / KP_NT)) * KP_NT;
-    __bf16* kout = Kf + (long long)layer * rows * KPERLAYER + n0;
-    const float sc = n0 < KPERLAYER / 2 ? sg : sf;            // gate rows (k-steps 0..5) / filter rows
+    h_load(min(item + 1, ie - 1));   // the next item's frames, under this item's work
+    const int nb = ng * KP_NG + wave * 64, layer = nb / KPERLAYER, n0 = nb - layer * KPERLAYER;
+    const float sc = n0 < KPERLAYER / 2 ? sg : sf;           // gate rows / filter rows
+    const __amdgpu_buffer_rsrc_t kout =
+        __builtin_amdgcn_make_buffer_rsrc(Kf + (long long)layer * rows * KPERLAYER, 0, rows * KPERLAYER * 2, 0x00020000);
+    const __bf16* hs = Hs[buf];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int ft = 0; ft < KP_F / 32; ++ft) {   // unrolled: hipcc counts the stores in vmcnt
+      f32x16 acc[2];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int nl = j * 32 + 8 * g + 4 * h;
-        const float4 bn = *reinterpret_cast<const float4*>(&Bs[(t - tb) * KP_NT + nl]);
-        *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + nl]) =
-            bf16x4{(__bf16)((acc[j][4 * g] + bn.x) * sc), (__bf16)((acc[j][4 * g + 1] + bn.y) * sc),
-                   (__bf16)((acc[j][4 * g + 2] + bn.z) * sc), (__bf16)((acc[j][4 * g + 3] + bn.w) * sc)};
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) {
+        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hs[(ft * 32 + r32) * KP_LDH + kk * 16 + h * 8]);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[kk], hb, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[12 + kk], hb, acc[1], 0, 0, 0);
       }
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
-    __builtin_amdgcn_wave_barrier();
+      // C[n][frame]: lane owns frame r32, rows n = 32j + 8g + 4h + (0..3)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
-      const int Rf = fw + fl;
-      const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
-      // streaming (non-temporal) store: 340 MB per launch, read back by the next launch from HBM
-      typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
-      if (Rf < rows)
-        __builtin_nontemporal_store(u32x4_{v.x, v.y, v.z, v.w},
-                                    reinterpret_cast<u32x4_*>(kout + (long long)Rf * KPERLAYER + ch));
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bn = *reinterpret_cast<const float4*>(&bw[j * 32 + 8 * g + 4 * h]);
+          *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + j * 32 + 8 * g + 4 * h]) =
+              bf16x4{(__bf16)((acc[j][4 * g] + bn.x) * sc), (__bf16)((acc[j][4 * g + 1] + bn.y) * sc),
+                     (__bf16)((acc[j][4 * g + 2] + bn.z) * sc), (__bf16)((acc[j][4 * g + 3] + bn.w) * sc)};
+        }
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
+      __builtin_amdgcn_wave_barrier();
+      const int f0 = fg * KP_F + ft * 32;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
+        // 340 MB per launch, read back by the next launch
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_{v.x, v.y, v.z, v.w}, kout,
+                                               ((f0 + fl) * KPERLAYER + n0 + ch) * 2, 0, KP_AUX);
+      }
+      __builtin_amdgcn_wave_barrier();      // the next frame tile rewrites ot
     }
-    __syncthreads();                      // every wave is past its Ws reads (and Ot reads)
-    if (t + 1 < te) KP_ST();
+    // the next item's frames into the other buffer, whose readers (the previous item) are
+    // past the last barrier; the barrier makes them visible
+    __builtin_amdgcn_sched_barrier(0);
+    h_store(buf ^ 1);
     __syncthreads();
   }
-#undef KP_LD
-#undef KP_ST
 }
 
 // prescale: the gate half scaled by -log2(e), the filter half by 2 log2(e) (the whole-block
@@ -2527,12 +2544,14 @@ __global__ __launch_bounds__(KP_THREADS, 2) void kp_kernel_bf16_kernel(const __b
 int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B, int Tc, hipStream_t st,
                    bool prescale = false) {
   const int rows = B * Tc;
-  const int fblocks = cdiv(rows, KP_FR);
-  int groups = 512 / fblocks;                 // 2 blocks per CU x 256 CUs, one wave of blocks (r02: 256 / 1024 slower)
-  groups = groups < 16 ? 16 : groups > KP_TILES ? KP_TILES : groups;   // >= 16: Bs holds a block's tiles
+  const int nfg = cdiv(rows, KP_F);
+  // buffer-store offsets are 32-bit bytes, up to the last (partial) item's rows
+  PD_CHECK_ARG((long long)nfg * KP_F * KPERLAYER * 2 < (1ll << 31), "kernel predictor: B*T' too large");
+  const int items = KP_NGROUPS * nfg;
+  const int grid = items < 256 ? items : 256;   // persistent: one block per CU
   ProfScope ps("fd_kp_kernel", st);
-  hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(fblocks, groups), dim3(KP_THREADS), 0, st, hk, lookup_bf16(K.kk_w),
-                     K.kk_b, Kb, Tc, rows, groups, prescale ? -LOG2E : 1.f, prescale ? 2.f * LOG2E : 1.f);
+  hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(grid), dim3(KP_THREADS), 0, st, hk, lookup_bf16(K.kk_w), K.kk_b, Kb,
+                     Tc, rows, nfg, prescale ? -LOG2E : 1.f, prescale ? 2.f * LOG2E : 1.f);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }

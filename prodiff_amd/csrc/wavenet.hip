@@ -72,7 +72,21 @@ struct WnLayerArgs {
   const __bf16* W2f;      // [2C/32][C/16][64][8]
   const float* b2;        // [2C]
   int B, T, H, dil, first;
+#ifdef WN_TRACE
+  unsigned long long* trace;   // tools/wn_probe.hip: per-phase s_memtime stamps
+#endif
 };
+#ifdef WN_TRACE
+#define WN_STAMP(i)                                                                          \
+  do {                                                                                       \
+    if (lane == 0 && blockIdx.x % 7 == 0)                                                    \
+      P.trace[((blockIdx.x / 7) * 8 + wave) * 8 + (i)] = __builtin_readcyclecounter();      \
+  } while (0)
+#else
+#define WN_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 // RT row tiles (32 frames each) per block: every weight fragment streamed from L2 feeds RT
 // MFMAs, so RT = 2 halves the L2 -> CU weight bytes per frame (the port, about 64 B/clk/CU,
@@ -89,6 +103,7 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
   __bf16* Gs = reinterpret_cast<__bf16*>(smem + (RT == 1 ? AS_BYTES : 0));   // RT = 2: aliases As
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int H = K1 - 3 * C, rows = P.B * P.T, R0 = blockIdx.x * 32 * RT;
+  WN_STAMP(0);
   // GEMM1: gate tile nt = wave, filter tile nt = 8 + wave.  Weight fragments stream from
   // L2 through a register ring WD k-steps deep (the loop is fully unrolled, so every
   // wait is a partial vmcnt): the L2 latency hides behind WD steps of MFMAs.  The ring
@@ -100,9 +115,6 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)wave * KS2 * 64 + lane;
   const bf16x8* wsk = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)(8 + wave) * KS2 * 64 + lane;
   bf16x8 rg[WD], rf[WD];
-  constexpr int WD0 = 6;   // primed before the staging (the rest after it: register budget)
-#pragma unroll
-  for (int i = 0; i < WD0; ++i) { rg[i] = wg[i * 64]; rf[i] = wf[i * 64]; }
   // stage [x(t-d)+dp; x(t)+dp; x(t+d)+dp; cond] as bf16 (zero outside each row's utterance).
   // Thread tid always owns column group g = 4 (tid % 256) (so its tap/channel is fixed)
   // and rows tid/256 + 2 it; all 16 loads of a 32-row half are issued before any is used
@@ -112,34 +124,64 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
   const int g = (tid & (NGR - 1)) * 4, r0 = tid / NGR;
   const bool isx = g < 3 * C;
   const int tap = g / C, c = isx ? g - tap * C : g - 3 * C, sh = (tap - 1) * P.dil;
+  // dp (the step's diffusion projection) depends on the utterance only: when T >= the
+  // block's rows the block spans at most two utterances, so two float4 cover every item
+  // (per-item loads otherwise)
+  const bool two_b = P.T >= 32 * RT;
+  const int bA = min(R0, rows - 1) / P.T, bB = min(R0 + 32 * RT - 1, rows - 1) / P.T;
+  float4 dA = make_float4(0.f, 0.f, 0.f, 0.f), dB = dA;
+  if (isx) {
+    dA = *reinterpret_cast<const float4*>(P.dp + (long long)bA * P.dp_ld + c);
+    dB = *reinterpret_cast<const float4*>(P.dp + (long long)bB * P.dp_ld + c);
+  }
 #pragma unroll
   for (int half = 0; half < RT; ++half) {
-    float4 sv[IT], dv[IT];
+    float4 sv[IT];
     float ok[IT];
+    int bi[IT];
+    // (utterance, time) of the rows without a division per item: the block's first row is
+    // split once (uniform), later rows step forward (r03: 16 integer divisions per thread
+    // were a large share of the staging's VALU work)
+    int bq = min(R0 + 32 * half + r0, rows - 1) / P.T;
+    int tq = min(R0 + 32 * half + r0, rows - 1) - bq * P.T;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int R = R0 + 32 * half + r0 + 2 * it;
-      const int Rc = R < rows ? R : rows - 1;
-      const int b = Rc / P.T, t = Rc - b * P.T, tt = isx ? t + sh : t;
+      if (it > 0 && R < rows) {
+        tq += 2;
+        while (tq >= P.T) { tq -= P.T; ++bq; }
+      }
+      const int b = bq, t = tq, tt = isx ? t + sh : t;
       const bool v = R < rows && tt >= 0 && tt < P.T;
       const int ttc = tt < 0 ? 0 : tt >= P.T ? P.T - 1 : tt;
       ok[it] = v ? 1.f : 0.f;
+      bi[it] = b;
       const float* src = isx ? P.xin + ((long long)b * P.T + ttc) * C + c : P.cond + ((long long)b * P.T + ttc) * H + c;
       sv[it] = *reinterpret_cast<const float4*>(src);
-      dv[it] = isx ? *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // the weight ring is primed right behind the first staging loads: they return first
+    // (in-order vmcnt), and the ring's L2 reads overlap their HBM round trip
+    // (tools/wn_probe.hip: staging was a quarter of the wave's life with the ring first)
+    if (half == 0) {
+#pragma unroll
+      for (int i = 0; i < WD; ++i) { rg[i] = wg[i * 64]; rf[i] = wf[i * 64]; }
     }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const float m = ok[it];
-      const float4 v = sv[it], d = dv[it];
+      const float4 v = sv[it];
+      // selected per component: a float4 ternary made hipcc pick through a scratch array
+      float4 d = dA;
+      if (bi[it] != bA) { d.x = dB.x; d.y = dB.y; d.z = dB.z; d.w = dB.w; }
+      if (isx && !two_b) d = *reinterpret_cast<const float4*>(P.dp + (long long)bi[it] * P.dp_ld + c);
       *reinterpret_cast<bf16x4*>(&As[(32 * half + r0 + 2 * it) * LDA + g]) =
           bf16x4{(__bf16)((v.x + d.x) * m), (__bf16)((v.y + d.y) * m), (__bf16)((v.z + d.z) * m),
                  (__bf16)((v.w + d.w) * m)};
     }
   }
-#pragma unroll
-  for (int i = WD0; i < WD; ++i) { rg[i] = wg[i * 64]; rf[i] = wf[i * 64]; }
+  WN_STAMP(1);
   __syncthreads();
+  WN_STAMP(2);
   f32x16 ag[RT], af[RT];
 #pragma unroll
   for (int q = 0; q < RT; ++q)
@@ -166,6 +208,7 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
       af[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], bft, af[q], 0, 0, 0);
     }
   }
+  WN_STAMP(3);
   if (RT > 1) __syncthreads();          // Gs aliases As: every wave is past its GEMM1 reads
   {
     const int n = wave * 32 + r32;
@@ -178,7 +221,9 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
         Gs[r * LDG + n] = (__bf16)gate_fast(ag[q][reg] + bgv, af[q][reg] + bfv);
       }
   }
+  WN_STAMP(4);
   __syncthreads();
+  WN_STAMP(5);
 
   // GEMM2: residual tile nt = wave, skip tile nt = 8 + wave.  The epilogue's x / skip
   // reads of the first row tile are issued first so they land under the MFMAs.
@@ -213,6 +258,7 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
       as_[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b1, as_[q], 0, 0, 0);
     }
   }
+  WN_STAMP(6);
   const float brv = P.b2[n], bsv = P.b2[C + n];
   const float rs2 = 0.70710678118654752440f;
 #pragma unroll
@@ -228,6 +274,7 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
         P.skip[o] = sv + as_[q][reg] + bsv;
       }
     }
+  WN_STAMP(7);
 }
 
 // ------------------------------------------------------------------ two-kernel residual layer (bf16)
