@@ -2068,7 +2068,13 @@ int lvc_stream_seg(int Lh, int B) {
 //   out = conv_d4(h2) + W_r xs + (b3 + b_r)        (conv.2 and residual_dense share one K=128 GEMM)
 // Block = 128 output rows of one utterance; local row p <-> i = i0 - 7 + p (halo 1+2+4).
 // Every intermediate is zeroed outside [0, Lout): each reference conv's zero padding.
+// AF: bound on the factor f of an audio-input block (the audio window is (DB_TS + 14) f
+// samples); the first DBlock has f = 4 in every shipped config.
+// r03 (SQ counters, C3): the audio block was issue-bound -- 1.1k VALU + 0.6k SALU instructions
+// per wave at 3 waves per SIMD -- so the first conv keeps its weights in registers and the
+// conv epilogues apply the utterance-edge mask only on edge tiles.
 constexpr int DB_TS = 128, DB_ROWS = 168, DB_LD = 40;
+template <int AF>
 __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                           const __bf16* __restrict__ W0, const float* __restrict__ b0,
                                                           const __bf16* __restrict__ W1, const float* __restrict__ b1,
@@ -2082,10 +2088,9 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   __shared__ __attribute__((aligned(16))) __bf16 H1[DB_ROWS * DB_LD];
   __bf16* H2 = U0;
   // audio input (the first DBlock): the block's samples t = f i + k - 3 of its rows, staged once
-  constexpr int DB_AUM = (DB_TS + 14) * 16 + 8;      // f <= 16 (fd_create's ratio bound)
+  constexpr int DB_AUM = (DB_TS + 14) * AF + 8;
   constexpr int DB_AUI = (DB_AUM + 255) / 256;
   __shared__ float AU[DB_AUM];
-  __shared__ float FWS[8 * 32];                       // first conv [tap][c] (+ bias row 7)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, i0 = blockIdx.x * DB_TS, ib = i0 - 7;
   const long long Lin = (long long)Lout * f;
@@ -2115,21 +2120,30 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
       const long long t = t0 + tid + 256 * it;
       av[it] = au[t < 0 ? 0 : t >= Lin ? Lin - 1 : t];
     }
-    const float fwv = tid < 224 ? fw[tid] : 0.f, fbv = tid < 32 ? fb[tid] : 0.f;
 #pragma unroll
     for (int it = 0; it < DB_AUI; ++it) {
       const int i = tid + 256 * it;
       const long long t = t0 + i;
       if (i < na) AU[i] = (t >= 0 && t < Lin) ? av[it] : 0.f;
     }
-    if (tid < 224) FWS[(tid % 7) * 32 + tid / 7] = fwv;   // fw is [c][tap]
-    if (tid < 32) FWS[224 + tid] = fbv;
     __syncthreads();
   }
   // staging: every thread's (<= DB_NI) items are loaded before any is converted, so their
   // strided HBM reads are in flight together (one round trip per block, not one per item)
   constexpr int DB_NI = (DB_ROWS * 8 + 255) / 256;
   float4 sv[DB_NI];
+  // a thread's channel quad q is the same for all its items: its first-conv weights (7 taps x
+  // 4 channels, fw is [c][tap]) and biases live in registers
+  float fq[7][4], fbq[4];
+  if (audio) {
+    const int q = (tid & 7) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      fbq[e] = fb[q + e];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) fq[k][e] = fw[(q + e) * 7 + k];
+    }
+  }
 #pragma unroll
   for (int u = 0; u < DB_NI; ++u) {
     const int i = tid + 256 * u;
@@ -2139,12 +2153,12 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
       if (audio) {
         float o[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = FWS[224 + q + e];
+        for (int e = 0; e < 4; ++e) o[e] = fbq[e];
 #pragma unroll
         for (int k = 0; k < 7; ++k) {                // first_conv_kernel's order
           const float a = AU[p * f + k];             // t = f ii + k - 3
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = fmaf(FWS[k * 32 + q + e], a, o[e]);
+          for (int e = 0; e < 4; ++e) o[e] = fmaf(fq[k][e], a, o[e]);
         }
         v = make_float4(o[0], o[1], o[2], o[3]);
       } else {
@@ -2177,13 +2191,20 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(&In[(first + mt * 32 + r32 + (tap - 1) * dil) * DB_LD + ci0 + h * 8]);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wf[kk], acc, 0, 0, 0);
       }
+      // rows outside [0, Lout) (and past DB_ROWS) are zeroed: tile-uniform test first
+      const int pt = first + mt * 32, it0 = ib + pt;
+      const bool edge = it0 < 0 || it0 + 31 >= Lout || pt + 31 >= DB_ROWS;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const int p = first + mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, ii = ib + p;
+        const int p = pt + (reg & 3) + 8 * (reg >> 2) + 4 * h, ii = ib + p;
         float v = acc[reg] + bv;
         v = v >= 0.f ? v : 0.2f * v;                        // the next conv's input activation
-        if (ii < 0 || ii >= Lout || p >= DB_ROWS) v = 0.f;
-        if (p < DB_ROWS) Out[p * DB_LD + r32] = (__bf16)v;
+        if (edge) {
+          if (ii < 0 || ii >= Lout || p >= DB_ROWS) v = 0.f;
+          if (p < DB_ROWS) Out[p * DB_LD + r32] = (__bf16)v;
+        } else {
+          Out[p * DB_LD + r32] = (__bf16)v;
+        }
       }
     }
   };
@@ -2716,9 +2737,14 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
   const long long bsi = (long long)Tout * f * CI, bso = (long long)Tout * CI;
   if (const __bf16* w0 = lookup_bf16(D.c0_w)) {   // bf16: one fused launch, intermediates in LDS
     ProfScope ps("fd_dblock_fused", st);
-    hipLaunchKernelGGL(dblock_bf16_kernel, dim3(cdiv(Tout, DB_TS), B), dim3(256), 0, st, in, out, w0, D.c0_b,
-                       lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, audio,
-                       audio ? m->first_w : nullptr, audio ? m->first_b : nullptr);
+    if (audio && f <= 4)
+      hipLaunchKernelGGL(dblock_bf16_kernel<4>, dim3(cdiv(Tout, DB_TS), B), dim3(256), 0, st, in, out, w0, D.c0_b,
+                         lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, audio, m->first_w,
+                         m->first_b);
+    else
+      hipLaunchKernelGGL(dblock_bf16_kernel<16>, dim3(cdiv(Tout, DB_TS), B), dim3(256), 0, st, in, out, w0, D.c0_b,
+                         lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, audio,
+                         audio ? m->first_w : nullptr, audio ? m->first_b : nullptr);
     PD_LAUNCH_CHECK();
     return PD_OK;
   }
