@@ -232,6 +232,17 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
               const float* noise, unsigned long long seed, const int* utt_ids, float* wav, int B,
               int Tc, void* workspace, size_t ws_bytes, void* stream);
 
+/* The same reverse process with the per-pass update given directly: pass j (j < N, sampling
+ * order) evaluates eps at step value steps[j] and sets x = (x - ce[j] eps) / den[j] + sg[j] z.
+ * fd_sample is this with DDPM coefficients (util.py:222-226); DDIM (util.py:215-220,
+ * ddim=True) is ce = -(c2 + c3) / c1, den = 1 / c1, sg = 0.  `draw0` offsets the passes'
+ * Philox stream ids (a sampler run pass by pass, return_sequence=True, keeps the fused
+ * run's draws); the x_T draw is taken only when x_T is NULL. */
+int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce, const float* den,
+                    const float* sg, const float* steps, int N, const float* x_T,
+                    const float* noise, unsigned long long seed, const int* utt_ids, int draw0,
+                    float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream);
+
 
 /* ==================================================================== NSF-HiFiGAN
  * SVS vocoder -- replaces modules/nsf_hifigan/models.py:222-283

@@ -92,6 +92,9 @@ _SIGS = {
     "fd_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                             C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, _VP, C.c_int,
                             C.c_int, _VP, C.c_size_t, _VP]),
+    "fd_sample_coefs": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                  C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, C.c_int, _VP,
+                                  C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "pd_cond_num_params": (C.c_int, [C.POINTER(pd_cond_dims)]),
     "pd_cond_create": (C.c_int, [C.POINTER(pd_cond_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
     "pd_cond_destroy": (None, [_VP]),

@@ -3310,11 +3310,12 @@ int fd_forward(const fd_model* m, const float* audio, const float* cond, const f
   return PD_OK;
 }
 
-int fd_sample(const fd_model* m, const float* mel, const float* beta, const float* alpha, const float* sigma,
-              const float* steps, int N, const float* x_T, const float* noise, unsigned long long seed,
-              const int* utt_ids, float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream) {
-  PD_CHECK_ARG(m && mel && beta && alpha && sigma && steps && wav && workspace, "null pointer");
-  PD_CHECK_ARG(B > 0 && Tc > 0 && N >= 1, "bad B/T'/N");
+int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce_, const float* den_, const float* sg_,
+                    const float* steps_, int N, const float* x_T, const float* noise, unsigned long long seed,
+                    const int* utt_ids, int draw0, float* wav, int B, int Tc, void* workspace, size_t ws_bytes,
+                    void* stream) {
+  PD_CHECK_ARG(m && mel && ce_ && den_ && sg_ && steps_ && wav && workspace, "null pointer");
+  PD_CHECK_ARG(B > 0 && Tc > 0 && N >= 1 && draw0 >= 0, "bad B/T'/N/draw0");
   // Long schedules (the 200- and 1000-step ones, fastdiff.py:58-61) run in chunks of
   // FD_STEP_CHUNK steps: each chunk's step embeddings and kernel-predictor hidden stacks
   // are computed in one batched launch, so the workspace is bounded by the chunk.
@@ -3350,9 +3351,9 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
   const int nb = m->nblocks, rows = B * Tc;
   for (int j0 = 0; j0 < N; j0 += CH) {
     const int nc = N - j0 < CH ? N - j0 : CH;
-    // the chunk's step embeddings at once: pass j uses n = N-1-j
+    // the chunk's step embeddings at once
     std::vector<float> sv(nc);
-    for (int j = 0; j < nc; ++j) sv[j] = steps[N - 1 - (j0 + j)];
+    for (int j = 0; j < nc; ++j) sv[j] = steps_[j0 + j];
     PD_TRY(fill_steps(ws + W.steps, sv.data(), nc, B, st));
     PD_TRY(fd_step_mlp(m, ws, W, nc * B, st));
     if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, mel, ws + W.nz, nc, B, Tc, st));
@@ -3361,7 +3362,7 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
       PD_HIP(hipStreamWaitEvent(m->side, m->ev_hidden, 0));
     }
     for (int jl = 0; jl < nc; ++jl) {
-      const int j = j0 + jl, n = N - 1 - j;
+      const int j = j0 + jl;
       if (side) {
         // step j's kernels for every block; slot b is rewritten once step j-1's block b has run
         for (int b = 0; b < nb; ++b) {
@@ -3373,12 +3374,10 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
         }
       }
       float* x = nullptr;
-      // x = (x - beta/sqrt(1-alpha^2) eps) / sqrt(1-beta) + [n>0] sigma z   (util.py:222-226)
-      const float ce = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
-      const float den = sqrtf(1.f - beta[n]);
-      const float sg = n > 0 ? sigma[n] : 0.f;
+      // x = (x - ce eps) / den + sg z  (pass j's coefficients, fd_sample / util.py:222-231)
+      const float ce = ce_[j], den = den_[j], sg = sg_[j];
       const FdFinal fin{other, noise ? noise + (size_t)j * B * L : (const float*)nullptr, ce, den, sg, seed,
-                        0x10000u + j, utt_ids};
+                        0x10000u + draw0 + j, utt_ids};
       PD_TRY(fd_net(m, ws, W, cur, mel, ws + W.nz + (size_t)jl * B * nb * CC, jl, B, Tc, &x, st,
                     fused ? &fin : nullptr, side));
       if (x == nullptr) {   // updated inside the last LVC block
@@ -3388,13 +3387,32 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
       {
         ProfScope ps("fd_final_update", st);
         hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w,
-                           m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + j, utt_ids, L);
+                           m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + draw0 + j, utt_ids, L);
       }
       PD_LAUNCH_CHECK();
     }
   }
   if (cur != wav) PD_HIP(hipMemcpyAsync(wav, cur, sizeof(float) * B * L, hipMemcpyDeviceToDevice, st));
   return PD_OK;
+}
+
+int fd_sample(const fd_model* m, const float* mel, const float* beta, const float* alpha, const float* sigma,
+              const float* steps, int N, const float* x_T, const float* noise, unsigned long long seed,
+              const int* utt_ids, float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream) {
+  PD_CHECK_ARG(m && mel && beta && alpha && sigma && steps && wav && workspace, "null pointer");
+  PD_CHECK_ARG(N >= 1, "bad N");
+  // pass j runs schedule index n = N-1-j:
+  //   x = (x - beta/sqrt(1-alpha^2) eps) / sqrt(1-beta) + [n>0] sigma z   (util.py:222-226)
+  std::vector<float> ce(N), den(N), sg(N), st(N);
+  for (int j = 0; j < N; ++j) {
+    const int n = N - 1 - j;
+    ce[j] = beta[n] / sqrtf(1.f - alpha[n] * alpha[n]);
+    den[j] = sqrtf(1.f - beta[n]);
+    sg[j] = n > 0 ? sigma[n] : 0.f;
+    st[j] = steps[n];
+  }
+  return fd_sample_coefs(m, mel, ce.data(), den.data(), sg.data(), st.data(), N, x_T, noise, seed, utt_ids, 0, wav,
+                         B, Tc, workspace, ws_bytes, stream);
 }
 
 }  // extern "C"

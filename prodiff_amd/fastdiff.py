@@ -261,6 +261,29 @@ class FastDiff(nn.Module):
         return eps
 
     @torch.no_grad()
+    def sample_coefs(self, mel, ce, den, sg, steps, x_T=None, noise=None, seed=None, utt_ids=None, draw0=0):
+        """The reverse loop with explicit per-pass coefficients (fd_sample_coefs): pass j
+        evaluates eps at steps[j] and sets x = (x - ce[j] eps) / den[j] + sg[j] z."""
+        h = self.handle()
+        B, Tc, _ = mel.shape
+        N = len(steps)
+        L = Tc * self.hop_length
+        dev = mel.device
+        mel = mel.float().contiguous()
+        xT = None if x_T is None else x_T.float().reshape(B, L).contiguous()
+        nz = None if noise is None else noise.float().reshape(-1, B, L).contiguous()
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        wav = torch.empty(B, 1, L, device=dev, dtype=torch.float32)
+        uid = _lib.utt_ids(utt_ids, B, dev)
+        lib = _lib.lib()
+        ws, wsb = self._ws.get(lib.fd_workspace_size(h, B, Tc, N), dev)
+        _lib.check(lib.fd_sample_coefs(h, _lib.fptr(mel), _lib.farr(ce), _lib.farr(den), _lib.farr(sg),
+                                       _lib.farr(steps), N, _lib.fptr(xT), _lib.fptr(nz), seed, _lib.iptr(uid),
+                                       int(draw0), _lib.fptr(wav), B, Tc, ws, wsb, _lib.stream_ptr(dev)))
+        return wav
+
+    @torch.no_grad()
     def sample(self, mel, beta, alpha, sigma, steps, x_T=None, noise=None, seed=None, utt_ids=None):
         """Fused reverse process.  mel [B,T',80] TIME-major (the ProDiff output);
         beta/alpha/sigma/steps: float32 arrays of the reverse schedule;
@@ -288,12 +311,40 @@ class FastDiff(nn.Module):
         return wav
 
 
+def _pass_coefs(b, a, s, steps, ddim):
+    """Per-pass (ce, den, sg, step) of the reverse loop (util.py:211-226), pass j = schedule
+    index n = N-1-j, in float32 as the reference forms them (torch float tensors):
+    DDPM  x = (x - b/sqrt(1-a^2) eps) / sqrt(1-b) + [n>0] s z
+    DDIM  x = c1 x + (c2 + c3) eps,  a' = a/sqrt(1-b), c1 = a'/a, c2 = -sqrt(1-a^2) c1,
+          c3 = sqrt(1-a'^2), as (x - ce eps) / den with ce = -(c2 + c3)/c1, den = 1/c1."""
+    N = len(steps)
+    f = np.float32
+    ce, den, sg, st = (np.zeros(N, f) for _ in range(4))
+    for j in range(N):
+        n = N - 1 - j
+        bn, an = f(b[n]), f(a[n])
+        st[j] = steps[n]
+        if ddim:
+            anext = f(an / f(np.sqrt(f(1) - bn)))
+            c1 = f(anext / an)
+            c2 = f(-f(np.sqrt(f(1) - f(an * an))) * c1)
+            c3 = f(np.sqrt(f(1) - f(anext * anext)))
+            ce[j] = f(-(c2 + c3) / c1)
+            den[j] = f(f(1) / c1)
+        else:
+            ce[j] = f(bn / f(np.sqrt(f(1) - f(an * an))))
+            den[j] = f(np.sqrt(f(1) - bn))
+            sg[j] = f(s[n]) if n > 0 else f(0)
+    return ce, den, sg, st
+
+
 def sampling_given_noise_schedule(net, size, diffusion_hyperparams, inference_noise_schedule, condition=None,
                                   ddim=False, return_sequence=False, x_T=None, noise=None, seed=None):
     """util.py:158-232 on the fused GPU path.  ``condition`` is [B,80,T'] as in the
-    reference; ``diffusion_hyperparams['alpha']`` is the training alpha table."""
-    if ddim or return_sequence:
-        raise NotImplementedError("ddim / return_sequence are not on the inference hot path")
+    reference; ``diffusion_hyperparams['alpha']`` is the training alpha table.
+    ddim=True takes the deterministic update (util.py:215-220); return_sequence=True returns
+    [x_T, x after pass 1, ..., x_0] (util.py:209-210,228-231), running the passes one call
+    each with the fused run's draw keys."""
     if not isinstance(net, FastDiff):
         raise TypeError("net must be a prodiff_amd.FastDiff")
     alpha_train = np.asarray(torch.as_tensor(diffusion_hyperparams["alpha"]).cpu().numpy(), np.float32)
@@ -302,5 +353,24 @@ def sampling_given_noise_schedule(net, size, diffusion_hyperparams, inference_no
     B, _, L = size
     mel = condition.float().transpose(1, 2).contiguous()
     assert L == mel.shape[1] * net.hop_length
-    return net.sample(mel, b[:len(steps)], a[:len(steps)], s[:len(steps)], steps, x_T=x_T, noise=noise,
-                      seed=seed)
+    N = len(steps)
+    if not ddim and not return_sequence:
+        return net.sample(mel, b[:N], a[:N], s[:N], steps, x_T=x_T, noise=noise, seed=seed)
+    ce, den, sg, st = _pass_coefs(b[:N], a[:N], s[:N], steps, ddim)
+    if not return_sequence:
+        return net.sample_coefs(mel, ce, den, sg, st, x_T=x_T, noise=noise, seed=seed)
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    if x_T is None:   # the fused run's x_T draw (Philox stream of fd_sample_coefs with x_T NULL)
+        # ce = 0, den = 1, sg = 0: the pass returns its x_T draw unchanged
+        x = net.sample_coefs(mel, np.zeros(1, np.float32), np.ones(1, np.float32), np.zeros(1, np.float32),
+                             st[:1], seed=seed, x_T=None, noise=None, draw0=0)
+    else:
+        x = x_T.float().reshape(B, 1, L).clone()
+    xs = [x.clone()]
+    nz = None if noise is None else noise.float().reshape(-1, B, 1, L)
+    for j in range(N):
+        x = net.sample_coefs(mel, ce[j:j + 1], den[j:j + 1], sg[j:j + 1], st[j:j + 1], x_T=x,
+                             noise=None if nz is None or sg[j] == 0 else nz[j:j + 1], seed=seed, draw0=j)
+        xs.append(x.clone())
+    return xs

@@ -292,6 +292,43 @@ def gen_fastdiff_samples(cases=None):
              wav=wav)
 
 
+def gen_fastdiff_variants():
+    """sampling_given_noise_schedule with ddim=True (4-step table) and return_sequence=True
+    (3-step table), util.py:209-231."""
+    seed = 31
+    m, _ = build_fastdiff(seed)
+    for name, n_iter, (B, Tc, seed_s), kw in (("fastdiff_sample_ddim_n4", 4, (2, 3, 47), dict(ddim=True)),
+                                              ("fastdiff_sample_seq_n3", 3, (1, 2, 48), dict(return_sequence=True))):
+        L = Tc * 256
+        c = synth.synth_inputs(seed_s + 2, (B, 80, Tc), loc=-5.0, scale=2.0)
+        dh = fd_util.compute_hyperparams_given_schedule(torch.linspace(1e-6, 0.01, 1000))
+        sched = torch.FloatTensor(FASTDIFF_SCHEDULES[n_iter])
+        draws = []
+        cnt = [0]
+
+        def std_normal(size):
+            a = synth.synth_inputs(seed_s * 1000 + cnt[0], tuple(size))
+            cnt[0] += 1
+            draws.append(a.copy())
+            return torch.from_numpy(a)
+
+        orig = fd_util.std_normal
+        fd_util.std_normal = std_normal
+        try:
+            with torch.no_grad():
+                out = fd_util.sampling_given_noise_schedule(m, (B, 1, L), dh, sched, condition=torch.from_numpy(c),
+                                                            **kw)
+        finally:
+            fd_util.std_normal = orig
+        if kw.get("ddim"):
+            assert len(draws) == 1
+            save(name, seed=seed, c=c, x_T=draws[0], wav=out.numpy())
+        else:
+            assert len(draws) == n_iter
+            save(name, seed=seed, c=c, x_T=draws[0], noise=np.stack(draws[1:]),
+                 seq=np.stack([x.numpy() for x in out]))
+
+
 # --------------------------------------------------------------------------
 # Rectified flow (reflow.py:5-144): the teacher's "reflow" sampler and the pitch
 # predictor's PitchRectifiedFlow, every algorithm; x_T = the torch.randn at :88.

@@ -169,6 +169,50 @@ def test_fastdiff_sample_golden(fdnet, n_iter):
     assert_close(wav, d["wav"], rel=1e-5)
 
 
+def _fd_golden_args(d, n_iter):
+    s = G.load("schedules")
+    dh = {"alpha": torch.from_numpy(s["fd_train_alpha"])}
+    sched = torch.from_numpy(s[f"fd_n{n_iter}_beta"])
+    B, _, Tc = d["c"].shape
+    return (B, 1, Tc * 256), dh, sched
+
+
+def test_fastdiff_sample_ddim_golden(fdnet):
+    """ddim=True (util.py:215-220): deterministic update, only x_T is drawn."""
+    m, _ = fdnet
+    d = G.load("fastdiff_sample_ddim_n4")
+    size, dh, sched = _fd_golden_args(d, 4)
+    wav = sampling_given_noise_schedule(m, size, dh, sched, condition=tt(d["c"]), ddim=True,
+                                        x_T=tt(d["x_T"])).cpu().numpy()
+    assert_close(wav, d["wav"], rel=1e-5)
+
+
+def test_fastdiff_sample_return_sequence_golden(fdnet):
+    """return_sequence=True (util.py:209-210,228-231): [x_T, x after each pass]."""
+    m, _ = fdnet
+    d = G.load("fastdiff_sample_seq_n3")
+    size, dh, sched = _fd_golden_args(d, 3)
+    xs = sampling_given_noise_schedule(m, size, dh, sched, condition=tt(d["c"]), return_sequence=True,
+                                       x_T=tt(d["x_T"]), noise=tt(d["noise"]))
+    assert len(xs) == d["seq"].shape[0] == 4
+    for x, ref in zip(xs, d["seq"]):
+        assert_close(x.cpu().numpy(), ref, rel=1e-5)
+
+
+def test_fastdiff_return_sequence_keeps_fused_draws(fdnet):
+    """Pass-by-pass (return_sequence) with on-device draws ends where the fused sampler does."""
+    m, _ = fdnet
+    from prodiff_amd.schedules import fastdiff_reverse_schedule, fastdiff_train_alpha
+    B, Tc = 2, 3
+    c = tt(synth.synth_inputs(12, (B, 80, Tc), loc=-5.0, scale=2.0))
+    dh = {"alpha": torch.from_numpy(fastdiff_train_alpha())}
+    sched = torch.from_numpy(fastdiff_reverse_schedule(4))
+    fused = sampling_given_noise_schedule(m, (B, 1, Tc * 256), dh, sched, condition=c, seed=77)
+    xs = sampling_given_noise_schedule(m, (B, 1, Tc * 256), dh, sched, condition=c, seed=77, return_sequence=True)
+    assert len(xs) == 5
+    assert_close(xs[-1].cpu().numpy(), fused.cpu().numpy(), rel=1e-5)
+
+
 def test_fastdiff_sample_batch_independence(fdnet):
     m, _ = fdnet
     from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
