@@ -317,6 +317,8 @@ typedef struct {
   int num_spk;               /* spk_embed rows                                               */
   int num_langs;             /* lang_embed rows = len(hparams["languages"]) + 1              */
   int use_dur_embed, use_spk_id, use_gender_id, use_lang_id, use_voicing_embed, use_breath_embed;
+  int rel_pos;               /* 1: RelPositionalEncoding (tts_modules.py:299-300,324-325,
+                                espnet_positional_embedding.py:89-115) instead of the sinusoid */
 } pd_cond_dims;
 
 /* Parameter order = the reference state-dict order (buffers and `diffusion.*` skipped), fp32:

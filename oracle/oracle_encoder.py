@@ -45,6 +45,19 @@ def sinusoid_table(n, dim, padding_idx=0):
     return emb
 
 
+def rel_pos_table(T, dim, max_len=5000):
+    """RelPositionalEncoding's table rows [0, T) (espnet_positional_embedding.py:24-45,108-115):
+    reversed positions max(max_len, T) - 1 - t, interleaved sin/cos, float32 as there."""
+    n = max(max_len, T)
+    pos = np.arange(n - 1, -1, -1.0, dtype=np.float32)[:, None]
+    div = np.exp(np.arange(0, dim, 2, dtype=np.float32) * np.float32(-(math.log(10000.0) / dim))).astype(np.float32)
+    a = (pos * div[None, :]).astype(np.float32)
+    pe = np.zeros((n, dim), np.float32)
+    pe[:, 0::2] = np.sin(a)
+    pe[:, 1::2] = np.cos(a)
+    return pe[:T].astype(np.float64)
+
+
 def make_positions(nonpad):
     """utils/tts_utils.py:6-18 on ~padding_mask (padding_idx 0)."""
     m = nonpad.astype(np.int64)
@@ -95,15 +108,18 @@ def ffn(x, w1, b1, w2, b2):
 
 
 def encoder(P, hp, txt_tokens, extra_embed):
-    """FastspeechEncoder.forward (tts_modules.py:310-317)."""
+    """FastspeechEncoder.forward (tts_modules.py:310-330)."""
     H = hp["hidden_size"]
     pad = txt_tokens == 0
     nonpad = (~pad)[..., None].astype(np.float64)
     x = math.sqrt(H) * P["encoder.embed_tokens.weight"][txt_tokens]
     if extra_embed is not None:
         x = x + extra_embed
-    pos = make_positions(~pad)
-    x = x + sinusoid_table(int(pos.max()) + 1, H)[pos]
+    if hp.get("rel_pos"):   # tts_modules.py:324-325: x * sqrt(H) + pe (no padding-aware positions)
+        x = x * math.sqrt(H) + rel_pos_table(txt_tokens.shape[1], H)[None]
+    else:
+        pos = make_positions(~pad)
+        x = x + sinusoid_table(int(pos.max()) + 1, H)[pos]
     x = x * nonpad
     for l in range(hp["enc_layers"]):
         pre = f"encoder.layers.{l}.op."

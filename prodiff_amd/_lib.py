@@ -52,7 +52,7 @@ class pd_cond_dims(C.Structure):
                 ("enc_ffn_kernel_size", C.c_int), ("num_heads", C.c_int), ("num_spk", C.c_int),
                 ("num_langs", C.c_int), ("use_dur_embed", C.c_int), ("use_spk_id", C.c_int),
                 ("use_gender_id", C.c_int), ("use_lang_id", C.c_int), ("use_voicing_embed", C.c_int),
-                ("use_breath_embed", C.c_int)]
+                ("use_breath_embed", C.c_int), ("rel_pos", C.c_int)]
 
 
 class pd_cond_inputs(C.Structure):

@@ -41,12 +41,17 @@ enum EncUse { U_ENC_QKV = 30, U_ENC_OUT = 31, U_ENC_FFN1 = 32, U_ENC_FFN2 = 33 }
 //  * x[t,c] = ((sqrt(H) emb[tok][c] + ((dur dw[c] + db[c]) + lang[l][c])) + pe(pos, c)) * [tok != 0]
 //    with pe(p, c) = sin(p f_c) | cos(p f_{c-H/2}), f_i = exp(-i ln(1e4)/(H/2-1))
 //    (SinusoidalPositionalEmbedding.get_embedding, common_layers.py:111-128, fp32 as there).
+//  * rel_pos: x[t,c] = ((sqrt(H) emb[tok][c] + extra) sqrt(H) + pr(t, c)) * [tok != 0], with
+//    the RelPositionalEncoding table pr(t, 2i) = sin(q g_i), pr(t, 2i+1) = cos(q g_i),
+//    q = max(5000, T) - 1 - t (reversed positions, max_len 5000), g_i = exp(2i (-ln(1e4)/H))
+//    (espnet_positional_embedding.py:24-45,108-115; FFTBlocks masks the padding, tts_modules.py:274).
 constexpr int EMB_TOK = 8;
 
 __global__ __launch_bounds__(256) void enc_embed_kernel(
     const long long* __restrict__ tok, const long long* __restrict__ lang, const long long* __restrict__ mel2ph,
     int Tt, int Tm, int H, const float* __restrict__ emb, int V, float scale, const float* __restrict__ dur_w,
-    const float* __restrict__ dur_b, const float* __restrict__ lang_emb, int NL, float neg_freq, float* __restrict__ x) {
+    const float* __restrict__ dur_b, const float* __restrict__ lang_emb, int NL, float neg_freq, int rel_pos,
+    float neg_rel, float* __restrict__ x) {
   const int b = blockIdx.y, t0 = blockIdx.x * EMB_TOK, tid = threadIdx.x;
   __shared__ int cnt[EMB_TOK];
   __shared__ int npre;
@@ -96,10 +101,17 @@ __global__ __launch_bounds__(256) void enc_embed_kernel(
       float extra = 0.f;
       if (dur_w) extra = d * dur_w[c] + dur_b[c];
       if (lr) extra = extra + lr[c];
-      const int i = c < half ? c : c - half;
-      const float arg = p * expf((float)i * neg_freq);
-      const float pe = pos[j] == 0 ? 0.f : (c < half ? sinf(arg) : cosf(arg));
-      const float v = (scale * er[c] + extra) + pe;
+      float v;
+      if (rel_pos) {
+        const float q = (float)((Tt > 5000 ? Tt : 5000) - 1 - t);
+        const float arg = q * expf((float)(c & ~1) * neg_rel);
+        v = (scale * er[c] + extra) * scale + ((c & 1) ? cosf(arg) : sinf(arg));
+      } else {
+        const int i = c < half ? c : c - half;
+        const float arg = p * expf((float)i * neg_freq);
+        const float pe = pos[j] == 0 ? 0.f : (c < half ? sinf(arg) : cosf(arg));
+        v = (scale * er[c] + extra) + pe;
+      }
       xr[c] = np ? v : 0.f;
     }
   }
@@ -542,11 +554,13 @@ int pd_cond_forward(const pd_cond* h, const pd_cond_inputs* in, float* cond, flo
   float* enc = enc_out ? enc_out : ws + w.enc;
   float* part = ws + w.part;
   const float neg_freq = (float)(-(std::log(10000.0) / (H / 2 - 1)));
+  const float neg_rel = (float)(-(std::log(10000.0) / H));
   {
     ProfScope ps("enc_embed", st);
     hipLaunchKernelGGL(enc_embed_kernel, dim3(cdiv(T_txt, EMB_TOK), B), dim3(256), 0, st, in->txt_tokens,
                        d.use_lang_id ? in->lang_seq : nullptr, in->mel2ph, T_txt, T_mel, H, h->emb, d.vocab_size,
-                       (float)std::sqrt((double)H), h->dur_w, h->dur_b, h->lang, d.num_langs, neg_freq, x);
+                       (float)std::sqrt((double)H), h->dur_w, h->dur_b, h->lang, d.num_langs, neg_freq, d.rel_pos,
+                       neg_rel, x);
   }
   PD_LAUNCH_CHECK();
   const float eps = 1e-5f;

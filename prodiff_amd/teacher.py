@@ -75,13 +75,22 @@ class SinusoidalPositionalEmbedding(nn.Module):
         self.register_buffer("_float_tensor", torch.FloatTensor(1))
 
 
+class RelPositionalEncoding(nn.Module):
+    """espnet_positional_embedding.py:89-115: no parameters or buffers (its table is a plain
+    attribute there); the encoder kernel computes the table (pd_cond_dims.rel_pos)."""
+
+    def __init__(self, d_model, dropout_rate=0.0, max_len=5000):
+        super().__init__()
+        self.d_model, self.max_len = d_model, max_len
+
+
 class FastspeechEncoder(nn.Module):
-    """tts_modules.py:291-308 (use_pos_embed False, use_last_norm, rel_pos False)."""
+    """tts_modules.py:291-330 (use_pos_embed False, use_last_norm; rel_pos selects the
+    RelPositionalEncoding embedding)."""
 
     def __init__(self, vocab_size, hidden_size, num_layers, kernel_size, dropout=0.1, num_heads=2, rel_pos=False):
         super().__init__()
-        if rel_pos:
-            raise NotImplementedError("rel_pos=True (RelPositionalEncoding) is not supported")
+        self.rel_pos = bool(rel_pos)
         self.hidden_size, self.num_layers, self.kernel_size, self.num_heads = hidden_size, num_layers, kernel_size, num_heads
         self.layers = nn.ModuleList([TransformerEncoderLayer(hidden_size, kernel_size, num_heads)
                                      for _ in range(num_layers)])
@@ -89,7 +98,8 @@ class FastspeechEncoder(nn.Module):
         self.embed_tokens = nn.Embedding(vocab_size, hidden_size, padding_idx=0)
         self.embed_scale = math.sqrt(hidden_size)
         self.padding_idx = 0
-        self.embed_positions = SinusoidalPositionalEmbedding(hidden_size, 0)
+        self.embed_positions = (RelPositionalEncoding(hidden_size) if self.rel_pos
+                                else SinusoidalPositionalEmbedding(hidden_size, 0))
 
     def ordered_params(self):
         out = []
@@ -168,7 +178,8 @@ class ProDiffTeacher(nn.Module):
             self.spk_embed.num_embeddings if self.with_spk_embed else 0,
             self.lang_embed.num_embeddings if self.with_lang_embed else 0,
             int(self.with_dur_embed), int(self.with_spk_embed), int(self.with_gender_embed),
-            int(self.with_lang_embed), int(self.with_voicing_embed), int(self.with_breath_embed))
+            int(self.with_lang_embed), int(self.with_voicing_embed), int(self.with_breath_embed),
+            int(e.rel_pos))
 
     def ordered_cond_params(self):
         """Tensors in the include/prodiff_hip.h pd_cond order (== reference state-dict order)."""

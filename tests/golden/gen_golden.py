@@ -444,6 +444,8 @@ COND_CASES = {
     # 1 head (head dim 256), long utterances: many query / key blocks, T_mel ~ 2000
     "cond_long": (dict(num_spk=2, num_langs=3, num_heads=1, enc_layers=2, use_breath_embed=False),
                   80, [300, 257], 0, 44, 144, "mix_1"),
+    # RelPositionalEncoding (tts_modules.py:299-300,324-325), padded batch
+    "cond_relpos": (dict(num_spk=2, num_langs=3, enc_layers=2, rel_pos=True), 40, [21, 13], 1, 45, 145, "id"),
 }
 
 

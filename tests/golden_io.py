@@ -54,4 +54,4 @@ def cond_case(name):
     return hp, P, ins, d
 
 
-COND_CASES = ("cond_small", "cond_handler", "cond_mix_gender", "cond_long")
+COND_CASES = ("cond_small", "cond_handler", "cond_mix_gender", "cond_long", "cond_relpos")
