@@ -157,8 +157,8 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
 # bench tag -> kernel symbols that can serve it (the default kernel first) for the PMC
 # traffic lookup; the first one present in a summary is used
 TAG_KERNEL = {
-    "fd_lvc_block_final": ("lvc_skew_bf16_kernel<true, true>", "lvc_block_bf16_kernel<384, true, true, true, true, false>"),
-    "fd_lvc_block_ups": ("lvc_skew_bf16_kernel<false, false>", "lvc_block_bf16_kernel<384, true, false, false, true, false>"),
+    "fd_lvc_block_final": ("lvc_block_bf16_kernel<384, true, true, true, true, false>",),
+    "fd_lvc_block_ups": ("lvc_block_bf16_kernel<384, true, false, false, true, false>",),
     "fd_lvc_block_sub": ("lvc_block_bf16_kernel<128, true, false, false, false, true>",),
     "fd_kp_kernel": ("kp_kernel_bf16_kernel",),
     "wn_layer": ("wn_layer_bf16_kernel",),
@@ -357,7 +357,7 @@ def main():
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default: newest profiles/r*_v*_traffic.json)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo launcher + sharding + gather check, no GPU")
     ap.add_argument("--fd-opt", action="append", default=[], metavar="NAME=VALUE",
-                    help="FastDiff kernel-variant option for A/B runs (fd_set_option, e.g. lvc_stream=1)")
+                    help="FastDiff kernel-variant option for A/B runs (fd_set_option, e.g. kp_chunk=4)")
     ap.add_argument("--wn-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="WaveNet kernel-variant option for A/B runs (pd_wavenet_set_option, e.g. layer=0)")
     args = ap.parse_args()

@@ -204,10 +204,9 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 #define FD_OPT_LVC_PF 3       /* 1: next-layer kernel fragments prefetched into registers (tile 384) */
 #define FD_OPT_LVC_SUB 4      /* 1: the hop < 32 block on the whole-block kernel too */
 #define FD_OPT_KP_SIDE 5      /* 1: kernel-predictor GEMMs of fd_sample on a low-priority side stream */
-#define FD_OPT_LVC_STREAM 6   /* 1: hop % 32 == 0 blocks on the streaming LVC pipeline kernel (default 0) */
+/* 6: reserved (r02's streaming LVC kernel, removed in r03: measured slower) */
 #define FD_OPT_KP_CHUNK 7     /* n > 0: kernel predictor + LVC block per chunk of n utterances (default 0 = whole batch) */
-#define FD_OPT_LVC_SKEW 8     /* 1: hop >= 64 blocks with r in {4,8} on the skewed persistent LVC kernel (default 0) */
-#define FD_OPT_LVC_SEG 9      /* n > 0: skewed-kernel segment length in 32-row tiles (default 0 = ~one workgroup per CU) */
+/* 8, 9: reserved (r03's skewed persistent LVC kernel, removed: measured slower) */
 int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */

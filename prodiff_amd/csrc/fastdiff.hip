@@ -62,10 +62,6 @@ struct fd_model {
   bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (FD_OPT_LVC_FUSE)
   bool lvc_pf = true;          // next-layer kernel fragments prefetched into registers (FD_OPT_LVC_PF)
   bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (FD_OPT_LVC_SUB)
-  // hop % 32 == 0 blocks with a fused upsample on the streaming kernel (FD_OPT_LVC_STREAM).  Off:
-  // measured slower than the whole-block kernel (r02: 688 vs 454 us on the hop-256 block,
-  // DESIGN.md §4), kept as a tested variant.
-  bool lvc_stream = false;
   // fd_sample (bf16): the kernel-predictor GEMMs run on a second, low-priority stream into a
   // ring of one K buffer per block, so step j+1's kernels for block n are written while
   // step j's later blocks run (FD_OPT_KP_SIDE).  Created on first use.  Off by default:
@@ -73,11 +69,7 @@ struct fd_model {
   // saves (r01 ab_v16b: 7.41 vs 7.33 ms/step).
   bool kp_side = false;
   int kp_chunk = 0;   // FD_OPT_KP_CHUNK: utterances per kernel-predictor -> LVC chunk (0 = whole batch)
-  // hop >= 64 blocks with a fused upsample (r in {4, 8}) on the skewed persistent kernel
-  // (lvc_skew_bf16_kernel, FD_OPT_LVC_SKEW); lvc_seg overrides its segment length in tiles.
-  bool lvc_skew = false;
-  int lvc_seg = 0;
-  int ncu = 256;      // compute units of the device (one skewed-kernel workgroup each)
+
   mutable hipStream_t side = nullptr;
   mutable hipEvent_t ev_hidden = nullptr, ev_kp[4] = {}, ev_lvc[4] = {};
   float* pool = nullptr;
@@ -1001,1067 +993,6 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
 #undef TILE
 }
 
-// ------------------------------------------------------------------ skewed persistent LVC block (bf16)
-// All 4 layers of one TimeAware_LVCBlock (modules.py:205-217) with the ConvTranspose
-// upsample in front (always fused), audio_down recomputed from the audio (AUD) and the
-// final conv + sampler update behind (FIN), for hop a power of 2 >= 64, r in {4, 8}.
-//
-// Why: the whole-block kernel recomputes a 64-row halo on each side of every 384-row
-// tile (25% of its MFMA/VALU work) and each of its short-lived workgroups pays a cold
-// prologue (x_prev, audio, biases, kernel fragments: ~30% of its life) and an epilogue
-// that nothing overlaps.  Here ONE workgroup per CU walks a long time segment of one
-// utterance in steps of W tiles and carries every layer's state from step to step, so
-// no row is computed twice and the next step's operands load under this step.
-//
-// The stencil dependency of layer l on layer l-1 (rows +-(d_l + 1)) is met by a
-// tile-level skew: at step j, stage U (upsample + audio_down) covers local tiles
-// [Wj+1, Wj+W+1), layer l covers [Wj-l, Wj-l+W) and the final-conv stage [Wj-4, Wj).
-// Local tile i belongs to wave pair i mod W in every stage; the pair splits the 32
-// residual channels (wave 2p + c owns channels 16c .. 16c+15), so a tile's fp32 state
-// (z = x + a and a) never leaves its waves.  The split is free for the location-variable
-// conv: a channel half's gate and filter rows of the frame kernel form one 32-row MFMA
-// operand (6 fragments per wave, no kernel byte loaded twice), and its accumulator holds
-// matching gate/filter pairs.  The pre-conv output (all 32 channels feed every LVC) is
-// split the same way on 16x16x32 MFMAs.  8 waves = 2 per SIMD, so one wave's MFMAs
-// overlap its partner's gate VALU and each one's LDS/barrier waits.
-// Because the windows shift, a pair holds two tiles for part of a step (slots `c` = the
-// layers' tile, `nx` = the U tile), switched by register moves at a pair-dependent layer.
-// Waves meet only through LDS and 10 barriers per step:
-//   A1 final-conv combine of the previous step, upsample phase GEMMs -> XS, prefetches
-//   A2 x_0 + audio_down -> registers, u_0 = lrelu(z_0) -> ring
-//   B_l pre-conv of layer l (u_l ring -> y buffer)
-//   C_l location-variable conv + gate (y buffer, kernel fragments) -> z, u_{l+1} ring
-// LDS: u rings 4 x (W + 2) tiles (a tile's rows are read by both neighbours), the y
-// buffer, pre-conv weights, an LVC-bias ring, staged x_prev, an audio ring and the
-// final-conv partial sums (one plane per channel half); the fp32 upsample output XS lives
-// in u-ring slots of layers 1-2 that are dead during A1/A2.  bf16 rows are 64 B with the
-// 16-B chunks XOR-swizzled by (row >> 2) & 3 (conflict-free b128 reads at any row offset).
-// Results equal the whole-block kernel's roundings up to fp32 summation order (the
-// accumulators start from the LVC bias as in its prefetch variant; the final conv sums
-// per-row partials).
-namespace lsw {
-constexpr int W = 4, NWV = 2 * W, NTH = 64 * NWV;          // tiles per step; a wave pair per tile
-constexpr int RT = W + 2;                                  // u-ring tiles per layer
-// Every ring is stored with a mirror tile at each end (physical slots 0 .. RT + 1: slot
-// (i mod RT) + 1 holds tile i, slot 0 repeats slot RT, slot RT + 1 repeats slot 1), so the
-// rows a tile's pre-conv reads (-28 .. +60 around it) are contiguous: one address per
-// lane plus immediate offsets, no per-lane wrap.
-constexpr int RP = RT + 2;
-constexpr int LDB = 80;                                    // bytes per bf16 row: 32 channels + 16 B pad
-constexpr int TB = 32 * LDB;                               // bytes per tile
-constexpr int U_LAYER = RP * TB;
-constexpr int U_OFF = 0;
-constexpr int YR = W * 32 + 2;                             // y buffer rows
-constexpr int Y_OFF = U_OFF + NLY * U_LAYER;
-constexpr int YC_OFF = Y_OFF + YR * LDB;                   // carries [layer][step parity][2 rows]
-constexpr int WC_OFF = YC_OFF + NLY * 2 * 2 * LDB;
-constexpr int BC_OFF = WC_OFF + NLY * 6 * 64 * 16;
-constexpr int BU_OFF = BC_OFF + NLY * CI * 4;
-constexpr int XP_OFF = BU_OFF + CI * 4;
-constexpr int XPR = 66;                                    // staged x_prev rows (32 W / r + 2 used; + the
-                                                           // unused columns' reads, so no clamp)
-constexpr int BF_OFF = XP_OFF + XPR * LDB;
-constexpr int XLD = 144;                                   // bytes per fp32 XS row (32 channels + pad)
-constexpr int NF = 8;                                      // LVC-bias ring frames
-constexpr int AUR = 16;                                    // audio ring tiles (>= 2W + 6, a power of 2)
-constexpr int PR = 256;                                    // final-conv partial rows (>= 6 tiles, a power of 2)
-template <bool AUD, bool FIN> struct Geo {
-  static constexpr int AU_OFF = BF_OFF + NF * NLY * 2 * CI * 4;
-  static constexpr int FW_OFF = AU_OFF + (AUD || FIN ? AUR * 32 * 4 : 0);
-  static constexpr int FF_OFF = FW_OFF + (AUD ? (7 + 1) * 32 * 4 : 0);   // first conv [tap][c] + bias
-  static constexpr int P_OFF = FF_OFF + (FIN ? 7 * 32 * 4 : 0);           // final conv [tap][c]
-  static constexpr int SMEM = P_OFF + (FIN ? 2 * PR * 7 * 4 : 0);         // partials [half][row][tap]
-};
-}  // namespace lsw
-#ifdef LB_TRACE
-// tools/skew_probe.hip: s_memtime stamps of workgroup 37, steps 8..15, [step][wave][20]
-#define SK_STAMP(jj, idx)                                                                    \
-  do {                                                                                       \
-    if (lane == 0 && blockIdx.x == 37 && (jj) >= 8 && (jj) < 16)                             \
-      P.trace[(((jj) - 8) * lsw::NWV + wv) * 20 + (idx)] = __builtin_readcyclecounter();    \
-  } while (0)
-#else
-#define SK_STAMP(jj, idx) \
-  do {                    \
-  } while (0)
-#endif
-
-template <bool AUD, bool FIN>
-__global__ __launch_bounds__(lsw::NTH, 2) void lvc_skew_bf16_kernel(const LvcBlockArgs P, int nseg, int seg_tiles) {
-  using namespace lsw;
-  using GG = Geo<AUD, FIN>;
-  static_assert(GG::SMEM <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char sm[GG::SMEM];
-  // wave index in an SGPR: every tile index and slot decision below is wave-uniform.
-  // m = the pair's tile group (local tile i = m mod W), ch = channel half.
-  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int m = wv >> 1, ch = wv & 1;
-  const int n = lane & 31, h = lane >> 5;            // 32x32 MFMA lane coordinates
-  const int m16 = lane & 15, q16 = lane >> 4;        // 16x16 MFMA lane coordinates
-  const int b = blockIdx.x / nseg, sg = blockIdx.x - b * nseg;
-  const int Tc = P.Tc, hop = P.hop, Lh = Tc * hop, NTu = Lh >> 5;
-  const int tau0 = sg * seg_tiles, tau1 = min(tau0 + seg_tiles, NTu);
-  if (tau0 >= tau1) return;                          // whole workgroup (uniform)
-  const int sigma = tau0 - 3;                        // global tile of local tile 0 (3 halo tiles)
-  const int nloc = tau1 - sigma;                     // outputs: local tiles [3, nloc)
-  const int J = (nloc + 3) / W + 1;                  // the last final-conv window [W(J-1)-4, W(J-1)+W-4) reaches nloc
-  const long long base = (long long)b * Lh;
-  const int r = P.r, pp = P.p, Tin = Lh / r;
-  const int fsh = __builtin_ctz(hop >> 5);           // tiles per frame = hop / 32, a power of 2
-  auto gt = [&](int i) { return sigma + i; };        // local -> global tile
-  auto inside = [&](int i) { return gt(i) >= 0 && gt(i) < NTu; };
-  auto frame_of = [&](int i) { return min(max(gt(i), 0) >> fsh, Tc - 1); };
-  auto pslot = [&](int i) { return (i % RT + RT) % RT + 1; };   // physical ring slot of local tile i
-  auto lds4 = [&](int off) -> float4& { return *reinterpret_cast<float4*>(sm + off); };
-  auto ldsb8 = [&](int off) -> bf16x8& { return *reinterpret_cast<bf16x8*>(sm + off); };
-  auto ldsf = [&](int off) -> float& { return *reinterpret_cast<float*>(sm + off); };
-  // this wave's channels in the 32x32 C layout: element e <-> channel 16ch + 4h + (e & 3) + 8(e >> 2)
-  const int cb0 = 16 * ch + 4 * h, cb1 = cb0 + 8;
-  // per-lane LDS address parts (constant for the whole kernel)
-  const int lc_ub = m16 * LDB + q16 * 16;                                        // pre-conv B (u rows)
-  const int lc_wc = WC_OFF + ((q16 >> 1) * 64 + 32 * (q16 & 1) + 16 * ch + m16) * 16;   // pre-conv A
-  const int lc_bc = BC_OFF + (16 * ch + 4 * q16) * 4;                            // pre-conv bias
-  const int lc_yw = Y_OFF + (2 + m16) * LDB + (2 * (q16 & 1) + ch) * 16 + 8 * (q16 >> 1);   // y write
-  const int lc_yr = Y_OFF + n * LDB + h * 16;                                    // LVC B (y rows)
-  const int lc_uw = n * LDB + (2 * h + ch) * 16;                                 // u write (lvc_pos 16h+8ch..)
-  const int lc_bf = BF_OFF + cb0 * 4;                                            // LVC bias
-
-  // ---- prologue: zero the state, stage the weights
-  for (int i = tid; i < GG::SMEM / 16; i += NTH) reinterpret_cast<uint4*>(sm)[i] = uint4{0u, 0u, 0u, 0u};
-  __syncthreads();
-  for (int i = tid; i < NLY * 6 * 64; i += NTH) {
-    const int l = i / 384, kk = (i >> 6) % 6, ln = i & 63;
-    const __bf16* w = P.Wc[l] + (ln & 31) * 96 + (kk >> 1) * 32 + 16 * (ln >> 5) + 4 * (kk & 1);
-    const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(w), w1 = *reinterpret_cast<const bf16x4*>(w + 8);
-    ldsb8(WC_OFF + i * 16) = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
-  }
-  if (tid < NLY * CI) ldsf(BC_OFF + tid * 4) = P.bc[tid / CI][tid % CI];
-  if (tid < CI) ldsf(BU_OFF + tid * 4) = P.bup[tid];
-  if constexpr (AUD) {
-    if (tid < 224) ldsf(GG::FW_OFF + tid * 4) = P.fw[(tid & 31) * 7 + (tid >> 5)];   // fw is [c][tap]
-    if (tid < 32) ldsf(GG::FW_OFF + (224 + tid) * 4) = P.fb[tid];
-  }
-  if constexpr (FIN) {
-    if (tid < 224) ldsf(GG::FF_OFF + tid * 4) = P.wfin[tid];                        // already [tap][c]
-  }
-  const float bfin = FIN ? P.bfin[0] : 0.f;
-  // upsample phase GEMM job of this wave: phase wv % r on column tile wv / r (r * tiles = 8);
-  // its weights are re-loaded (L2-resident) at the end of each step, ahead of the kernel prefetch
-  const int uk = wv % r, ujt = wv / r;
-  const int rw = r * (ujt * 32 + n) + uk - pp;       // the window row this lane's column writes (t - T0)
-  const bool rw_ok = rw >= 0 && rw < 32 * W;
-  bf16x8 wup[4];
-  auto wup_load = [&]() {
-    const __bf16* wa = P.Wup + ((long long)uk * 32 + n) * 64 + 8 * h;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) wup[kk] = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
-  };
-  wup_load();
-  // XS (fp32 upsample output) in ring 1 (rows 0-15 of a window tile) / ring 2 (rows 16-31):
-  // window tile q of step j lives in the slot of local tile Wj - ring + 1 + q, which that
-  // ring's writer (layer ring - 1) rewrites later in the same step
-  auto xsoff = [&](int j, int rr) {
-    const int ring = 1 + ((rr >> 4) & 1);
-    const int ps = pslot(W * j - ring + 1 + (rr >> 5));
-    return U_OFF + ring * U_LAYER + ps * TB + (rr & 15) * XLD;
-  };
-  // per-step operand loads (issued one step ahead, stored to LDS at the end of the step)
-  const float* xprev = P.xin + (long long)b * Tin * CI;
-  const int xpn = 32 * W / r + 2;                    // x_prev rows per step
-  constexpr int IX = ((32 * W / 4 + 2) * 8 + NTH - 1) / NTH;   // float4 per thread
-  float4 xv[IX];
-  float av = 0.f;
-  float4 bfv;
-  const int nfill = ((W + 4) * 32 + hop - 1) / hop + 1;   // LVC-bias frames a step can touch (<= 8)
-  auto flo = [&](int j) { return max(gt(W * j - 3), 0) >> fsh; };
-  auto issue_xprev = [&](int j) {                    // x_prev rows jb .. jb + xpn of step j
-    const int jb = 32 * gt(W * j + 1) / r - 1;
-#pragma unroll
-    for (int it = 0; it < IX; ++it) {
-      const int i = tid + it * NTH, q = (i & 7) * 4, jj = min(max(jb + (i >> 3), 0), Tin - 1);
-      xv[it] = *reinterpret_cast<const float4*>(xprev + (long long)jj * CI + q);
-    }
-  };
-  auto store_xprev = [&](int j) {
-    const int jb = 32 * gt(W * j + 1) / r - 1;
-#pragma unroll
-    for (int it = 0; it < IX; ++it) {
-      const int i = tid + it * NTH, rr = i >> 3, q = (i & 7) * 4, jj = jb + rr;
-      if (rr < xpn) {
-        const float mk = (jj >= 0 && jj < Tin) ? 1.f : 0.f;     // rows outside x_prev are zero
-        const f32x2 u0 = lrelu2(f32x2{xv[it].x, xv[it].y} * mk), u1 = lrelu2(f32x2{xv[it].z, xv[it].w} * mk);
-        *reinterpret_cast<bf16x4*>(sm + XP_OFF + rr * LDB + q * 2) =
-            bf16x4{(__bf16)u0.x, (__bf16)u0.y, (__bf16)u1.x, (__bf16)u1.y};
-      }
-    }
-  };
-  auto aroff = [&](int R) { return GG::AU_OFF + (R & (AUR * 32 - 1)) * 4; };
-  auto issue_audio = [&](int t0tile) {               // AUD / FIN: W tiles of samples from local tile t0tile
-    if (tid < 32 * W) {
-      const int t = gt(t0tile) * 32 + tid;
-      av = P.audio[base + min(max(t, 0), Lh - 1)];
-    }
-  };
-  auto store_audio = [&](int t0tile) {
-    if (tid < 32 * W) {
-      const int t = gt(t0tile) * 32 + tid;
-      ldsf(aroff(t0tile * 32 + tid)) = (t >= 0 && t < Lh) ? av : 0.f;
-    }
-  };
-  auto issue_bias = [&](int j) {                     // frames flo(j) .. + 8, 64 float4 each
-    const int fr = flo(j) + (tid >> 6), c = (tid & 63) * 4;
-    bfv = *reinterpret_cast<const float4*>(P.Bf + ((long long)b * Tc + min(fr, Tc - 1)) * (2 * CI * NLY) + c);
-  };
-  auto store_bias = [&](int j) {
-    const int fr = flo(j) + (tid >> 6), c = (tid & 63) * 4;
-    if ((tid >> 6) < nfill) {
-      // gate pre-scale (the accumulators are exp2 arguments); frames past the end are zero
-      const float sc = fr >= Tc ? 0.f : (c & 63) < 32 ? -LOG2E : 2.f * LOG2E;
-      lds4(BF_OFF + ((fr % NF) * 256 + c) * 4) = make_float4(bfv.x * sc, bfv.y * sc, bfv.z * sc, bfv.w * sc);
-    }
-  };
-  // kernel fragments of (layer, local tile): this half's gate rows 16ch.. and filter rows
-  // 32+16ch.. as ONE 32-row A operand (A-row n < 16: gate 16ch + n; n >= 16: filter 16ch + n-16),
-  // picked from the frame-major fragment order (kp_kernel_bf16_kernel)
-  bf16x8 kn[6];
-  const int kofs = ((n >= 16 ? 6 * 64 : 0) + 32 * h + 16 * ch + (n & 15)) * 16;   // bytes
-  auto kload = [&](int l, int i) {
-    const char* kq = reinterpret_cast<const char*>(P.Kf[l] + ((long long)b * Tc + frame_of(i)) * KPERLAYER);
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk) kn[kk] = *reinterpret_cast<const bf16x8*>(kq + kofs + kk * 1024);
-  };
-  // audio_down of the U tile (non-AUD: loaded one step ahead, this wave's 8 channels per lane)
-  float4 apf[2];
-  auto issue_a = [&](int i) {
-    const int t = min(max(gt(i) * 32 + n, 0), Lh - 1);
-    apf[0] = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + cb0);
-    apf[1] = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + cb1);
-  };
-  // this pair's tile in stage U / layer l at step j
-  auto iU = [&](int j) { return W * j + (m == 0 ? W : m); };
-  auto iL = [&](int j, int l) { return W * j + m - (m + l >= W ? W : 0); };
-  // bf16 row of tile i (this lane's row n, its 8 channels) into ring l, and the mirror copy
-  auto uwrite = [&](int l, int i, const bf16x8& v) {
-    const int ps = pslot(i);
-    ldsb8(lc_uw + U_OFF + l * U_LAYER + ps * TB) = v;
-    if (ps == RT) ldsb8(lc_uw + U_OFF + l * U_LAYER) = v;
-    if (ps == 1) ldsb8(lc_uw + U_OFF + l * U_LAYER + (RT + 1) * TB) = v;
-  };
-
-  // step-0 operands
-  issue_xprev(0);
-  if constexpr (AUD || FIN) {
-    // tiles [-4, W + 2): step 0's final-conv window and audio_down taps
-    for (int i = tid; i < (W + 6) * 32; i += NTH) {
-      const int t = gt(-4) * 32 + i;
-      ldsf(aroff(-4 * 32 + i)) = (t >= 0 && t < Lh) ? P.audio[base + min(max(t, 0), Lh - 1)] : 0.f;
-    }
-  }
-  issue_bias(0);
-  if constexpr (!AUD) issue_a(iU(0));
-  kload(0, iL(0, 0));
-  store_xprev(0);
-  store_bias(0);
-  __syncthreads();
-
-  // fp32 state (this wave's 8 channels per lane): the layers' tile (c) and the U tile (nx)
-  f32x2 cz[4], ca[4], nz[4], na[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) { cz[p] = ca[p] = nz[p] = na[p] = f32x2{0.f, 0.f}; }
-  auto swap_slots = [&]() {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const f32x2 tz = cz[p], ta = ca[p];
-      cz[p] = nz[p]; ca[p] = na[p]; nz[p] = tz; na[p] = ta;
-    }
-  };
-  auto pofs = [&](int half, int R, int tap) { return GG::P_OFF + ((half * PR + (R & (PR - 1))) * 7 + tap) * 4; };
-
-  // final-conv combine of step jf's window: eps(t) = b + sum_tap P(t + tap - 3)[tap];
-  // audio_out = (x_t - ce eps) / den + sig z   (FastDiff_model.py:100, util.py:222-226)
-  auto fin_combine = [&](int jf) {
-    if (tid < 32 * W) {
-      const int R = 32 * (W * jf - 4) + tid, i = R >> 5, t = 32 * sigma + R;
-      if (i >= 3 && i < nloc && t >= 0 && t < Lh) {
-        float e = 0.f;
-#pragma unroll
-        for (int tap = 0; tap < 7; ++tap) e += ldsf(pofs(0, R + tap - 3, tap)) + ldsf(pofs(1, R + tap - 3, tap));
-        e += bfin;
-        float v = (ldsf(aroff(R)) - P.ce * e) / P.den;
-        if (P.sig != 0.f)
-          v += P.sig * (P.noise ? P.noise[base + t]
-                                : philox_normal_u(P.seed, utt_id(P.uid, b + P.b_off), (unsigned)t, P.stream));
-        P.audio_out[base + t] = v;
-      }
-    }
-  };
-
-  for (int j = 0; j < J; ++j) {
-    SK_STAMP(j, 0);
-    // ================= A1: previous final conv, upsample phase GEMM -> XS, next-step loads
-    if constexpr (FIN) {
-      if (j > 0) fin_combine(j - 1);
-    }
-    {
-      // C^T[co][col] = [W_k^T | W_{k+r}^T] . [xp(j0); xp(j0 - 1)],  t = r j0 + k - p  (modules.py:205-206)
-      // column c' = ujt*32 + n is input j0 = T0 / r + c' (XP row c' + 1): window row rw = r c' + k - p
-      f32x16 acc;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-      const int xo = XP_OFF + (ujt * 32 + n) * LDB + h * 16;
-      bf16x8 xb[4];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) xb[kk] = ldsb8(xo + (kk < 2 ? LDB : 0) + 32 * (kk & 1));
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wup[kk], xb[kk], acc, 0, 0, 0);
-      if (rw_ok) {
-        const int xs = xsoff(j, rw);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 bv = lds4(BU_OFF + (8 * g + 4 * h) * 4);
-          lds4(xs + (2 * g + h) * 16) =
-              make_float4(acc[4 * g] + bv.x, acc[4 * g + 1] + bv.y, acc[4 * g + 2] + bv.z, acc[4 * g + 3] + bv.w);
-        }
-      }
-    }
-    if (j + 1 < J) {
-      issue_xprev(j + 1);
-      issue_bias(j + 1);
-      if constexpr (AUD || FIN) issue_audio(W * j + W + 2);
-    }
-    SK_STAMP(j, 1);
-    __syncthreads();
-    SK_STAMP(j, 2);
-    // ================= A2: z_0 = upsample + audio_down of the U tile, u_0 ring
-    {
-      const int iu = iU(j), q = iu - W * j - 1, R = 32 * iu + n;
-      const int xs = xsoff(j, 32 * q + n);
-      f32x2 x0[4], a0[4];
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        const int cb = g ? cb1 : cb0;
-        const float4 xv4 = lds4(xs + cb * 4);
-        float4 a4;
-        if constexpr (AUD) {
-          // a0[t][c] = b[c] + sum_tap w[c][tap] audio[t + tap - 3]  (first_conv_kernel's order)
-          float sa[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) sa[c] = ldsf(GG::FW_OFF + (224 + cb + c) * 4);
-#pragma unroll
-          for (int tap = 0; tap < 7; ++tap) {
-            const float au = ldsf(aroff(R + tap - 3));
-            const float4 w = lds4(GG::FW_OFF + (tap * 32 + cb) * 4);
-            sa[0] = fmaf(w.x, au, sa[0]); sa[1] = fmaf(w.y, au, sa[1]);
-            sa[2] = fmaf(w.z, au, sa[2]); sa[3] = fmaf(w.w, au, sa[3]);
-          }
-          a4 = make_float4(sa[0], sa[1], sa[2], sa[3]);
-        } else {
-          a4 = apf[g];
-        }
-        x0[2 * g] = f32x2{xv4.x + a4.x, xv4.y + a4.y}; x0[2 * g + 1] = f32x2{xv4.z + a4.z, xv4.w + a4.w};
-        a0[2 * g] = f32x2{a4.x, a4.y}; a0[2 * g + 1] = f32x2{a4.z, a4.w};
-      }
-      bf16x8 u0 = {};
-      if (inside(iu)) {                              // rows outside the utterance stay zero (conv padding)
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const f32x2 v = lrelu2(x0[p]);
-          u0[2 * p] = (__bf16)v.x; u0[2 * p + 1] = (__bf16)v.y;
-        }
-      }
-      uwrite(0, iu, u0);                             // positions 16h + 8ch + e (lvc_pos of the channels)
-#pragma unroll
-      for (int p = 0; p < 4; ++p) { nz[p] = x0[p]; na[p] = a0[p]; }
-      // pair 0's U tile is next step's; pairs m >= 1 start this step's layers on it, and
-      // keep their older tile (layers >= W - m) in `nx` until then
-      if (m >= 1) swap_slots();
-    }
-    SK_STAMP(j, 3);
-    __syncthreads();
-    // ================= layers (unrolled: the slot switch and the last layer's epilogue are
-    // static per layer, so the state registers are not shuffled through loop phis)
-#pragma unroll
-    for (int l = 0; l < NLY; ++l) {
-      const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
-      const int i = iL(j, l), w = (m + l) % W;       // tile, window position (window at Wj - l)
-      if (l > 0 && m == W - l) swap_slots();         // the older tile takes over
-      if constexpr (!AUD) {
-        if (l == 0 && j + 1 < J) issue_a(iU(j + 1));
-      }
-      SK_STAMP(j, 4 + 4 * l);
-      // ---- B_l: y rows [32i+1, 32i+33) = lrelu(W_c . [u(t-d); u(t); u(t+d)] + b) -> y rows 32w+2..,
-      //      this wave's 16 output channels 16ch.. on 16x16x32 MFMAs (2 row blocks x 3 taps)
-      {
-        // every operand of the 6 MFMAs is read before the first one issues (one LDS latency)
-        const int ub = lc_ub + U_OFF + l * U_LAYER + (32 * pslot(i) + 1 - d) * LDB;
-        bf16x8 wa[3], uv[2][3];
-#pragma unroll
-        for (int ks = 0; ks < 3; ++ks) {   // the 32x32x16 fragment (k-step 2ks + q/2, lane 32(q&1) + 16ch + m16)
-          wa[ks] = ldsb8(lc_wc + (l * 6 + 2 * ks) * 1024);
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb) uv[rb][ks] = ldsb8(ub + (ks * d + 16 * rb) * LDB);
-        }
-        const float4 bv = lds4(lc_bc + l * CI * 4);
-        __builtin_amdgcn_sched_barrier(0);
-        f32x4 acc[2];
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 3; ++ks)
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb)
-            acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks], uv[rb][ks], acc[rb], 0, 0, 0);
-        f32x2 v[2][2];
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          v[rb][0] = lrelu2(f32x2{acc[rb][0], acc[rb][1]} + f32x2{bv.x, bv.y});
-          v[rb][1] = lrelu2(f32x2{acc[rb][2], acc[rb][3]} + f32x2{bv.z, bv.w});
-        }
-        const int tt = 32 * gt(i) + 1;                // global time of this pre-conv tile's row 0
-        if (tt < 0 || tt + 31 >= Lh) {                // utterance-edge tile: the LVC zero-pads y
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb) {
-            const int t = tt + 16 * rb + m16;
-            if (t < 0 || t >= Lh) { v[rb][0] = f32x2{0.f, 0.f}; v[rb][1] = f32x2{0.f, 0.f}; }
-          }
-        }
-        // lvc_pos(co + e) = 16(q&1) + 8ch + 4(q>>1) + e: 4 contiguous positions (8 bytes)
-        const int yw = lc_yw + 32 * w * LDB;
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          const bf16x4 y4 = {(__bf16)v[rb][0].x, (__bf16)v[rb][0].y, (__bf16)v[rb][1].x, (__bf16)v[rb][1].y};
-          *reinterpret_cast<bf16x4*>(sm + yw + 16 * rb * LDB) = y4;
-          if (w == W - 1 && rb == 1 && m16 >= 14)    // rows 32W, 32W + 1: the next step's rows 0, 1
-            *reinterpret_cast<bf16x4*>(sm + yw + 16 * LDB - Y_OFF - (32 * W) * LDB + YC_OFF + (l * 2 + (j & 1)) * 2 * LDB) = y4;
-        }
-        if (w == 0 && ch == 0 && lane < 10) {        // rows 0, 1 from the previous step (2 x 80 B)
-          const int ci = YC_OFF + ((l * 2 + ((j + 1) & 1)) * 2) * LDB + lane * 16;
-          *reinterpret_cast<uint4*>(sm + Y_OFF + lane * 16) = *reinterpret_cast<const uint4*>(sm + ci);
-        }
-      }
-      SK_STAMP(j, 5 + 4 * l);
-      __syncthreads();
-      SK_STAMP(j, 6 + 4 * l);
-      // ---- C_l: o^T = K_frame . [y(t-1); y(t); y(t+1)]^T + Bf;  z += gate(o) (+ a)
-      {
-        f32x16 acc;
-        bf16x8 yb[6];
-        {
-          const int bo = lc_bf + ((frame_of(i) % NF) * NLY + l) * 2 * CI * 4;
-          const float4 g0 = lds4(bo), g1 = lds4(bo + 32), f0 = lds4(bo + 128), f1 = lds4(bo + 160);
-          acc[0] = g0.x; acc[1] = g0.y; acc[2] = g0.z; acc[3] = g0.w;
-          acc[4] = g1.x; acc[5] = g1.y; acc[6] = g1.z; acc[7] = g1.w;
-          acc[8] = f0.x; acc[9] = f0.y; acc[10] = f0.z; acc[11] = f0.w;
-          acc[12] = f1.x; acc[13] = f1.y; acc[14] = f1.z; acc[15] = f1.w;
-          const int yr = lc_yr + 32 * w * LDB;
-#pragma unroll
-          for (int kk = 0; kk < 6; ++kk) yb[kk] = ldsb8(yr + (kk >> 1) * LDB + 32 * (kk & 1));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kk = 0; kk < 6; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb[kk], acc, 0, 0, 0);
-        // next LVC's kernel fragments, in flight under the gate, the next pre-conv and barriers
-        // (issued once this chain has read its fragments)
-        __builtin_amdgcn_sched_barrier(0);
-        if (l + 1 < NLY) {
-          kload(l + 1, iL(j, l + 1));
-        } else if (j + 1 < J) {
-          wup_load();
-          kload(0, iL(j + 1, 0));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const f32x2 o = gate2s(f32x2{acc[2 * p], acc[2 * p + 1]}, f32x2{acc[8 + 2 * p], acc[8 + 2 * p + 1]});
-          if (l + 1 < NLY) cz[p] += ca[p] + o;
-          else cz[p] += o;
-        }
-        if (l + 1 < NLY) {
-          bf16x8 u0 = {};
-          if (inside(i)) {
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-              const f32x2 v = lrelu2(cz[p]);
-              u0[2 * p] = (__bf16)v.x; u0[2 * p + 1] = (__bf16)v.y;
-            }
-          }
-          uwrite(l + 1, i, u0);
-        } else if constexpr (FIN) {
-          // per-row partial sums of the final conv over this half's channels: P[t][tap] = sum_c w[tap][c] x4[t][c]
-          float sv[7];
-#pragma unroll
-          for (int tap = 0; tap < 7; ++tap) {
-            const float4 w0 = lds4(GG::FF_OFF + (tap * 32 + cb0) * 4), w1 = lds4(GG::FF_OFF + (tap * 32 + cb1) * 4);
-            float s = fmaf(w0.x, cz[0].x, fmaf(w0.y, cz[0].y, fmaf(w0.z, cz[1].x, w0.w * cz[1].y)));
-            s = fmaf(w1.x, cz[2].x, fmaf(w1.y, cz[2].y, fmaf(w1.z, cz[3].x, fmaf(w1.w, cz[3].y, s))));
-            sv[tap] = s + __shfl_xor(s, 32);
-          }
-          if (!inside(i)) {                           // the final conv zero-pads x outside the utterance
-#pragma unroll
-            for (int tap = 0; tap < 7; ++tap) sv[tap] = 0.f;
-          }
-          const int po = pofs(ch, 32 * i + n, 0);
-          if (h == 0) {
-#pragma unroll
-            for (int tap = 0; tap < 4; ++tap) ldsf(po + tap * 4) = sv[tap];
-          } else {
-#pragma unroll
-            for (int tap = 4; tap < 7; ++tap) ldsf(po + tap * 4) = sv[tap];
-          }
-        } else {
-          const int t = 32 * gt(i) + n;
-          if (i >= 3 && i < nloc && inside(i)) {
-            *reinterpret_cast<float4*>(P.xout + (base + t) * CI + cb0) = make_float4(cz[0].x, cz[0].y, cz[1].x, cz[1].y);
-            *reinterpret_cast<float4*>(P.xout + (base + t) * CI + cb1) = make_float4(cz[2].x, cz[2].y, cz[3].x, cz[3].y);
-          }
-        }
-        if (l == NLY - 1 && j + 1 < J) {             // the next step's staged operands
-          store_xprev(j + 1);
-          store_bias(j + 1);
-          if constexpr (AUD || FIN) store_audio(W * j + W + 2);
-        }
-      }
-      SK_STAMP(j, 7 + 4 * l);
-      __syncthreads();
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) { cz[p] = nz[p]; ca[p] = na[p]; }   // the U tile becomes the layers' tile
-  }
-  if constexpr (FIN) fin_combine(J - 1);
-}
-
-// Workgroups per utterance for the skewed kernel: about one per CU over the batch, at
-// least 8 tiles each.
-void lvc_skew_segments(int NTu, int B, int ncu, int seg_override, int* nseg, int* seg_tiles) {
-  const int s = seg_override > 0 ? cdiv(NTu, seg_override) : std::max(1, std::min((ncu + B - 1) / B, NTu / 8));
-  *seg_tiles = cdiv(NTu, s);
-  *nseg = cdiv(NTu, *seg_tiles);
-}
-
-// ------------------------------------------------------------------ streaming LVC block (bf16)
-// All 4 layers of one TimeAware_LVCBlock (modules.py:205-217) for hop % 32 == 0, with the
-// ConvTranspose upsample in front (UPS always), audio_down recomputed from the audio (AUD)
-// and the final conv + sampler update behind (FIN), as ONE streaming pipeline per workgroup.
-//
-// Why streaming: the whole-block kernel (lvc_block_bf16_kernel) recomputes a 64-row halo
-// on each side of every 384-row tile and runs its 8 waves through the same barrier-
-// separated phases (all waves in the gate at once, then all in the MFMAs), so a SIMD's
-// vector and matrix pipes rarely work together.  Here a workgroup walks ONE long time
-// range [R0, R1) of an utterance tile by tile (32 rows), with 2 halo tiles per side
-// (reach 47 rows < 64) for the whole range instead of per tile, and every wave keeps one
-// kind of work:
-//   * 4 "owner" waves (V): wave w owns the tiles j = w (mod 4).  Each step it runs the
-//     location-variable conv + gate of one layer on one of its tiles, and keeps the
-//     tiles' fp32 state z = x + a in registers across the 4 layers (a 4-deep queue).
-//   * 4 "pre-conv" waves (P): wave 4 + l computes layer l's dilated pre-conv
-//     y = lrelu(W_l . [u(t-d); u(t); u(t+d)] + b), u = lrelu(z), for one tile per step.
-//     Wave 5 also runs the input stage S (upsample + audio_down -> u_0), wave 7 the final
-//     conv + sampler update F.
-// The waves of a step touch different tiles, so a SIMD hosts one V and one P wave with
-// MFMA work and gate work interleaved.  Tiles meet through LDS rings (one per layer) and
-// ONE workgroup barrier per step.  Stage schedule (a stage at step s sees everything done
-// at steps < s):  S(j) at j;  P_l(j) at j + Q_l, Q = 2, 6, 11, 16;  V_l(j) at j + 5l + 4;
-// F(j) at j + 21.  P_l(j) reads u_l of tiles j-1..j+1 (written by V_{l-1} or S), V_l(j)
-// reads y_l of tiles j-1..j+1.  Owner w runs layer (s - w) mod 4 at step s, so inside its
-// unrolled 4-step cycle the layer is a compile-time constant.
-//
-// LDS (bytes): u rings 4 x 4 slots, y rings 4 + 3 x 5 slots (32 rows x 80 B), x_0 ring 5
-// slots and x_4 ring 4 slots (32 rows x 144 B), the audio samples of 32 tiles (AUD, FIN) =
-// 136 KB: one workgroup (8 waves) per CU.
-// Latency: the only global loads a V wave waits on are its kernel/bias fragments, loaded into
-// registers one step ahead, and the input stage's x_prev / audio_down / audio rows are loaded
-// two steps ahead (a barrier per step makes every step as slow as its slowest wave, so no
-// wave may wait on a cold load).  Every global pointer a wave indexes by a run-time layer is
-// read once before the step loop: a pointer load inside it would wait for all the wave's
-// outstanding prefetches (vmcnt retires in order).
-namespace lsk {
-constexpr int LD = 40, XLD = 36;
-constexpr int TROW = 32 * LD;                  // bf16 per ring slot
-constexpr int XROW = 32 * XLD;                 // fp32 per ring slot
-constexpr int NU = 4, NY0 = 4, NY = 5, NX0 = 5, NX4 = 4;
-constexpr int U_OFF = 0;                                   // bf16 units
-constexpr int Y_OFF = U_OFF + 4 * NU * TROW;
-constexpr int BF_END = Y_OFF + (NY0 + 3 * NY) * TROW;
-constexpr int X0_OFF = BF_END / 2;                         // fp32 units (BF_END is even)
-constexpr int X4_OFF = X0_OFF + NX0 * XROW;
-constexpr int NAU = 1024;                                  // audio ring: 32 tiles of samples
-constexpr int WLD = 72;                                    // bf16 per upsample weight row (64 + 8 pad)
-// the x_4 ring (FIN), audio ring (AUD) and upsample weights (ratio <= RMAX) exist per variant
-template <bool AUD, bool FIN, int RMAX> struct Geo {
-  static constexpr int AU_OFF = X4_OFF + (FIN ? NX4 * XROW : 0);
-  static constexpr int WU_OFF = AU_OFF + (AUD ? NAU : 0);               // fp32 units
-  static constexpr int SMEM = (WU_OFF + RMAX * 32 * WLD / 2) * 4;
-};
-constexpr int HALO = 2;                                    // halo tiles per side
-constexpr int LAG_F = 21, LAG_V3 = 19;
-__device__ __forceinline__ int qlag(int l) { return l == 0 ? 2 : l == 1 ? 6 : l == 2 ? 11 : 16; }
-__device__ __forceinline__ int ymod(int l) { return l == 0 ? 32 * NY0 : 32 * NY; }
-__device__ __forceinline__ int yslot0(int l) { return l == 0 ? 0 : NY0 + (l - 1) * NY; }
-__device__ __forceinline__ int pmod(int x, int m) { x %= m; return x < 0 ? x + m : x; }
-}  // namespace lsk
-#ifdef LB_TRACE
-// tools/stream_probe.hip: s_memtime stamps of workgroup (5, 0), steps 100..107, [step][wave][8]
-#define LS_STAMP(s, i)                                                                         \
-  do {                                                                                         \
-    if (lane == 0 && blockIdx.x == 5 && blockIdx.y == 0 && (s) >= 100 && (s) < 108)            \
-      P.trace[(((s) - 100) * 8 + wave) * 8 + (i)] = __builtin_readcyclecounter();             \
-  } while (0)
-#else
-#define LS_STAMP(s, i) \
-  do {                 \
-  } while (0)
-#endif
-
-template <bool AUD, bool FIN, int RMAX>
-__global__ __launch_bounds__(512, 1) void lvc_stream_bf16_kernel(const LvcBlockArgs P, int seg) {
-  using namespace lsk;
-  using GG = Geo<AUD, FIN, RMAX>;
-  constexpr int SMEM = GG::SMEM, AU_OFF = GG::AU_OFF, WU_OFF = GG::WU_OFF;
-  static_assert(SMEM + (FIN ? 7 * 32 * 4 : 16) <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  __shared__ __attribute__((aligned(16))) float FWF[FIN ? 7 * 32 : 4];
-  __bf16* const BS = reinterpret_cast<__bf16*>(smem);
-  float* const FS = reinterpret_cast<float*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, h = lane >> 5;
-  const int b = blockIdx.y;
-  const int Tc = P.Tc, hop = P.hop, Lh = Tc * hop;
-  const int R0 = blockIdx.x * seg, R1 = min(R0 + seg, Lh);
-  const int tg = R0 - 32 * HALO;                                // time of tile 0, row 0
-  const int NT = (R1 - R0 + 31) / 32 + 2 * HALO;
-  const int NSTEP = NT + (FIN ? LAG_F : LAG_V3) + 1;
-  const long long base = (long long)b * Lh;
-
-  // zero the rings: halo tiles read slots nobody wrote (rows outside [0, Lh) are written
-  // as zeros, the reference convs' zero padding)
-  for (int i = tid; i < SMEM / 16; i += 512) reinterpret_cast<uint4*>(smem)[i] = uint4{0u, 0u, 0u, 0u};
-  if constexpr (FIN) {
-    if (tid < 224) FWF[tid] = P.wfin[tid];                      // [tap][c]
-  }
-  {   // upsample phase weights [r][32 co][64] -> LDS rows of WLD (conflict-free A-fragment reads)
-    __bf16* WU = BS + 2 * WU_OFF;
-    for (int i = tid; i < P.r * 32 * 8; i += 512) {
-      const int row = i >> 3, c = (i & 7) * 8;
-      *reinterpret_cast<bf16x8*>(WU + row * WLD + c) = *reinterpret_cast<const bf16x8*>(P.Wup + row * 64 + c);
-    }
-  }
-  __syncthreads();
-  if constexpr (AUD) {     // audio samples of tile 0 (the input stage writes tile s + 1 at step s)
-    if (tid < 32) {
-      const int t = tg + tid;
-      FS[AU_OFF + tid] = (t >= 0 && t < Lh) ? P.audio[base + t] : 0.f;
-    }
-  }
-  __syncthreads();
-
-  // audio_down = first_conv(audio) (FastDiff_model.py:90) of one 32-row tile, in the MFMA C
-  // layout (lane = time tt + n, channels (reg&3) + 8(reg>>2) + 4h), as 2 bf16 MFMAs on a
-  // hi/lo split of weights and audio (|error| ~ 2^-16 relative):  A1 = [W_hi, b_hi | W_lo,
-  // b_lo], B1 = [x_hi(t-3..t+3), 1 | same];  A2 = [W_hi, 0 | 0], B2 = [x_lo(t-3..t+3), 0 | *].
-  bf16x8 fa1 = {}, fa2 = {};
-  if constexpr (AUD) {
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const float w = P.fw[n * 7 + k];                          // fw is [c][tap]
-      const __bf16 whi = (__bf16)w, wlo = (__bf16)(w - (float)whi);
-      fa1[k] = h ? wlo : whi;
-      fa2[k] = h ? (__bf16)0.f : whi;
-    }
-    const float bb = P.fb[n];
-    const __bf16 bhi = (__bf16)bb;
-    fa1[7] = h ? (__bf16)(bb - (float)bhi) : bhi;
-    fa2[7] = (__bf16)0.f;
-  }
-  auto audio_down = [&](int tt) -> f32x16 {
-    f32x16 acc;
-    if constexpr (AUD) {
-      // samples from the LDS ring (zero outside the utterance: the first conv's padding)
-      const float* ar = FS + AU_OFF;
-      const int i0 = tt - tg + n - 3;
-      float xv[7];
-#pragma unroll
-      for (int k = 0; k < 7; ++k) xv[k] = ar[(i0 + k) & (NAU - 1)];
-      bf16x8 bh, bl;
-#pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        bh[k] = (__bf16)xv[k];
-        bl[k] = (__bf16)(xv[k] - (float)bh[k]);
-      }
-      bh[7] = (__bf16)1.f;
-      bl[7] = (__bf16)0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, bh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa2, bl, acc, 0, 0, 0);
-    } else {
-      const int t = tt + n;
-      const bool ok = t >= 0 && t < Lh;
-      const float* ap = P.a + (base + min(max(t, 0), Lh - 1)) * CI + 4 * h;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float4 v = *reinterpret_cast<const float4*>(ap + 8 * i);
-        acc[4 * i] = ok ? v.x : 0.f; acc[4 * i + 1] = ok ? v.y : 0.f;
-        acc[4 * i + 2] = ok ? v.z : 0.f; acc[4 * i + 3] = ok ? v.w : 0.f;
-      }
-    }
-    return acc;
-  };
-  // u = bf16 lrelu(z) of one tile row into a ring slot (positions 16h + reg: kernel k-order)
-  auto store_u = [&](__bf16* row, const f32x2* z, bool in) {
-    bf16x8 u0, u1;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const f32x2 v0 = in ? lrelu2(z[p]) : f32x2{0.f, 0.f}, v1 = in ? lrelu2(z[4 + p]) : f32x2{0.f, 0.f};
-      u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
-      u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
-    }
-    *reinterpret_cast<bf16x8*>(row + 16 * h) = u0;
-    *reinterpret_cast<bf16x8*>(row + 16 * h + 8) = u1;
-  };
-
-  if (wave < 4) {
-    // ============================ owner waves: V_l(j), l = (s - w) mod 4
-    const int w = wave;
-    f32x2 z[4][8];                                   // z of the tiles at layers 0..3 (queue)
-    bf16x8 kn[12];                                   // prefetched kernel fragments of the next V stage
-    float4 bn[8];                                    // and its frame's LVC biases (4 gate, 4 filter)
-    auto prefetch = [&](int l, int j) {
-      const int fr = min(max((tg + 32 * j) / hop, 0), Tc - 1);
-      const long long row = (long long)b * Tc + fr;
-      const __bf16* kq = P.Kf[l] + row * KPERLAYER;
-#pragma unroll
-      for (int kk = 0; kk < 12; ++kk) kn[kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
-      const float* bq = P.Bf + row * (2 * CI * NLY) + l * 2 * CI + 4 * h;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        bn[i] = *reinterpret_cast<const float4*>(bq + 8 * i);
-        bn[4 + i] = *reinterpret_cast<const float4*>(bq + 32 + 8 * i);
-      }
-    };
-    prefetch(0, 0);
-    for (int s = 0; s < w; ++s) __syncthreads();
-    for (int c = 0; 4 * c + w < NSTEP; ++c) {
-      // queue shift: the tile at layer l last cycle is at layer l + 1 now
-#pragma unroll
-      for (int q = 3; q > 0; --q)
-#pragma unroll
-        for (int p = 0; p < 8; ++p) z[q][p] = z[q - 1][p];
-#pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        const int s = 4 * c + w + l;
-        if (s >= NSTEP) break;
-        const int j = s - 5 * l - 4;
-        LS_STAMP(s, 0);
-        if (j >= 0 && j < NT) {
-          const int tt = tg + 32 * j, t = tt + n;
-          const bool in = t >= 0 && t < Lh;
-          f32x16 av;
-          if (l < 3) av = audio_down(tt);
-          if (l == 0) {      // z_0 = x_0 (from the input stage) + a
-            const float* xr = FS + X0_OFF + pmod(32 * j + n, 32 * NX0) * XLD + 4 * h;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float4 v = *reinterpret_cast<const float4*>(xr + 8 * i);
-              z[0][2 * i] = f32x2{v.x + av[4 * i], v.y + av[4 * i + 1]};
-              z[0][2 * i + 1] = f32x2{v.z + av[4 * i + 2], v.w + av[4 * i + 3]};
-            }
-          }
-          LS_STAMP(s, 1);
-          // o^T = K . [y(t-1); y(t); y(t+1)]^T + Bf, pre-scaled for exp2 (kp_kernels_all prescale)
-          f32x16 g, f;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            g[4 * i] = -LOG2E * bn[i].x; g[4 * i + 1] = -LOG2E * bn[i].y;
-            g[4 * i + 2] = -LOG2E * bn[i].z; g[4 * i + 3] = -LOG2E * bn[i].w;
-            f[4 * i] = 2.f * LOG2E * bn[4 + i].x; f[4 * i + 1] = 2.f * LOG2E * bn[4 + i].y;
-            f[4 * i + 2] = 2.f * LOG2E * bn[4 + i].z; f[4 * i + 3] = 2.f * LOG2E * bn[4 + i].w;
-          }
-          const __bf16* Yl = BS + Y_OFF + yslot0(l) * TROW;
-          const int ym = ymod(l);
-#pragma unroll
-          for (int kk = 0; kk < 6; ++kk) {
-            const bf16x8 yb = *reinterpret_cast<const bf16x8*>(
-                Yl + pmod(32 * j + n + (kk >> 1) - 1, ym) * LD + 16 * (kk & 1) + 8 * h);
-            g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g, 0, 0, 0);
-            f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f, 0, 0, 0);
-          }
-          LS_STAMP(s, 2);
-          {   // the next step's V stage: layer (l + 1) mod 4
-            const int l2 = (l + 1) & 3, j2 = s + 1 - 5 * l2 - 4;
-            prefetch(l2, min(max(j2, 0), NT - 1));
-          }
-          LS_STAMP(s, 3);
-          // x_{l+1} = z_l + sigmoid(o_g) tanh(o_f); z_{l+1} = x_{l+1} + a (l < 3)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const f32x2 o0 = gate2s(f32x2{g[4 * i], g[4 * i + 1]}, f32x2{f[4 * i], f[4 * i + 1]});
-            const f32x2 o1 = gate2s(f32x2{g[4 * i + 2], g[4 * i + 3]}, f32x2{f[4 * i + 2], f[4 * i + 3]});
-            if (l < 3) {
-              z[l][2 * i] += o0 + f32x2{av[4 * i], av[4 * i + 1]};
-              z[l][2 * i + 1] += o1 + f32x2{av[4 * i + 2], av[4 * i + 3]};
-            } else {
-              z[l][2 * i] += o0;
-              z[l][2 * i + 1] += o1;
-            }
-          }
-          LS_STAMP(s, 4);
-          if (l < 3) {
-            store_u(BS + U_OFF + ((l + 1) * NU * 32 + ((32 * j + n) & (32 * NU - 1))) * LD, z[l], in);
-          } else if constexpr (FIN) {
-            float* xr = FS + X4_OFF + ((32 * j + n) & (32 * NX4 - 1)) * XLD + 4 * h;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              *reinterpret_cast<float4*>(xr + 8 * i) =
-                  in ? make_float4(z[3][2 * i].x, z[3][2 * i].y, z[3][2 * i + 1].x, z[3][2 * i + 1].y)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
-          } else {
-            if (t >= R0 && t < R1) {
-#pragma unroll
-              for (int i = 0; i < 4; ++i)
-                *reinterpret_cast<float4*>(P.xout + (base + t) * CI + 8 * i + 4 * h) =
-                    make_float4(z[3][2 * i].x, z[3][2 * i].y, z[3][2 * i + 1].x, z[3][2 * i + 1].y);
-            }
-          }
-        } else {    // no tile this step: still fetch the next step's fragments
-          const int l2 = (l + 1) & 3, j2 = s + 1 - 5 * l2 - 4;
-          prefetch(l2, min(max(j2, 0), NT - 1));
-        }
-        LS_STAMP(s, 6);
-        __syncthreads();
-      }
-    }
-  } else {
-    // ============================ pre-conv waves: P_l(j), l = wave - 4 (+ S on wave 5, F on wave 7)
-    const int l = wave - 4;
-    const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
-    bf16x8 wf[6];
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk) {
-      const __bf16* wq = P.Wc[l] + n * 96 + (kk >> 1) * 32 + 16 * h + 4 * (kk & 1);
-      const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(wq), w1 = *reinterpret_cast<const bf16x4*>(wq + 8);
-      wf[kk] = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
-    }
-    f32x2 bias[8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float4 bv = *reinterpret_cast<const float4*>(P.bc[l] + 8 * i + 4 * h);
-      bias[2 * i] = f32x2{bv.x, bv.y}; bias[2 * i + 1] = f32x2{bv.z, bv.w};
-    }
-    const __bf16* Ul = BS + U_OFF + l * NU * 32 * LD;
-    __bf16* Yl = BS + Y_OFF + yslot0(l) * TROW;
-    const int ym = ymod(l), ql = qlag(l);
-    // input stage (wave 5): ConvTranspose upsample (modules.py:205-206) from x_prev as r phase
-    // GEMMs on 16x16x32 MFMAs.  Output t = r m + k - p takes taps k (input m) and k + r (input
-    // m - 1): C[co][m] = [W_k^T | W_{k+r}^T] . [lrelu(x_prev(m)); lrelu(x_prev(m - 1))].
-    const int r = P.r, pp = P.p, Tin = Lh / r;
-    const int l16 = lane & 15, kg = lane >> 4;
-    float bup[8] = {};
-    if (wave == 5) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bup[4 * ct + e] = P.bup[16 * ct + 4 * kg + e];
-    }
-    // input-stage operands of tile j, loaded two steps ahead (buffer j & 1)
-    struct SIn {
-      float4 xv[2][2];    // x_prev rows m = mb + l16 - ks, channels 8 kg .. 8 kg + 7
-      float4 av[4];       // audio_down rows (!AUD): a[tt + n][8 i + 4 h ..]
-      float au;           // AUD/FIN: audio sample of tile j + 1, row n
-    };
-    auto s_load = [&](SIn& q, int j) {
-      if (wave != 5 || j >= NT) return;
-      const int tt = tg + 32 * j, mb = floordiv(tt + pp, r) - 1;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int m = min(max(mb + l16 - ks, 0), Tin - 1);
-        const float* xp = P.xin + ((long long)b * Tin + m) * CI + 8 * kg;
-        q.xv[ks][0] = *reinterpret_cast<const float4*>(xp);
-        q.xv[ks][1] = *reinterpret_cast<const float4*>(xp + 4);
-      }
-      if constexpr (AUD) {
-        q.au = P.audio[base + min(max(tt + 32 + n, 0), Lh - 1)];
-      } else {
-        const float* ap = P.a + (base + min(max(tt + n, 0), Lh - 1)) * CI + 4 * h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q.av[i] = *reinterpret_cast<const float4*>(ap + 8 * i);
-      }
-    };
-    SIn sq[2];
-    s_load(sq[0], 0);
-    s_load(sq[1], 1);
-    auto step = [&](int s, SIn& cur) {
-      LS_STAMP(s, 0);
-      // ---- P_l(j): y = lrelu(W . [u(t-d); u(t); u(t+d)] + b), rows outside the utterance zero
-      {
-        const int j = s - ql;
-        if (j >= 0 && j < NT) {
-          f32x16 acc, acc1;     // two accumulation chains (even / odd k-steps) halve the MFMA latency chain
-#pragma unroll
-          for (int q = 0; q < 16; ++q) { acc[q] = 0.f; acc1[q] = 0.f; }
-#pragma unroll
-          for (int kk = 0; kk < 6; ++kk) {
-            const int tap = kk >> 1;
-            const bf16x8 bu = *reinterpret_cast<const bf16x8*>(
-                Ul + ((32 * j + n + (tap - 1) * d) & (32 * NU - 1)) * LD + 16 * (kk & 1) + 8 * h);
-            if (kk & 1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc1, 0, 0, 0);
-            else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc, 0, 0, 0);
-          }
-          acc += acc1;
-          const int t = tg + 32 * j + n;
-          const bool in = t >= 0 && t < Lh;
-          f32x2 v[8];
-#pragma unroll
-          for (int p = 0; p < 8; ++p) {
-            const f32x2 y = lrelu2(f32x2{acc[2 * p], acc[2 * p + 1]} + bias[p]);
-            v[p] = in ? y : f32x2{0.f, 0.f};
-          }
-          bf16x8 y0, y1;
-#pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            y0[2 * p] = (__bf16)v[p].x; y0[2 * p + 1] = (__bf16)v[p].y;
-            y1[2 * p] = (__bf16)v[4 + p].x; y1[2 * p + 1] = (__bf16)v[4 + p].y;
-          }
-          __bf16* dst = Yl + pmod(32 * j + n, ym) * LD + 16 * h;
-          *reinterpret_cast<bf16x8*>(dst) = y0;
-          *reinterpret_cast<bf16x8*>(dst + 8) = y1;
-        }
-      }
-      LS_STAMP(s, 1);
-      // ---- S(j = s) (wave 5): x_0 = upsample(lrelu(x_prev)) -> x_0 ring; u_0 = lrelu(x_0 + a)
-      if (wave == 5 && s < NT) {
-        const int j = s, tt = tg + 32 * j;
-        if constexpr (AUD) {   // the audio samples of tile j + 1 (tile j's own were written last step)
-          if (lane < 32) {
-            const int t = tt + 32 + n;
-            FS[AU_OFF + ((32 * j + 32 + n) & (NAU - 1))] = (t >= 0 && t < Lh) ? cur.au : 0.f;
-          }
-        }
-        LS_STAMP(s, 3);
-        // input positions m of this tile: m in [mb, mb + 16), mb = floor((tt + p) / r) - 1
-        const int mb = floordiv(tt + pp, r) - 1;
-        bf16x8 xb[2];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {        // ks 0: x_prev(m), ks 1: x_prev(m - 1)
-          const int m = mb + l16 - ks;
-          const bool ok = m >= 0 && m < Tin;
-          const float e[8] = {cur.xv[ks][0].x, cur.xv[ks][0].y, cur.xv[ks][0].z, cur.xv[ks][0].w,
-                              cur.xv[ks][1].x, cur.xv[ks][1].y, cur.xv[ks][1].z, cur.xv[ks][1].w};
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const float u = ok ? e[q] : 0.f;
-            xb[ks][q] = (__bf16)(u >= 0.f ? u : 0.2f * u);
-          }
-        }
-        float* X0 = FS + X0_OFF;
-        // all r x 2 phase-tile products issued back to back (independent accumulators), then stored
-        typedef float f32x4_ __attribute__((ext_vector_type(4)));
-        f32x4_ pacc[RMAX][2];
-#pragma unroll
-        for (int k = 0; k < RMAX; ++k) {
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) {
-            pacc[k][ct] = f32x4_{0.f, 0.f, 0.f, 0.f};
-            if (k < r) {
-#pragma unroll
-              for (int ks = 0; ks < 2; ++ks) {
-                const bf16x8 wa = *reinterpret_cast<const bf16x8*>(
-                    BS + 2 * WU_OFF + (k * 32 + 16 * ct + l16) * WLD + 32 * ks + 8 * kg);
-                pacc[k][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xb[ks], pacc[k][ct], 0, 0, 0);
-              }
-            }
-          }
-        }
-        LS_STAMP(s, 4);
-        const int x0base = 32 * j - tt;
-#pragma unroll
-        for (int k = 0; k < RMAX; ++k) {
-          // C[co = 16 ct + 4 kg + e][m = mb + l16] -> time r m + k - p
-          const int row = r * (mb + l16) + k - pp - tt;
-          if (k < r && row >= 0 && row < 32) {
-            float* xrow = X0 + pmod(x0base + tt + row, 32 * NX0) * XLD + 4 * kg;
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-              *reinterpret_cast<float4*>(xrow + 16 * ct) =
-                  make_float4(pacc[k][ct][0] + bup[4 * ct], pacc[k][ct][1] + bup[4 * ct + 1],
-                              pacc[k][ct][2] + bup[4 * ct + 2], pacc[k][ct][3] + bup[4 * ct + 3]);
-          }
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's x_0 rows / audio are in LDS
-        __builtin_amdgcn_wave_barrier();
-        LS_STAMP(s, 5);
-        const int t = tt + n;
-        const bool in = t >= 0 && t < Lh;
-        f32x16 av;
-        if constexpr (AUD) {
-          av = audio_down(tt);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            av[4 * i] = in ? cur.av[i].x : 0.f; av[4 * i + 1] = in ? cur.av[i].y : 0.f;
-            av[4 * i + 2] = in ? cur.av[i].z : 0.f; av[4 * i + 3] = in ? cur.av[i].w : 0.f;
-          }
-        }
-        LS_STAMP(s, 7);
-        const float* xr = X0 + pmod(32 * j + n, 32 * NX0) * XLD + 4 * h;
-        f32x2 zz[8];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float4 v = *reinterpret_cast<const float4*>(xr + 8 * i);
-          zz[2 * i] = f32x2{v.x + av[4 * i], v.y + av[4 * i + 1]};
-          zz[2 * i + 1] = f32x2{v.z + av[4 * i + 2], v.w + av[4 * i + 3]};
-        }
-        store_u(BS + U_OFF + ((32 * j + n) & (32 * NU - 1)) * LD, zz, in);
-      }
-      LS_STAMP(s, 2);
-      s_load(cur, s + 2);
-      // ---- F(j) (wave 7): eps = final_conv(x_4), audio_out = (x_t - ce eps) / den + sig z
-      if constexpr (FIN) {
-        const int j = s - LAG_F;
-        if (wave == 7 && j >= 0 && j < NT) {
-          const int sm = lane >> 1, c0 = (lane & 1) * 16, t = tg + 32 * j + sm;
-          const float* X4 = FS + X4_OFF;
-          f32x2 ea[4] = {};     // independent accumulators: the LDS reads pipeline under the FMAs
-#pragma unroll
-          for (int tap = 0; tap < 7; ++tap) {
-            const float* xrow = X4 + ((32 * j + sm + tap - 3) & (32 * NX4 - 1)) * XLD + c0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float4 v = *reinterpret_cast<const float4*>(xrow + 4 * q);
-              const float4 w4 = *reinterpret_cast<const float4*>(&FWF[tap * 32 + c0 + 4 * q]);
-              ea[q] = __builtin_elementwise_fma(f32x2{w4.x, w4.y}, f32x2{v.x, v.y}, ea[q]);
-              ea[q] = __builtin_elementwise_fma(f32x2{w4.z, w4.w}, f32x2{v.z, v.w}, ea[q]);
-            }
-          }
-          const f32x2 e2 = (ea[0] + ea[1]) + (ea[2] + ea[3]);
-          float e = e2.x + e2.y;
-          e += __shfl_xor(e, 1);
-          if ((lane & 1) == 0 && t >= R0 && t < R1) {
-            e += P.bfin[0];
-            float v = (FS[AU_OFF + ((32 * j + sm) & (NAU - 1))] - P.ce * e) / P.den;
-            if (P.sig != 0.f)
-              v += P.sig * (P.noise ? P.noise[base + t]
-                                    : philox_normal_u(P.seed, utt_id(P.uid, b + P.b_off), (unsigned)t, P.stream));
-            P.audio_out[base + t] = v;
-          }
-        }
-      }
-      LS_STAMP(s, 6);
-      __syncthreads();
-    };
-    for (int s = 0; s < NSTEP; s += 2) {
-      step(s, sq[0]);
-      if (s + 1 < NSTEP) step(s + 1, sq[1]);
-    }
-  }
-}
-
-// Rows per workgroup: one wave of about 256 workgroups over the chip (one per CU), whole
-// tiles, at least 16 tiles so the 4 halo tiles and the 21-step pipeline fill stay small.
-int lvc_stream_seg(int Lh, int B) {
-  const long long rows = (long long)Lh * B;
-  int seg = (int)((rows + 256LL * 32 - 1) / (256LL * 32)) * 32;
-  return seg < 512 ? 512 : seg;
-}
-
 // ------------------------------------------------------------------ DiffusionDBlock (bf16)
 // modules.py:131-138 in one launch:
 //   xs = x[f i];  h1 = lrelu(conv_d1(lrelu(xs)));  h2 = lrelu(conv_d2(h1));
@@ -2943,8 +1874,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf);
       // FD_OPT_KP_CHUNK: kernel predictor + LVC block per chunk of utterances, so a chunk's
       // kernel tensor can still be on-die (Infinity Cache) when the LVC block reads it
-      const bool stream_path = m->lvc_stream && ups && hop % 32 == 0 && r >= 4 && (last && aud ? r <= 4 : r <= 8);
-      const int cb = (!side && !stream_path && m->kp_chunk > 0 && m->kp_chunk < B) ? m->kp_chunk : B;
+      const int cb = (!side && m->kp_chunk > 0 && m->kp_chunk < B) ? m->kp_chunk : B;
       for (int b0 = 0; b0 < B; b0 += cb) {
       const int nbk = B - b0 < cb ? B - b0 : cb;
       const int rows = nbk * Tc;
@@ -2975,36 +1905,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         la.ce = fin->ce; la.den = fin->den;
         la.sig = fin->sig; la.seed = fin->seed; la.stream = fin->stream; la.uid = fin->uid;
       }
-      // (the LDS image holds upsample weights for r <= 4 with the audio fusions, r <= 8 without)
-      const bool skew_path = !stream_path && m->lvc_skew && ups && hop >= 64 && (hop & (hop - 1)) == 0 &&
-                             (r == 4 || r == 8);
-      if (skew_path) {
-        ProfScope ps(fuse_fin ? "fd_lvc_block_final" : "fd_lvc_block_ups", st);
-        int nseg = 1, seg_tiles = 1;
-        lvc_skew_segments((int)(Tout / 32), nbk, m->ncu, m->lvc_seg, &nseg, &seg_tiles);
-        const dim3 grid(nbk * nseg);
-        if (last && aud && fuse_fin)
-          hipLaunchKernelGGL((lvc_skew_bf16_kernel<true, true>), grid, dim3(lsw::NTH), 0, st, la, nseg, seg_tiles);
-        else if (last && aud)
-          hipLaunchKernelGGL((lvc_skew_bf16_kernel<true, false>), grid, dim3(lsw::NTH), 0, st, la, nseg, seg_tiles);
-        else
-          hipLaunchKernelGGL((lvc_skew_bf16_kernel<false, false>), grid, dim3(lsw::NTH), 0, st, la, nseg, seg_tiles);
-        PD_LAUNCH_CHECK();
-      } else if (stream_path) {
-        // streaming pipeline: one long time range per workgroup (lvc_stream_bf16_kernel)
-        ProfScope ps(fuse_fin ? "fd_lvc_block_final" : "fd_lvc_block_ups", st);
-        const int Lh = (int)Tout, seg = lvc_stream_seg(Lh, nbk);
-        const dim3 grid(cdiv(Lh, seg), nbk);
-        if (last && aud && fuse_fin)
-          hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, true, 4>), grid, dim3(512), 0, st, la, seg);
-        else if (last && aud)
-          hipLaunchKernelGGL((lvc_stream_bf16_kernel<true, false, 4>), grid, dim3(512), 0, st, la, seg);
-        else if (r <= 4)
-          hipLaunchKernelGGL((lvc_stream_bf16_kernel<false, false, 4>), grid, dim3(512), 0, st, la, seg);
-        else
-          hipLaunchKernelGGL((lvc_stream_bf16_kernel<false, false, 8>), grid, dim3(512), 0, st, la, seg);
-        PD_LAUNCH_CHECK();
-      } else {
+      {
         ProfScope ps(fuse_fin ? "fd_lvc_block_final" : hop < 32 ? "fd_lvc_block_sub" : ups ? "fd_lvc_block_ups"
                                                                                    : "fd_lvc_block", st);
         const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
@@ -3098,12 +1999,6 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   PD_CHECK_ARG(dims->num_blocks >= 1 && dims->num_blocks <= 4, "num_blocks in [1,4]");
   hipStream_t st = (hipStream_t)stream;
   fd_model* m = new fd_model();
-  {
-    int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
-      m->ncu = ncu;
-  }
   m->nblocks = dims->num_blocks;
   m->dtype = dtype;
   int hop = 1;
@@ -3273,15 +2168,9 @@ int fd_set_option(fd_model* m, int option, int value) {
     case FD_OPT_LVC_PF: m->lvc_pf = value != 0; return PD_OK;
     case FD_OPT_LVC_SUB: m->lvc_sub = value != 0; return PD_OK;
     case FD_OPT_KP_SIDE: m->kp_side = value != 0; return PD_OK;
-    case FD_OPT_LVC_STREAM: m->lvc_stream = value != 0; return PD_OK;
     case FD_OPT_KP_CHUNK:
       PD_CHECK_ARG(value >= 0, "FD_OPT_KP_CHUNK >= 0");
       m->kp_chunk = value;
-      return PD_OK;
-    case FD_OPT_LVC_SKEW: m->lvc_skew = value != 0; return PD_OK;
-    case FD_OPT_LVC_SEG:
-      PD_CHECK_ARG(value >= 0, "FD_OPT_LVC_SEG >= 0");
-      m->lvc_seg = value;
       return PD_OK;
     default: break;
   }

@@ -92,27 +92,17 @@ def test_fastdiff_sample_bf16(fd16):
 
 
 def _lvc_opts(ts):
-    """FD options selecting one LVC-block implementation: "skew" = the skewed persistent
-    kernel (FD_OPT_LVC_SKEW), "skew8" = the same with 8-tile segments (many workgroups
-    per utterance), "stream" = the streaming pipeline kernel, an int = the whole-block kernel
-    with that tile (0 = one fused launch per layer)."""
-    if ts == "skew":
-        return dict(lvc_skew=1, lvc_stream=0)
-    if ts == "skew8":
-        return dict(lvc_skew=1, lvc_stream=0, lvc_seg=8)
-    if ts == "stream":
-        return dict(lvc_stream=1, lvc_skew=0)
-    return dict(lvc_ts=ts, lvc_stream=0, lvc_skew=0)
+    """FD options selecting one LVC-block implementation: the whole-block kernel with tile
+    `ts` (0 = one fused launch per layer)."""
+    return dict(lvc_ts=ts)
 
 
-@pytest.mark.parametrize("ts", ["skew", "skew8", "stream", 0, 128, 256, 384])
+@pytest.mark.parametrize("ts", [0, 128, 256, 384])
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9), (1, 40)])
 def test_fastdiff_lvc_block_bf16(ts, B, Tc):
     """LVC modes against the oracle, including utterances shorter than one block and the
-    grid/halo edges: the skewed persistent kernel (FD_OPT_LVC_SKEW; "skew8" cuts
-    every utterance into 8-tile segments, so segment halos and the staircase fill run at
-    every boundary), the streaming pipeline kernel (FD_OPT_LVC_STREAM) and the whole-block
-    kernel (FD_OPT_LVC_TS: 0 = one fused launch per layer, 128/256/384 = whole block)."""
+    grid/halo edges: the whole-block kernel (FD_OPT_LVC_TS: 0 = one fused launch per layer,
+    128/256/384 = whole block)."""
     p = G.fastdiff_params(31)
     m = FastDiff()
     m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
@@ -126,8 +116,7 @@ def test_fastdiff_lvc_block_bf16(ts, B, Tc):
                       f"lvc_block ts={ts} B={B} Tc={Tc}", EPS_REL_L2, EPS_REL_MAX)
 
 
-@pytest.mark.parametrize("fuse,ts", [(0, 128), (0, 256), (0, 384), (1, 128), (1, 256), (1, 384), (1, "stream"),
-                                     (1, "skew"), (1, "skew8")])
+@pytest.mark.parametrize("fuse,ts", [(0, 128), (0, 256), (0, 384), (1, 128), (1, 256), (1, 384)])
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
 def test_fastdiff_sample_bf16_oracle(fuse, ts, B, Tc):
     """The 4-step sampler with the upsample / first conv / final update fused into the LVC
@@ -217,36 +206,3 @@ def test_wavenet_two_kernel_vs_fused(cyc):
     print(f"BF16ERR two-kernel vs fused WaveNet cyc={cyc} B={B}x{T} rel-L2={rel:.3e}")
     assert np.isfinite(a).all() and rel <= 2e-3
 
-
-@pytest.mark.parametrize("seg", [0, 8, 13, 40])
-@pytest.mark.parametrize("B,Tc", [(2, 40), (3, 7)])
-def test_lvc_skew_vs_block(seg, B, Tc):
-    """The skewed persistent LVC kernel against the whole-block kernel (FD_OPT_LVC_SKEW 1 vs 0)
-    on the same inputs and on-device Philox draws.  Both round the same bf16 operands; the
-    fp32 orders differ slightly (the skewed kernel seeds the LVC accumulators with the bias,
-    as the whole-block kernel's prefetch variant does but not its fd_forward variant, and sums
-    the fused final conv per row), and a 1-ulp fp32 difference can flip a bf16 rounding of
-    the next operand, so the bar is rel-L2 <= 5e-3 (bf16 flips, not systematic error; the
-    oracle tests above hold both kernels to the bf16 bar).  seg (FD_OPT_LVC_SEG) sets the
-    segment length in 32-row tiles: 0 = one workgroup per CU, 8 / 13 / 40 put segment
-    boundaries (halo + staircase fill) inside utterances and frames."""
-    from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
-    p = G.fastdiff_params(31)
-    audio = synth.synth_inputs(90 + B, (B, 1, Tc * 256))
-    c = synth.synth_inputs(91 + B, (B, 80, Tc), loc=-5.0, scale=2.0)
-    st = np.full((B, 1), 74.9923, np.float32)
-    bb, a, s, stp = fastdiff_infer_params(fastdiff_reverse_schedule(4), fastdiff_train_alpha())
-    mel = np.ascontiguousarray(np.transpose(c, (0, 2, 1)))
-    outs = {}
-    for skew in (0, 1):
-        m = FastDiff()
-        m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
-        m = m.to(DEV).set_compute_dtype("bf16").set_options(lvc_skew=skew, lvc_seg=seg)
-        eps = m((tt(audio), tt(c), tt(st))).cpu().numpy()
-        wav = m.sample(tt(mel), bb, a, s, stp, seed=4321).cpu().numpy()
-        outs[skew] = (eps, wav)
-    for k, name in ((0, "eps"), (1, "sampler")):
-        a1, a0 = outs[1][k], outs[0][k]
-        rel = float(np.linalg.norm(a1 - a0) / np.linalg.norm(a0))
-        print(f"BF16ERR skew vs block {name} seg={seg} B={B} Tc={Tc} rel-L2={rel:.3e}")
-        assert np.isfinite(a1).all() and rel <= 5e-3
