@@ -159,7 +159,8 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
 TAG_KERNEL = {
     "fd_lvc_block_final": ("lvc_block_bf16_kernel<384, true, true, true, true, false>",),
     "fd_lvc_block_ups": ("lvc_block_bf16_kernel<384, true, false, false, true, false>",),
-    "fd_lvc_block_sub": ("lvc_block_bf16_kernel<128, true, false, false, false, true>",),
+    "fd_lvc_block_sub": ("lvc_block_bf16_kernel<256, true, false, false, false, true>",
+                         "lvc_block_bf16_kernel<128, true, false, false, false, true>"),
     "fd_kp_kernel": ("kp_kernel_bf16_kernel",),
     "wn_layer": ("wn_layer_bf16_kernel",),
     "wn_gate2": ("wn_gate_bf16_kernel",),

@@ -199,7 +199,7 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
  * the measured production configuration; the tests select each variant.
  * Set them before the handle's first forward/sample call; not thread-safe against calls. */
 #define FD_OPT_LVC_TS 0       /* whole-block LVC tile, hop >= 32: 384 (default), 256, 128; 0 = per-layer launches */
-#define FD_OPT_LVC_TS_SUB 1   /* whole-block LVC tile of the hop < 32 block: 128 (default), 256, 384 */
+#define FD_OPT_LVC_TS_SUB 1   /* whole-block LVC tile of the hop < 32 block: 256 (default), 128, 384 */
 #define FD_OPT_LVC_FUSE 2     /* 1: upsample / first conv / sampler update fused into the LVC blocks */
 #define FD_OPT_LVC_PF 3       /* 1: next-layer kernel fragments prefetched into registers (tile 384) */
 #define FD_OPT_LVC_SUB 4      /* 1: the hop < 32 block on the whole-block kernel too */

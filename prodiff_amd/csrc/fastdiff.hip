@@ -58,7 +58,7 @@ struct fd_model {
   // fused launch per layer.  Every field below is an fd_set_option (FD_OPT_*) with these
   // measured defaults; the tests use the options to cover each variant.
   int lvc_ts = 384;
-  int lvc_ts_sub = 128;
+  int lvc_ts_sub = 256;        // hop < 32 (hop-8) block tile: r03 A/B with plain K stores 105 vs 112 us (128), 121 (384)
   bool lvc_fuse = true;        // upsample / first conv / final update fused into the LVC block (FD_OPT_LVC_FUSE)
   bool lvc_pf = true;          // next-layer kernel fragments prefetched into registers (FD_OPT_LVC_PF)
   bool lvc_sub = true;         // hop < 32 blocks (hop 8) on the whole-block kernel too (FD_OPT_LVC_SUB)

@@ -97,6 +97,23 @@ def _lvc_opts(ts):
     return dict(lvc_ts=ts)
 
 
+@pytest.mark.parametrize("ts_sub", [128, 384])
+@pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
+def test_fastdiff_lvc_sub_tiles_bf16(ts_sub, B, Tc):
+    """The hop-8 block's non-default tiles (FD_OPT_LVC_TS_SUB; 256 is the default, covered by
+    every other FastDiff test) against the oracle."""
+    p = G.fastdiff_params(31)
+    m = FastDiff()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+    m = m.to(DEV).set_compute_dtype("bf16").set_options(lvc_ts_sub=ts_sub)
+    audio = synth.synth_inputs(5 * B + Tc, (B, 1, Tc * 256))
+    c = synth.synth_inputs(5 * B + Tc + 1, (B, 80, Tc), loc=-5.0, scale=2.0)
+    st = np.full((B, 1), 23.47, np.float32)
+    eps = m((tt(audio), tt(c), tt(st))).cpu().numpy()
+    assert_bf16_close(eps, OF.fastdiff_forward(OF.fold_weight_norm(p), audio, c, st),
+                      f"lvc_sub ts={ts_sub} B={B} Tc={Tc}", EPS_REL_L2, EPS_REL_MAX)
+
+
 @pytest.mark.parametrize("ts", [0, 128, 256, 384])
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9), (1, 40)])
 def test_fastdiff_lvc_block_bf16(ts, B, Tc):
