@@ -192,6 +192,9 @@ def test_bench_traffic_keyed_by_workload(tmp_path):
     # legacy (pre-r03) summaries are C3 8 x 861 unless named *c5*
     assert bench.traffic_workload({}, "profiles/r02_v4_traffic.json") == ("C3", 8, 861)
     assert bench.traffic_workload({}, "profiles/r02_v4c5_traffic.json") == ("C5", 8, 861)
-    # the committed summaries never serve a C4 line
-    for tag in bench.TAG_KERNEL:
-        assert bench.pmc_traffic(tag, "C4", 32, 861) == (None, None)
+    # a C4 line reads only a C4 summary (profiles/r03_v4c4_traffic.json), never a C3 figure
+    c3 = bench.pmc_traffic("fd_lvc_block_final", "C3", 8, 861)
+    c4 = bench.pmc_traffic("fd_lvc_block_final", "C4", 32, 861)
+    if c4[0] is not None:
+        assert "c4" in c4[1] and c4[0] > 3 * c3[0]
+    assert bench.pmc_traffic("fd_lvc_block_final", "C4", 16, 861) == (None, None)
