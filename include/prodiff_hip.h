@@ -92,6 +92,9 @@ void pd_wavenet_destroy(pd_wavenet* h);
 /* PD_WN_OPT_KSPLIT (fp32 path): the residual-layer GEMMs split their K range over several blocks
  * until the grid holds 512 (default) or 256 blocks; 0 = never split. */
 #define PD_WN_OPT_KSPLIT 1
+/* PD_WN_OPT_L2PF (bf16 fused layer): 1 (default) each layer launch pulls the next layer's weight
+ * fragments into every XCD's L2 while it runs; 0 = off. */
+#define PD_WN_OPT_L2PF 2
 int pd_wavenet_set_option(pd_wavenet* h, int option, int value);
 /* S = number of reverse steps the workspace must serve (1 for pd_wavenet_forward). */
 size_t pd_wavenet_workspace_size(const pd_wavenet* h, int B, int T, int S);

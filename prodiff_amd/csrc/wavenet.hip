@@ -35,6 +35,7 @@ struct pd_wavenet {
   // frames per block; 1 = GATE + RESSKIP kernels; 2 = auto between 0 and 3 by grid size
   int layer_mode = 2;
   int ksplit_blocks = 512;   // PD_WN_OPT_KSPLIT: fp32 layer GEMMs split K up to this many blocks
+  int l2_prefetch = 1;       // PD_WN_OPT_L2PF: fused layer l pulls layer l + 1's weights into L2
 };
 
 namespace {
@@ -72,6 +73,8 @@ struct WnLayerArgs {
   const __bf16* W2f;      // [2C/32][C/16][64][8]
   const float* b2;        // [2C]
   int B, T, H, dil, first;
+  const __bf16* pfw[2];   // the next layer's W1 and W2 fragments (never null), pulled into each
+  int pf_lines[2];        //   XCD's L2 line by line: pf_lines 128-B lines each
 #ifdef WN_TRACE
   unsigned long long* trace;   // tools/wn_probe.hip: per-phase s_memtime stamps
 #endif
@@ -115,6 +118,27 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)wave * KS2 * 64 + lane;
   const bf16x8* wsk = reinterpret_cast<const bf16x8*>(P.W2f) + (long long)(8 + wave) * KS2 * 64 + lane;
   bf16x8 rg[WD], rf[WD];
+  // The next layer's 1.3 MB of weights into this XCD's L2 while this layer runs (blocks are dealt
+  // round-robin over the 8 XCDs; the blocks of one XCD split its lines): otherwise every layer
+  // starts by fetching them from memory into 8 cold L2s (tools/wn_probe.hip: 22.5 us per launch
+  // with warm weights, 25.6 cold).  One dword per 128-B line, issued in GEMM2 after its last
+  // weight load (vmcnt is in order: an L2-hit load issued after an HBM-miss prefetch would wait
+  // for it); the values are consumed (never stored) at the very end.  A fixed count per thread
+  // (2 per range, clamped addresses, no loop, no branch -- the host always passes ranges): after
+  // a loop of loads the waitcnt pass cannot count what is in flight and waits for all of it, the
+  // GEMM2 ring included (measured: GEMM2 +30%).  2 x 512 lines per block cover the 10240 lines
+  // at >= 10 blocks per XCD (C3: 27).
+  unsigned pfr[4];
+  auto l2_prefetch = [&]() {
+    const int xcd = blockIdx.x & 7, nslot = ((int)gridDim.x - xcd + 7) >> 3, slot = blockIdx.x >> 3;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ln = min(slot * 512 + tid + i * nslot * 512, P.pf_lines[r] - 1);
+        pfr[2 * r + i] = *reinterpret_cast<const unsigned*>(reinterpret_cast<const char*>(P.pfw[r]) + (long long)ln * 128);
+      }
+  };
   // stage [x(t-d)+dp; x(t)+dp; x(t+d)+dp; cond] as bf16 (zero outside each row's utterance).
   // Thread tid always owns column group g = 4 (tid % 256) (so its tap/channel is fixed)
   // and rows tid/256 + 2 it; all 16 loads of a 32-row half are issued before any is used
@@ -251,6 +275,7 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
       r2a[ks % WD2] = wr[(ks + WD2) * 64];
       r2b[ks % WD2] = wsk[(ks + WD2) * 64];
     }
+    if (ks == KS2 - WD2 - 1) l2_prefetch();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < RT; ++q) {
@@ -274,6 +299,8 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
         P.skip[o] = sv + as_[q][reg] + bsv;
       }
     }
+  if ((pfr[0] ^ pfr[1] ^ pfr[2] ^ pfr[3]) == 0x9E3779B9u && P.pf_lines[0] < 0)   // never true: keeps
+    P.xout[0] = 0.f;                                                               // the prefetch loads
   WN_STAMP(7);
 }
 
@@ -747,6 +774,12 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       P.W1f = h->W1f + (size_t)l * 2 * C * (3 * C + H); P.b1 = h->bl1 + (size_t)l * 2 * C;
       P.W2f = h->W2f + (size_t)l * 2 * C * C; P.b2 = h->bl2 + (size_t)l * 2 * C;
       P.B = B; P.T = T; P.H = H; P.dil = 1 << (l % h->cyc); P.first = (l == 0);
+      // the next layer's weights (the last layer, or prefetch off: this layer's, already on-die)
+      const int lp = l + 1 < Ly && h->l2_prefetch ? l + 1 : l;
+      P.pfw[0] = h->W1f + (size_t)lp * 2 * C * (3 * C + H);
+      P.pfw[1] = h->W2f + (size_t)lp * 2 * C * C;
+      P.pf_lines[0] = (int)((size_t)2 * C * (3 * C + H) * 2 / 128);
+      P.pf_lines[1] = (int)((size_t)2 * C * C * 2 / 128);
       ProfScope ps("wn_layer", st);
       // auto: 64-frame blocks once they still fill every CU (r02: B=32 x 861 frames 73 vs 88 us per
       // layer), else 32-frame blocks (B=8: 108 blocks of 64 frames leave half the chip idle, 37 vs 27 us)
@@ -925,6 +958,11 @@ int pd_wavenet_set_option(pd_wavenet* h, int option, int value) {
   if (option == PD_WN_OPT_KSPLIT) {
     PD_CHECK_ARG(value == 0 || value == 256 || value == 512, "PD_WN_OPT_KSPLIT is 0 (no split), 256 or 512");
     h->ksplit_blocks = value == 0 ? 1 : value;
+    return PD_OK;
+  }
+  if (option == PD_WN_OPT_L2PF) {
+    PD_CHECK_ARG(value == 0 || value == 1, "PD_WN_OPT_L2PF is 0 or 1");
+    h->l2_prefetch = value;
     return PD_OK;
   }
   set_error("pd_wavenet_set_option: unknown option " + std::to_string(option));
