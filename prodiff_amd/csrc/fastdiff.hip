@@ -456,8 +456,12 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
     bx = logical - b * gridDim.x;
   }
   // Tiles of wave w: PF -- the adjacent pair 2w, 2w + 1 (one frame, one shared kernel);
-  // otherwise w and w + NW (better balanced over the shrinking per-layer tile ranges).
-#define TILE(j) (PF ? 2 * wave + (j) : wave + (j) * NW)
+  // otherwise w and w + NW (better balanced over the shrinking per-layer tile ranges), the
+  // upper half first in odd time tiles: a block's last 4 grid tiles are the next block's
+  // first 4 (the 2 x 64-row halo), so both read those frames' kernels in the same pass and
+  // the second read can hit L2 (hop 8: the halo re-reads were a third of the launch's bytes).
+  const int jsw = !PF && (bx & 1);
+#define TILE(j) (PF ? 2 * wave + (j) : wave + ((j) ^ jsw) * NW)
   const int Tc = P.Tc, hop = P.hop;
   const int Lh = Tc * hop;                           // utterance-local times fit in 32 bits
   const int t0 = bx * TS, tg = t0 - 64;              // time of grid row 0
