@@ -348,7 +348,13 @@ __device__ __forceinline__ void stage_window(const void* __restrict__ in, int b,
 // weight-fragment prefetch depth (k-steps).  Measured (r02, C5 B=8): ring 4 without a
 // sched_barrier 386 us for the 128-channel k=11 conv; pinning the ring with sched_barrier
 // raised VGPRs to 2 waves/SIMD and ran slower (459 us at depth 4, 486 us at depth 8).
-constexpr int NSF_PF = 4;
+#ifndef NSF_PF_DEPTH
+#define NSF_PF_DEPTH 4
+#endif
+#ifndef NSF_RING_PIN
+#define NSF_RING_PIN 0
+#endif
+constexpr int NSF_PF = NSF_PF_DEPTH;
 
 template <int C, int FM, int FN, int WM, int WN, bool IN_BF, bool OUT_BF>
 __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
@@ -402,6 +408,9 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
     for (int q = 0; q < PF; ++q) {
       const int s = s0 + q;
       bload(min(s + PF - 1, S - 1), bq[(q + PF - 1) % PF]);
+#if NSF_RING_PIN
+      __builtin_amdgcn_sched_barrier(0);   // keep the load PF - 1 steps ahead of its use
+#endif
       const int tap = s / KS, kc = s - tap * KS;
       bf16x8 af[FM];
 #pragma unroll

@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B the bench under several env settings (one line each), e.g.
 #   tools/ab_bench.sh <tag> "" "PRODIFF_LVC_PF=1" "PRODIFF_LVC_TS=256"
-# Optional: AB_TESTS=<pytest -k expr> runs those bf16 tests under every setting first.
+# Optional: AB_TESTS=<pytest -k expr> runs those bf16 tests under every setting first;
+# BENCH_ARGS=<extra bench.py arguments> (e.g. "--config C5").
 set -e
 TAG=$1; shift
 R=$GRAFT_REPO_ROOT
@@ -16,7 +17,7 @@ for envs in "$@"; do
       --timeout-method thread -k "$AB_TESTS" > $O/tests_$i.log 2>&1
     echo "[$envs] $(tail -1 $O/tests_$i.log)"
   fi
-  env $envs timeout -k 10 300 python -u bench.py --cpu-frames 0 > $O/bench_$i.json 2> $O/bench_$i.err
+  env $envs timeout -k 10 300 python -u bench.py --cpu-frames 0 $BENCH_ARGS > $O/bench_$i.json 2> $O/bench_$i.err
   python - "$envs" $O/bench_$i.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
