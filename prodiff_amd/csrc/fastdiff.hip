@@ -1220,6 +1220,20 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   __bf16* hout = A.hout + (long long)z * A.B * Tc * HK;
   float* Bfo = A.Bf + (long long)z * A.B * Tc * (2 * CI * NLY);
 
+  // Stage 0's weight fragments (30 k-steps; both of a wave's jobs use column tile wave & 1)
+  // run through a KH0-deep register ring, primed here so the first ones land with the
+  // staging loads: a load right before each MFMA made stage 0 thirty L2 round trips per job.
+  constexpr int KH0 = 10;
+  const __bf16* wrow0 = A.Win[nblk] + ((wave & 1) * 32 + r32) * 480 + h * 8;
+  bf16x8 w0r[KH0];
+#pragma unroll
+  for (int s = 0; s < KH0; ++s) w0r[s] = *reinterpret_cast<const bf16x8*>(wrow0 + s * 16);
+  bf16x8 bwn[12];   // stage 1's fragments (stages 1..6 below), in flight from here on
+  {
+    const __bf16* wrow = A.Wr[nblk][0] + ((wave & 1) * 32 + r32) * 192 + h * 8;
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk) bwn[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
+  }
   // c' = c + fc_t(e) on frames f0-18 .. f0+81 (channels 80..95 zero).  All loads are issued
   // before any is used (clamped addresses, masked at the store): one round trip, not ten.
   constexpr int NCI = (100 * 24 + 255) / 256;
@@ -1251,20 +1265,27 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   __syncthreads();
 
   float keep[2][16];   // h0 in fp32 for the residual add (same job->wave map in every stage)
-  // stage 0: h0 = lrelu(conv5(c')) ; jobs = 3 row tiles x 2 column tiles
-  for (int job = wave, q = 0; job < 6; job += 4, ++q) {
-    const int mt = job >> 1, nt = job & 1;
+  // stage 0: h0 = lrelu(conv5(c')) ; jobs = 3 row tiles x 2 column tiles.  Waves 2 and 3 have
+  // one job: their second pass runs on a clamped tile and is dropped (they would wait at the
+  // barrier anyway), so the ring's step index stays static.
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int job = wave + 4 * q;
+    const int mt = min(job >> 1, 2), nt = job & 1;
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const __bf16* wrow = A.Win[nblk] + (nt * 32 + r32) * 480 + h * 8;
 #pragma unroll
     for (int kk = 0; kk < 30; ++kk) {
+      const int st = q * 30 + kk;
+      const bf16x8 bw = w0r[st % KH0];
+      if (st + KH0 < 60) w0r[st % KH0] = *reinterpret_cast<const bf16x8*>(wrow0 + ((st + KH0) % 30) * 16);
+      __builtin_amdgcn_sched_barrier(0);   // keep the load KH0 steps ahead (hipcc sinks loads to their use)
       const int tap = kk / 6, kc = kk - tap * 6;
       const bf16x8 af = *reinterpret_cast<const bf16x8*>(Cs + (mt * 32 + r32 + tap) * LDC + kc * 16 + h * 8);
-      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bw, acc, 0, 0, 0);
     }
+    if (job >= 6) continue;
     const int n = nt * 32 + r32;
     const float bias = A.bin[nblk][n];
 #pragma unroll
@@ -1282,12 +1303,6 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   // A wave's jobs (wave, wave + 4) share the column tile nt = wave & 1: its 12 weight fragments
   // are loaded once per stage and reused by both jobs; stage j + 1's fragments are loaded while
   // stage j computes (no L2 round trip at a stage start).
-  bf16x8 bwn[12];
-  {
-    const __bf16* wrow = A.Wr[nblk][0] + ((wave & 1) * 32 + r32) * 192 + h * 8;
-#pragma unroll
-    for (int kk = 0; kk < 12; ++kk) bwn[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
-  }
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     const __bf16* In = Hb[j == 0 ? 0 : (j & 1 ? 1 : 2)];
