@@ -1091,9 +1091,10 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   for (int u = 0; u < DB_NI; ++u) {
     const int i = tid + 256 * u;
     const int p = i >> 3, q = (i & 7) * 4, ii = ib + p;
+    const bool ok = i < DB_ROWS * 8 && p < DB_TS + 14 && ii >= 0 && ii < Lout;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < DB_ROWS * 8 && p < DB_TS + 14 && ii >= 0 && ii < Lout) {
-      if (audio) {
+    if (audio) {
+      if (ok) {
         float o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = fbq[e];
@@ -1104,9 +1105,13 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
           for (int e = 0; e < 4; ++e) o[e] = fmaf(fq[k][e], a, o[e]);
         }
         v = make_float4(o[0], o[1], o[2], o[3]);
-      } else {
-        v = *reinterpret_cast<const float4*>(src + (long long)ii * f * CI + q);
       }
+    } else {
+      // unconditional load at a clamped row, masked per component: a load under the range
+      // branch made the staging one round trip per item (late r03 asm: 5 in a row)
+      const int iic = ii < 0 ? 0 : ii >= Lout ? Lout - 1 : ii;
+      const float4 x = *reinterpret_cast<const float4*>(src + (long long)iic * f * CI + q);
+      v.x = ok ? x.x : 0.f; v.y = ok ? x.y : 0.f; v.z = ok ? x.z : 0.f; v.w = ok ? x.w : 0.f;
     }
     sv[u] = v;
   }
