@@ -434,10 +434,12 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   // block's frames (pre-scaled for the gate) live in LDS, so no global load but the
   // next layer's kernel prefetch is in flight across a layer (vmcnt retires in order:
   // a global weight load behind the prefetch would wait for the whole prefetch).
-  constexpr bool WL = PF;
+  // SUB (hop 8) stages the pre-conv weights too (WW): a global load per layer made every layer
+  // start with an L2 round trip; its LVC biases stay per-frame global reads.
+  constexpr bool WL = PF, WW = PF || SUB;
   constexpr int BFR = WL ? GR / 32 + 2 : 1;          // frames a block touches at hop >= 32
-  __shared__ __attribute__((aligned(16))) bf16x8 WCL[WL ? NLY * 6 * 64 : 1];
-  __shared__ __attribute__((aligned(16))) float BCL[WL ? NLY * CI : 4];
+  __shared__ __attribute__((aligned(16))) bf16x8 WCL[WW ? NLY * 6 * 64 : 1];
+  __shared__ __attribute__((aligned(16))) float BCL[WW ? NLY * CI : 4];
   __shared__ __attribute__((aligned(16))) float BFL[WL ? BFR * 2 * CI * NLY : 4];
   __bf16* U = reinterpret_cast<__bf16*>(smem);
   __bf16* Y = U + G::UROWS * LB_LD;
@@ -492,12 +494,12 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   if constexpr (FIN) {
     if (tid < 224) wfv = P.wfin[tid];                        // already [tap][c]
   }
-  constexpr int IW = WL ? (6 * 64 + G::NT - 1) / G::NT : 1;
+  constexpr int IW = WW ? (6 * 64 + G::NT - 1) / G::NT : 1;
   constexpr int N4 = BFR * 2 * CI * NLY / 4, IB = WL ? (N4 + G::NT - 1) / G::NT : 1;
   bf16x4 wv[IW][NLY][2];
   float bcv = 0.f;
   float4 bfv[IB];
-  if constexpr (WL) {
+  if constexpr (WW) {
 #pragma unroll
     for (int it = 0; it < IW; ++it) {
       const int i = min(tid + it * G::NT, 6 * 64 - 1), kk = i >> 6, ln = i & 63;
@@ -513,6 +515,8 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
       for (int l = 0; l < NLY; ++l)
         if (tid / CI == l) bcv = P.bc[l][tid % CI];
     }
+  }
+  if constexpr (WL) {
 #pragma unroll
     for (int it = 0; it < IB; ++it) {
       const int i = min(tid + it * G::NT, N4 - 1), fr = min(fbase + i / (2 * CI * NLY / 4), Tc - 1);
@@ -599,7 +603,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   if constexpr (FIN) {
     if (tid < 224) FWF[tid] = wfv;
   }
-  if constexpr (WL) {
+  if constexpr (WW) {
 #pragma unroll
     for (int it = 0; it < IW; ++it) {
       const int i = tid + it * G::NT;
@@ -610,6 +614,8 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
       }
     }
     if (tid < NLY * CI) BCL[tid] = bcv;
+  }
+  if constexpr (WL) {
 #pragma unroll
     for (int it = 0; it < IB; ++it) {
       const int i = tid + it * G::NT, c = (i % (2 * CI * NLY / 4)) * 4;
@@ -755,7 +761,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
       bf16x8 wf[6];
 #pragma unroll
       for (int kk = 0; kk < 6; ++kk) {
-        if constexpr (WL) {
+        if constexpr (WW) {
           wf[kk] = WCL[(l * 6 + kk) * 64 + lane];
         } else {
           const __bf16* w = P.Wc[l] + n * 96 + (kk >> 1) * 32 + 16 * h + 4 * (kk & 1);
@@ -766,7 +772,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
       f32x2 bias[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float4 bv = *reinterpret_cast<const float4*>((WL ? &BCL[l * CI] : P.bc[l]) + 8 * i + 4 * h);
+        const float4 bv = *reinterpret_cast<const float4*>((WW ? &BCL[l * CI] : P.bc[l]) + 8 * i + 4 * h);
         bias[2 * i] = f32x2{bv.x, bv.y}; bias[2 * i + 1] = f32x2{bv.z, bv.w};
       }
       for (int kp = kf + wave; kp <= kpl; kp += NW) {
