@@ -210,6 +210,7 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 /* 6: reserved (r02's streaming LVC kernel, removed in r03: measured slower) */
 #define FD_OPT_KP_CHUNK 7     /* n > 0: kernel predictor + LVC block per chunk of n utterances (default 0 = whole batch) */
 /* 8, 9: reserved (r03's skewed persistent LVC kernel, removed: measured slower) */
+#define FD_OPT_LVC_TPW 10     /* 32-row tiles per wave of the 384-sample hop >= 32 LVC blocks: 2 (8 waves) or 1 (16 waves) */
 int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */
@@ -245,6 +246,11 @@ int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce, const 
                     const float* noise, unsigned long long seed, const int* utt_ids, int draw0,
                     float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream);
 
+/* The sampler's x_T ~ N(0,1) draw alone (util.py:208): exactly the [B,L] array fd_sample /
+ * fd_sample_coefs draw when their x_T is NULL (same seed and utt_ids), written to x_T.  A
+ * pass-by-pass run (return_sequence=True) takes its first state from here. */
+int fd_draw_x_T(const fd_model* m, float* x_T, int B, int Tc, unsigned long long seed, const int* utt_ids,
+                void* stream);
 
 /* ==================================================================== NSF-HiFiGAN
  * SVS vocoder -- replaces modules/nsf_hifigan/models.py:222-283
@@ -319,8 +325,12 @@ typedef struct {
   int num_spk;               /* spk_embed rows                                               */
   int num_langs;             /* lang_embed rows = len(hparams["languages"]) + 1              */
   int use_dur_embed, use_spk_id, use_gender_id, use_lang_id, use_voicing_embed, use_breath_embed;
-  int rel_pos;               /* 1: RelPositionalEncoding (tts_modules.py:299-300,324-325,
-                                espnet_positional_embedding.py:89-115) instead of the sinusoid */
+  int rel_pos;               /* > 0: RelPositionalEncoding (tts_modules.py:299-300,324-325,
+                                espnet_positional_embedding.py:89-115) instead of the sinusoid,
+                                with a table of max(rel_pos, 5000 if rel_pos == 1) rows: the
+                                reference's table starts at 5000 rows and extend_pe (:24-45)
+                                keeps the longest input's length, which then sets the
+                                reversed positions of every later, shorter batch         */
 } pd_cond_dims;
 
 /* Parameter order = the reference state-dict order (buffers and `diffusion.*` skipped), fp32:

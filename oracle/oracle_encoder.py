@@ -116,7 +116,7 @@ def encoder(P, hp, txt_tokens, extra_embed):
     if extra_embed is not None:
         x = x + extra_embed
     if hp.get("rel_pos"):   # tts_modules.py:324-325: x * sqrt(H) + pe (no padding-aware positions)
-        x = x * math.sqrt(H) + rel_pos_table(txt_tokens.shape[1], H)[None]
+        x = x * math.sqrt(H) + rel_pos_table(txt_tokens.shape[1], H, hp.get("rel_pos_len") or 5000)[None]
     else:
         pos = make_positions(~pad)
         x = x + sinusoid_table(int(pos.max()) + 1, H)[pos]

@@ -15,7 +15,8 @@ PD_DTYPE_F32 = 0
 PD_DTYPE_BF16 = 1
 PD_REFLOW = {"euler": 0, "rk2": 1, "rk4": 2, "rk5": 3}
 # fd_set_option / nsf_set_option ids (include/prodiff_hip.h)
-FD_OPTIONS = {"lvc_ts": 0, "lvc_ts_sub": 1, "lvc_fuse": 2, "lvc_pf": 3, "lvc_sub": 4, "kp_side": 5, "kp_chunk": 7}
+FD_OPTIONS = {"lvc_ts": 0, "lvc_ts_sub": 1, "lvc_fuse": 2, "lvc_pf": 3, "lvc_sub": 4, "kp_side": 5, "kp_chunk": 7,
+               "lvc_tpw": 10}
 NSF_OPTIONS = {"small_max": 0, "wconv": 1}
 WN_OPTIONS = {"layer": 0, "ksplit": 1, "l2pf": 2}
 
@@ -94,6 +95,7 @@ _SIGS = {
     "fd_sample_coefs": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                   C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, C.c_int, _VP,
                                   C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
+    "fd_draw_x_T": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_ulonglong, _VP, _VP]),
     "pd_cond_num_params": (C.c_int, [C.POINTER(pd_cond_dims)]),
     "pd_cond_create": (C.c_int, [C.POINTER(pd_cond_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
     "pd_cond_destroy": (None, [_VP]),
@@ -169,30 +171,46 @@ def utt_ids(ids, B, device):
     (ids 0..B-1) or B ints -> (device int32 tensor or None).  Keep the tensor alive until
     the call's stream work is done (a captured graph keeps it).
 
-    A device int32 tensor is used as given (not range-checked: that would read it back).
-    Host ids are checked here and their device copy is cached by value: a pageable
-    host-to-device copy blocks the host until the stream drains, which left the GPU idle
-    while the host queued the next launches (C3 trace r03: ~50 us per sampler call)."""
+    A device int32 tensor must live on the sampler's device (a tensor on another GPU is
+    copied there); its values are NOT range-checked (that would read it back to the host),
+    and a negative id draws the same noise as the id it wraps to as uint32.  Host ids are
+    checked here and their device copy is cached by value: a pageable host-to-device copy
+    blocks the host until the stream drains, which left the GPU idle while the host queued
+    the next launches (C3 trace r03: ~50 us per sampler call).  Cached tensors are marked
+    as in use by the current stream on every hit (record_stream), so an evicted entry is
+    not reused by the allocator while another stream's kernels still read it; a cache
+    miss is refused while the current stream is capturing a graph (the H2D copy would be
+    captured): pass a device tensor or warm the cache before the capture."""
     if ids is None:
         return None
     import torch
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
     if torch.is_tensor(ids) and ids.is_cuda:
         t = ids.reshape(-1)
         if t.numel() != B:
             raise HipError(f"utt_ids holds {t.numel()} ids for a batch of {B}")
+        if t.device != dev:
+            t = t.to(dev)
         return t if t.dtype == torch.int32 and t.is_contiguous() else t.to(torch.int32).contiguous()
     t = torch.as_tensor(ids).reshape(-1)
     if t.numel() != B:
         raise HipError(f"utt_ids holds {t.numel()} ids for a batch of {B}")
     if t.numel() and (int(t.min()) < 0 or int(t.max()) >= 2 ** 31):
         raise HipError("utt_ids must lie in [0, 2**31)")
-    key = (str(torch.device(device)), tuple(int(v) for v in t.tolist()))
+    key = (str(dev), tuple(int(v) for v in t.tolist()))
     d = _UTT_CACHE.get(key)
     if d is None:
+        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            raise HipError("utt_ids: host ids not seen before cannot be copied to the device during a "
+                           "graph capture; pass a device int32 tensor (or call once before capturing)")
         if len(_UTT_CACHE) >= 256:
             _UTT_CACHE.pop(next(iter(_UTT_CACHE)))
-        d = t.to(device=device, dtype=torch.int32).contiguous()
+        d = t.to(device=dev, dtype=torch.int32).contiguous()
         _UTT_CACHE[key] = d
+    elif dev.type == "cuda":
+        d.record_stream(torch.cuda.current_stream(dev))
     return d
 
 

@@ -43,7 +43,8 @@ enum EncUse { U_ENC_QKV = 30, U_ENC_OUT = 31, U_ENC_FFN1 = 32, U_ENC_FFN2 = 33 }
 //    (SinusoidalPositionalEmbedding.get_embedding, common_layers.py:111-128, fp32 as there).
 //  * rel_pos: x[t,c] = ((sqrt(H) emb[tok][c] + extra) sqrt(H) + pr(t, c)) * [tok != 0], with
 //    the RelPositionalEncoding table pr(t, 2i) = sin(q g_i), pr(t, 2i+1) = cos(q g_i),
-//    q = max(5000, T) - 1 - t (reversed positions, max_len 5000), g_i = exp(2i (-ln(1e4)/H))
+//    q = max(P, T) - 1 - t (reversed positions; P = the rows of the reference's table, 5000 at
+//    first and the longest input seen since: pd_cond_dims.rel_pos), g_i = exp(2i (-ln(1e4)/H))
 //    (espnet_positional_embedding.py:24-45,108-115; FFTBlocks masks the padding, tts_modules.py:274).
 constexpr int EMB_TOK = 8;
 
@@ -103,7 +104,8 @@ __global__ __launch_bounds__(256) void enc_embed_kernel(
       if (lr) extra = extra + lr[c];
       float v;
       if (rel_pos) {
-        const float q = (float)((Tt > 5000 ? Tt : 5000) - 1 - t);
+        const int P = rel_pos > 1 ? rel_pos : 5000;
+        const float q = (float)((Tt > P ? Tt : P) - 1 - t);
         const float arg = q * expf((float)(c & ~1) * neg_rel);
         v = (scale * er[c] + extra) * scale + ((c & 1) ? cosf(arg) : sinf(arg));
       } else {

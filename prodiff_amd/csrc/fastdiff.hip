@@ -69,6 +69,7 @@ struct fd_model {
   // saves (r01 ab_v16b: 7.41 vs 7.33 ms/step).
   bool kp_side = false;
   int kp_chunk = 0;   // FD_OPT_KP_CHUNK: utterances per kernel-predictor -> LVC chunk (0 = whole batch)
+  int lvc_tpw = 2;    // FD_OPT_LVC_TPW: 32-row tiles per wave of the 384-sample hop >= 32 blocks (2 or 1)
 
   mutable hipStream_t side = nullptr;
   mutable hipEvent_t ev_hidden = nullptr, ev_kp[4] = {}, ev_lvc[4] = {};
@@ -379,9 +380,9 @@ struct LvcBlockArgs {
 #endif
 constexpr int LB_LD = 40;
 constexpr int LB_XLD = 36;                          // fp32 staging rows (144 B)
-template <int TS> struct LbGeo {
+template <int TS, int TPW = 2> struct LbGeo {
   static constexpr int NG = TS / 32 + 4;            // tiles in the grid
-  static constexpr int NW = NG / 2;                 // waves; two tiles each
+  static constexpr int NW = NG / TPW;               // waves; TPW tiles each
   static constexpr int NT = NW * 64;
   static constexpr int UOFF = 28;                   // U index = row + 28 (pre-conv reach 1 + 27)
   static constexpr int UROWS = NG * 32 + 2 * UOFF;
@@ -417,10 +418,14 @@ __device__ __forceinline__ f32x2 gate2r(f32x2 gs, f32x2 fs) {
 }
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0 ? a : a - b + 1) / b; }
 
-template <int TS, bool UPS, bool AUD, bool FIN, bool PF = false, bool SUB = false>
-__global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_bf16_kernel(const LvcBlockArgs P) {
+// TPW = tiles per wave: 2 (NG/2 waves, 2 per SIMD at TS = 384) or 1 (NG waves: 16 at TS = 384,
+// 4 per SIMD, so one wave's MFMAs run beside another's gate VALU; <= 128 VGPRs).
+template <int TS, bool UPS, bool AUD, bool FIN, bool PF = false, bool SUB = false, int TPW = 2>
+__global__ __launch_bounds__((LbGeo<TS, TPW>::NT), (TPW == 1 ? LbGeo<TS, TPW>::NT / 256 : (PF || SUB) ? 2 : 3))
+void lvc_block_bf16_kernel(const LvcBlockArgs P) {
   static_assert(!(PF && SUB), "prefetch assumes one frame per tile");
-  using G = LbGeo<TS>;
+  static_assert(TPW == 1 || TPW == 2, "one or two tiles per wave");
+  using G = LbGeo<TS, TPW>;
   constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF, GR = NG * 32;
   constexpr int EX = FIN ? 3 : 0;                    // extra valid rows for the fused final conv
   // Rows = time, 40 bf16 per row; position p of a row holds channel lvc_chan(p).
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   // first 4 (the 2 x 64-row halo), so both read those frames' kernels in the same pass and
   // the second read can hit L2 (hop 8: the halo re-reads were a third of the launch's bytes).
   const int jsw = !PF && (bx & 1);
-#define TILE(j) (PF ? 2 * wave + (j) : wave + ((j) ^ jsw) * NW)
+#define TILE(j) (TPW == 1 ? wave : PF ? 2 * wave + (j) : wave + ((j) ^ jsw) * NW)
   const int Tc = P.Tc, hop = P.hop;
   const int Lh = Tc * hop;                           // utterance-local times fit in 32 bits
   const int t0 = bx * TS, tg = t0 - 64;              // time of grid row 0
@@ -564,7 +569,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   // and share one 64x96 kernel.  Layer l's fragments are loaded into registers while layer
   // l - 1 finishes (issued right after the pair's MFMAs), so their latency hides behind the
   // gates, the staging and the pre-conv.  Loads are unconditional (frame clamped).
-  const int fpair = min(max(tg + 64 * wave + 32, 0) / hop, Tc - 1);
+  const int fpair = min(max(tg + 32 * TPW * wave + 16 * TPW, 0) / hop, Tc - 1);
   bf16x8 kn[12];
   auto kload = [&](int l) {
     const __bf16* kq = P.Kf[l] + ((long long)b * Tc + fpair) * KPERLAYER;
@@ -627,7 +632,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   }
   LB_STAMP(16);
   // ---- x rows (upsampled in-kernel, or loaded) -> registers
-  f32x2 xr[2][8], ar[2][8];
+  f32x2 xr[TPW][8], ar[TPW][8];
   if constexpr (UPS) {
     // (a) XP[j - jb] = bf16 lrelu(x_prev[j]), j in [jb, jb + 32 ntj]: j0 - 1 .. j0 of every column
 #pragma unroll
@@ -687,7 +692,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   // (reg&3) + 8(reg>>2) + 4h; pair p = regs (2p, 2p+1).  Four float4 loads per tensor
   // (channels 8i + 4h .. +3).
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < TPW; ++j) {
     const int k = TILE(j), row = k * 32 + n, t = tg + row;
     const bool ok = row >= RLO && row < RHI && t >= 0 && t < Lh;
 #pragma unroll
@@ -738,7 +743,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
     const int kpl = kl + 1 < NG - 1 ? kl + 1 : NG - 1;           // last pre-conv tile
     // (1) u = lrelu(z) (z = x + a) of the owned tiles the pre-conv reads: 2 x 16 B per lane
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int k = TILE(j);
       if (k >= kf - 1 && k <= kl + 2) {
         bf16x8 u0, u1;
@@ -846,11 +851,11 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
       // the pair's 24 MFMAs as 4 interleaved chains on the shared kernel (an inactive tile
       // of the pair computes on its own rows and is dropped), then the next layer's
       // prefetch, then the two gates.  Accumulators start from the frame's staged bias.
-      bool act[2];
-      f32x16 g[2], f[2];
+      bool act[TPW];
+      f32x16 g[TPW], f[TPW];
       const float* bq = &BFL[((fpair - fbase) * NLY + l) * 2 * CI];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < TPW; ++j) {
         const int k = TILE(j), ts = tg + k * 32;
         act[j] = k >= kf && k <= kl && ts >= 0 && ts < Lh;
 #pragma unroll
@@ -864,7 +869,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
 #pragma unroll
       for (int kk = 0; kk < 6; ++kk) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < TPW; ++j) {
           const bf16x8 yb = *reinterpret_cast<const bf16x8*>(
               &Y[(TILE(j) * 32 + n + (kk >> 1)) * LB_LD + 16 * (kk & 1) + 8 * h]);
           g[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g[j], 0, 0, 0);
@@ -873,11 +878,11 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
       }
       if (l + 1 < NLY) kload(l + 1);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TPW; ++j)
         if (act[j]) gate_update(j, g[j], f[j], nullptr, true);
     } else {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int k = TILE(j), ts = tg + k * 32;
       if (k >= kf && k <= kl && ts >= 0 && ts < Lh) {
         f32x16 g, f;
@@ -955,7 +960,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
     float* E = XS;                                   // [GR rows][8]
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int k = TILE(j), row = k * 32 + n;
       if (k >= 1 && k <= NG - 2) {
         float st[7];
@@ -997,7 +1002,7 @@ __global__ __launch_bounds__(LbGeo<TS>::NT, (PF || SUB) ? 2 : 3) void lvc_block_
   } else {
     // centre tiles [2, 2 + TS/32) -> x out
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int k = TILE(j), t = tg + k * 32 + n;
       if (k >= 2 && k < 2 + TS / 32 && t < Lh) {
 #pragma unroll
@@ -1784,14 +1789,26 @@ struct FdFinal {
   const int* uid;
 };
 
-template <int TS, bool UPS, bool AUD, bool FIN, bool PF, bool SUB = false>
+template <int TS, bool UPS, bool AUD, bool FIN, bool PF, bool SUB = false, int TPW = 2>
 void launch_lvc_block_t(const LvcBlockArgs& la, long long Tout, int B, hipStream_t st) {
-  hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, UPS, AUD, FIN, PF, SUB>), dim3(cdiv(Tout, TS), B),
-                     dim3(LbGeo<TS>::NT), 0, st, la);
+  hipLaunchKernelGGL((lvc_block_bf16_kernel<TS, UPS, AUD, FIN, PF, SUB, TPW>), dim3(cdiv(Tout, TS), B),
+                     dim3(LbGeo<TS, TPW>::NT), 0, st, la);
 }
-template <int TS>
+template <int TS, int TPW = 2>
 int launch_lvc_block_ts(const LvcBlockArgs& la, bool ups, bool aud, bool fin, bool pf, long long Tout, int B,
                         hipStream_t st) {
+  if constexpr (TPW == 1) {   // one tile per wave (hop >= 32 only)
+    if (la.hop < 32 || !ups || (aud != fin)) { set_error("lvc_block: one tile per wave needs hop >= 32 and the fused upsample"); return PD_ERR_ARG; }
+    if (fin) {
+      if (pf) launch_lvc_block_t<TS, true, true, true, true, false, 1>(la, Tout, B, st);
+      else launch_lvc_block_t<TS, true, true, true, false, false, 1>(la, Tout, B, st);
+    } else {
+      if (pf) launch_lvc_block_t<TS, true, false, false, true, false, 1>(la, Tout, B, st);
+      else launch_lvc_block_t<TS, true, false, false, false, false, 1>(la, Tout, B, st);
+    }
+    PD_LAUNCH_CHECK();
+    return PD_OK;
+  }
   if (la.hop < 32) {   // several frames per 32-row tile (the hop-8 block)
     if (aud || fin) { set_error("lvc_block: audio/final fusion needs hop >= 32"); return PD_ERR_ARG; }
     if (ups) launch_lvc_block_t<TS, true, false, false, false, true>(la, Tout, B, st);
@@ -1949,6 +1966,8 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
         const bool pf = m->lvc_pf && hop % 64 == 0;   // a 64-row tile pair shares one frame
         if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
+        else if (ts == 384 && m->lvc_tpw == 1 && hop >= 32 && ups && (last && aud) == fuse_fin)
+          PD_TRY((launch_lvc_block_ts<384, 1>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st)));
         else if (ts == 384) PD_TRY(launch_lvc_block_ts<384>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
         else PD_TRY(launch_lvc_block_ts<128>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
       }
@@ -2190,6 +2209,14 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S) {
   return fd_layout(m, B, Tc, S < FD_STEP_CHUNK ? S : FD_STEP_CHUNK).total;
 }
 
+int fd_draw_x_T(const fd_model* m, float* x_T, int B, int Tc, unsigned long long seed, const int* utt_ids,
+                void* stream) {
+  PD_CHECK_ARG(m && x_T, "null pointer");
+  PD_CHECK_ARG(B >= 0 && Tc >= 0, "bad shape");
+  const long long L = (long long)Tc * m->hops[m->nblocks - 1];
+  return fill_normal_utt(x_T, B, L, seed, 0xFFFF0001u, utt_ids, (hipStream_t)stream);   // fd_sample_coefs' x_T stream
+}
+
 int fd_set_option(fd_model* m, int option, int value) {
   PD_CHECK_ARG(m, "null pointer");
   switch (option) {
@@ -2209,6 +2236,10 @@ int fd_set_option(fd_model* m, int option, int value) {
     case FD_OPT_KP_CHUNK:
       PD_CHECK_ARG(value >= 0, "FD_OPT_KP_CHUNK >= 0");
       m->kp_chunk = value;
+      return PD_OK;
+    case FD_OPT_LVC_TPW:
+      PD_CHECK_ARG(value == 1 || value == 2, "FD_OPT_LVC_TPW in {1,2}");
+      m->lvc_tpw = value;
       return PD_OK;
     default: break;
   }

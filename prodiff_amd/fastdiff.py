@@ -261,6 +261,16 @@ class FastDiff(nn.Module):
         return eps
 
     @torch.no_grad()
+    def draw_x_T(self, B, Tc, seed, utt_ids=None, device=None):
+        """The samplers' x_T ~ N(0,1) draw (util.py:208) for (seed, utt_ids): [B,1,L]."""
+        h = self.handle()
+        dev = device if device is not None else next(self.parameters()).device
+        x = torch.empty(B, 1, Tc * self.hop_length, device=dev, dtype=torch.float32)
+        uid = _lib.utt_ids(utt_ids, B, dev)
+        _lib.check(_lib.lib().fd_draw_x_T(h, _lib.fptr(x), B, Tc, int(seed), _lib.iptr(uid), _lib.stream_ptr(dev)))
+        return x
+
+    @torch.no_grad()
     def sample_coefs(self, mel, ce, den, sg, steps, x_T=None, noise=None, seed=None, utt_ids=None, draw0=0):
         """The reverse loop with explicit per-pass coefficients (fd_sample_coefs): pass j
         evaluates eps at steps[j] and sets x = (x - ce[j] eps) / den[j] + sg[j] z."""
@@ -361,10 +371,8 @@ def sampling_given_noise_schedule(net, size, diffusion_hyperparams, inference_no
         return net.sample_coefs(mel, ce, den, sg, st, x_T=x_T, noise=noise, seed=seed)
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-    if x_T is None:   # the fused run's x_T draw (Philox stream of fd_sample_coefs with x_T NULL)
-        # ce = 0, den = 1, sg = 0: the pass returns its x_T draw unchanged
-        x = net.sample_coefs(mel, np.zeros(1, np.float32), np.ones(1, np.float32), np.zeros(1, np.float32),
-                             st[:1], seed=seed, x_T=None, noise=None, draw0=0)
+    if x_T is None:   # the fused run's x_T draw (fd_draw_x_T: fd_sample_coefs' draw with x_T NULL)
+        x = net.draw_x_T(B, mel.shape[1], seed, device=mel.device)
     else:
         x = x_T.float().reshape(B, 1, L).clone()
     xs = [x.clone()]

@@ -180,7 +180,7 @@ def _numel(shape):
     return int(np.prod(shape)) if len(shape) else 1
 
 
-def gather_to_root(t, root=0, shapes=None):
+def gather_to_root(t, root=0, shapes=None, force=False):
     """Point-to-point gather of per-rank tensors of DIFFERENT shapes to `root`
     (torch's NCCL backend -- RCCL on ROCm -- implements gather as sends to the
     root; gloo on CPU).  Every rank passes a tensor of the same ndim and dtype.
@@ -189,8 +189,9 @@ def gather_to_root(t, root=0, shapes=None):
     already knows them (``shapes``: one tuple per rank, e.g. from the shard plan,
     which saves that round trip).  Each rank's tensor is flattened and padded to
     the largest size, gathered, and trimmed on the root.  Returns the list of
-    per-rank tensors (rank order) on the root, None elsewhere."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    per-rank tensors (rank order) on the root, None elsewhere.  ``force`` runs the
+    collective even at world size 1 (tests drive RCCL on a one-GPU box that way)."""
+    if not dist.is_initialized() or (dist.get_world_size() == 1 and not force):
         return [t]
     world, rank = dist.get_world_size(), dist.get_rank()
     t = t.contiguous()
@@ -233,7 +234,8 @@ def length_groups(lengths, idx):
     return sorted(groups.items(), key=lambda kv: -kv[0])
 
 
-def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None):
+def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None,
+                           collectives=False):
     """Synthesize utterances sharded over the ranks of the default process group
     (SURVEY §8(e)); the reference runs them one by one, B=1 per segment
     (handler/infer/handler.py:373-388).
@@ -253,7 +255,9 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     deterministic, so no shape exchange is needed.  Returns on the root the lists
     [mel_i [T_i,M]], [wav_i [T_i*hop]] in input order; (None, None) elsewhere.
     ``stats`` (a dict, optional) receives this rank's ``compute_ms`` (its shard's
-    synthesis, device-synchronized) and ``gather_ms`` (the collectives after it)."""
+    synthesis, device-synchronized) and ``gather_ms`` (the collectives after it).
+    ``collectives=True`` runs the all_reduce and the ragged gathers even at world size 1
+    (otherwise short-circuited), so the N > 1 code path can be exercised on one GPU."""
     import time
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -286,7 +290,7 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         mel_flat, wav_flat = torch.cat(mel_parts), torch.cat(wav_parts)
     sync()
     t1 = time.perf_counter()
-    if world == 1:
+    if world == 1 and not (collectives and dist.is_initialized()):
         mels_all, wavs_all = [mel_flat], [wav_flat]
     else:
         # mel bins: known to every rank with a non-empty shard
@@ -295,8 +299,8 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         M = int(mt.item())
         mel_shapes = [(sum(lengths[i] for i in s) * M,) for s in shards]
         wav_shapes = [(sum(lengths[i] for i in s) * hop,) for s in shards]
-        mels_all = gather_to_root(mel_flat, root, mel_shapes)
-        wavs_all = gather_to_root(wav_flat, root, wav_shapes)
+        mels_all = gather_to_root(mel_flat, root, mel_shapes, force=collectives)
+        wavs_all = gather_to_root(wav_flat, root, wav_shapes, force=collectives)
     sync()
     if stats is not None:
         stats["compute_ms"] = (t1 - t0) * 1e3

@@ -82,6 +82,13 @@ class RelPositionalEncoding(nn.Module):
     def __init__(self, d_model, dropout_rate=0.0, max_len=5000):
         super().__init__()
         self.d_model, self.max_len = d_model, max_len
+        # rows of the reference's table: extend_pe (:24-45) regrows it for a longer input and
+        # keeps the longer table, so later, shorter batches count their reversed positions from
+        # the largest length seen so far; tracked here and passed as pd_cond_dims.rel_pos
+        self.pe_len = max_len
+
+    def extend(self, T):
+        self.pe_len = max(self.pe_len, int(T))
 
 
 class FastspeechEncoder(nn.Module):
@@ -179,7 +186,7 @@ class ProDiffTeacher(nn.Module):
             self.lang_embed.num_embeddings if self.with_lang_embed else 0,
             int(self.with_dur_embed), int(self.with_spk_embed), int(self.with_gender_embed),
             int(self.with_lang_embed), int(self.with_voicing_embed), int(self.with_breath_embed),
-            int(e.rel_pos))
+            e.embed_positions.pe_len if e.rel_pos else 0)
 
     def ordered_cond_params(self):
         """Tensors in the include/prodiff_hip.h pd_cond order (== reference state-dict order)."""
@@ -201,7 +208,7 @@ class ProDiffTeacher(nn.Module):
 
     def cond_handle(self):
         ps = self.ordered_cond_params()
-        sig = (self.compute_dtype,) + tuple((p.data_ptr(), p._version) for p in ps)
+        sig = (self.compute_dtype, self.cond_dims().rel_pos) + tuple((p.data_ptr(), p._version) for p in ps)
         if self._h is not None and sig == self._sig:
             return self._h
         L = _lib.lib()
@@ -247,6 +254,8 @@ class ProDiffTeacher(nn.Module):
             raise AssertionError("spk_embed_id or spk_mix_embed is required")
         if self.with_gender_embed and gender_embed_id is None and gender_mix_embed is None:
             raise AssertionError("gender_embed_id or gender_mix_embed is required")
+        if self.encoder.rel_pos:
+            self.encoder.embed_positions.extend(txt_tokens.shape[1])
         h = self.cond_handle()
         dev = txt_tokens.device
         B, Tt = txt_tokens.shape

@@ -380,15 +380,14 @@ def gen_reflow():
 # Full-size fixtures (SURVEY §8(c) fixture (vi)): C2 (ProDiff 2-iter, B=1, T=1000)
 # and a C3 slice (B=2 x 861 frames: ProDiff 2-iter -> FastDiff 4-iter).  Every
 # input and draw is regenerated from its seed by prodiff_amd.synth (see
-# FULLSIZE_CASES), so only outputs are stored: the full mel, the waveform at every
-# 8th sample, and per-utterance statistics of the whole waveform.
+# FULLSIZE_CASES), so only outputs are stored: the full mel, the whole waveform (fp32,
+# 2 x 220,416 samples for C3) and per-utterance statistics of it.
 # --------------------------------------------------------------------------
 FULLSIZE_CASES = {
     # name: (B, T, prodiff weight seed, fastdiff weight seed or None, draw seed for FastDiff)
     "fullsize_c2": (1, 1000, 61, None, None),
     "fullsize_c3_b2": (2, 861, 62, 63, 64),
 }
-WAV_STRIDE = 8
 
 
 def gen_fullsize():
@@ -424,7 +423,7 @@ def gen_fullsize():
                 fd_util.std_normal = orig
             assert cnt[0] == 4
             w64 = wav.astype(np.float64)
-            out.update(fastdiff_seed=fs, draw_seed=ds, wav_stride=WAV_STRIDE, wav_sub=wav[:, ::WAV_STRIDE],
+            out.update(fastdiff_seed=fs, draw_seed=ds, wav=wav.astype(np.float32),
                        wav_l2=np.linalg.norm(w64, axis=1), wav_mean=w64.mean(1), wav_absmax=np.abs(w64).max(1))
         save(name, **out)
 
@@ -446,6 +445,10 @@ COND_CASES = {
                   80, [300, 257], 0, 44, 144, "mix_1"),
     # RelPositionalEncoding (tts_modules.py:299-300,324-325), padded batch
     "cond_relpos": (dict(num_spk=2, num_langs=3, enc_layers=2, rel_pos=True), 40, [21, 13], 1, 45, 145, "id"),
+    # the same after the module's table grew to 5,010 rows (extend_pe, espnet_positional_embedding.py:24-45,
+    # as a 5,010-token batch leaves it): later batches count reversed positions from 5,010
+    "cond_relpos_grown": (dict(num_spk=2, num_langs=3, enc_layers=2, rel_pos=True), 40, [21, 13], 1, 45, 145, "id",
+                          5010),
 }
 
 
@@ -457,7 +460,8 @@ def cond_hparams(over):
 
 def gen_cond():
     from modules.svs.prodiff_teacher import ProDiffTeacher
-    for name, (over, V, lengths, padt, ps, xs, spk_mode) in COND_CASES.items():
+    for name, case in COND_CASES.items():
+        (over, V, lengths, padt, ps, xs, spk_mode), grow = case[:7], (case[7] if len(case) > 7 else 0)
         hp = cond_hparams(over)
         rhp = dict(hp, audio_num_mel_bins=128, dropout=0.1, languages=["l%d" % i for i in range(hp["num_langs"] - 1)],
                    residual_layers=1, residual_channels=64, dilation_cycle_length=1, timesteps=4, timescale=1000,
@@ -489,6 +493,9 @@ def gen_cond():
             kw["voicing"] = torch.from_numpy(x["voicing"])
         if hp["use_breath_embed"]:
             kw["breath"] = torch.from_numpy(x["breath"])
+        if grow:
+            m.encoder.embed_positions.extend_pe(torch.zeros(1, grow))
+            assert m.encoder.embed_positions.pe.shape[1] == grow
         enc_out = {}
         hook = m.encoder.register_forward_hook(lambda mod, inp, out: enc_out.setdefault("enc", out.detach().clone()))
         with torch.no_grad():
@@ -497,7 +504,7 @@ def gen_cond():
         hook.remove()
         save(name, vocab=V, lengths=np.array(lengths), pad_tokens=padt, param_seed=ps, input_seed=xs,
              spk_mode=spk_mode, hp_keys=np.array(list(over)), hp_vals=np.array([int(v) for v in over.values()]),
-             cond=cond, enc=enc_out["enc"].numpy(), **{k: v for k, v in x.items()}, **extra)
+             cond=cond, enc=enc_out["enc"].numpy(), grow=grow, **{k: v for k, v in x.items()}, **extra)
 
 
 if __name__ == "__main__":

@@ -43,6 +43,8 @@ def cond_case(name):
     over = {str(k): int(v) for k, v in zip(d["hp_keys"], d["hp_vals"])}
     hp = dict(synth.COND_DEFAULTS)
     hp.update(over)
+    if int(d.get("grow", 0)):   # the reference's RelPositionalEncoding table had grown to this many rows
+        hp["rel_pos_len"] = int(d["grow"])
     P = synth.synth_cond_params(synth.cond_param_shapes(int(d["vocab"]), **hp), int(d["param_seed"]))
     ins = {k: d[k] for k in ("txt_tokens", "mel2ph", "f0") + COND_INPUTS if k in d}
     if str(d["spk_mode"]) != "id":
@@ -54,4 +56,4 @@ def cond_case(name):
     return hp, P, ins, d
 
 
-COND_CASES = ("cond_small", "cond_handler", "cond_mix_gender", "cond_long", "cond_relpos")
+COND_CASES = ("cond_small", "cond_handler", "cond_mix_gender", "cond_long", "cond_relpos", "cond_relpos_grown")

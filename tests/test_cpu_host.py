@@ -168,6 +168,31 @@ def test_teacher_needs_gpu_and_lang_seq():
                             voicing=torch.zeros(1, 4), breath=torch.zeros(1, 4))
 
 
+def test_rel_pos_table_grows_like_the_reference():
+    """RelPositionalEncoding's table (espnet_positional_embedding.py:24-45) starts at 5,000 rows,
+    grows to a longer input's length and never shrinks; the mirror tracks the same length and
+    hands it to the kernel as pd_cond_dims.rel_pos (0 when the encoder uses the sinusoid)."""
+    from prodiff_amd.teacher import ProDiffTeacher
+    t = ProDiffTeacher(40, dict(TEACHER_HP, rel_pos=True))
+    assert t.cond_dims().rel_pos == 5000
+    t.encoder.embed_positions.extend(4000)
+    assert t.cond_dims().rel_pos == 5000
+    t.encoder.embed_positions.extend(6001)
+    t.encoder.embed_positions.extend(21)
+    assert t.cond_dims().rel_pos == 6001
+    assert ProDiffTeacher(40, TEACHER_HP).cond_dims().rel_pos == 0
+
+
+def test_utt_ids_host_checks():
+    with pytest.raises(_lib.HipError):
+        _lib.utt_ids([1, 2], 3, "cpu")
+    with pytest.raises(_lib.HipError):
+        _lib.utt_ids([-1, 2], 2, "cpu")
+    assert _lib.utt_ids(None, 3, "cpu") is None
+    d = _lib.utt_ids([4, 5], 2, "cpu")
+    assert d.dtype == torch.int32 and d.tolist() == [4, 5]
+
+
 def test_cond_create_rejects_bad_dims():
     lib = _lib.lib()
     d = _lib.pd_cond_dims(40, 256, 4, 9, 3, 1, 3, 1, 1, 0, 1, 0, 0)   # 256 / 3 heads

@@ -223,3 +223,26 @@ def test_wavenet_two_kernel_vs_fused(cyc):
     print(f"BF16ERR two-kernel vs fused WaveNet cyc={cyc} B={B}x{T} rel-L2={rel:.3e}")
     assert np.isfinite(a).all() and rel <= 2e-3
 
+
+
+@pytest.mark.parametrize("pf", [0, 1])
+@pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
+def test_fastdiff_lvc_one_tile_per_wave(pf, B, Tc):
+    """FD_OPT_LVC_TPW=1 (16 waves, one 32-row tile each) computes every tile with the same
+    instructions as the 8-wave kernel (TPW=2): the sample is bit-identical, with and without
+    the next-layer kernel prefetch, and within the bf16 bar of the oracle."""
+    from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
+    p = G.fastdiff_params(31)
+    b, a, s, st = fastdiff_infer_params(fastdiff_reverse_schedule(4), fastdiff_train_alpha())
+    mel = synth.synth_inputs(60 + B, (B, Tc, 80), loc=-5.0, scale=2.0)
+    xT = synth.synth_inputs(61 + B, (B, 1, Tc * 256))
+    nz = synth.synth_inputs(62 + B, (3, B, 1, Tc * 256))
+    outs = {}
+    for tpw in (2, 1):
+        m = FastDiff()
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+        m = m.to(DEV).set_compute_dtype("bf16").set_options(lvc_pf=pf, lvc_tpw=tpw)
+        outs[tpw] = m.sample(tt(mel), b, a, s, st, x_T=tt(xT), noise=tt(nz)).cpu().numpy()
+    np.testing.assert_array_equal(outs[1], outs[2])
+    ref = OF.fastdiff_sample(OF.fold_weight_norm(p), np.transpose(mel, (0, 2, 1)), xT, nz, b, a, s, st)
+    assert_bf16_close(outs[1].reshape(ref.shape), ref, f"sampler tpw=1 pf={pf} B={B} Tc={Tc}")

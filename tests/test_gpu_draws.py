@@ -10,6 +10,9 @@ semantics, not values of the reference.
 
 Bar: a batch of 3 equals each utterance run alone (and a permuted batch), |delta| <= 1e-5
 relative to max|x| (fp32: the batched kernels may sum in a different order at other B).
+The bf16 path (the one bench.py and C4 run: the FIN epilogue of the last LVC block draws
+each output sample's noise by Philox keyed with utt_id(uid, b + b_off)) is held to the same
+bar: every bf16 kernel computes a row from that row's inputs only, in a fixed order.
 """
 import numpy as np
 import pytest
@@ -29,13 +32,14 @@ def close(a, b, rel=1e-5):
     assert err <= tol, (err, tol)
 
 
-@pytest.fixture(scope="module")
-def syn():
+@pytest.fixture(scope="module", params=["fp32", "bf16"])
+def syn(request):
     # the full FastDiff vocoder; a 4-layer ProDiff WaveNet keeps the test short
-    return Synthesizer.synthetic(DEV, seed=3, dtype="fp32", residual_layers=4)
+    return Synthesizer.synthetic(DEV, seed=3, dtype=request.param, residual_layers=4)
 
 
 def test_synthesizer_batch_equals_each_alone(syn):
+    # 9 frames = 2,304 samples per utterance: several 384-sample LVC tiles per utterance
     B, T = 3, 9
     cond = torch.from_numpy(synth.synth_inputs(77, (B, T, 256))).to(DEV)
     ids = [5, 9, 2]
@@ -74,7 +78,8 @@ def test_distributed_synthesize_matches_batched(syn):
         close(wavs[i][None], w1[:, :wavs[i].shape[0]])
 
 
-def test_reflow_and_nsf_batch_equals_each_alone():
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_reflow_and_nsf_batch_equals_each_alone(dtype):
     from prodiff_amd import WaveNet
     from prodiff_amd.nsf_hifigan import Generator
     from prodiff_amd.reflow import RectifiedFlow
@@ -83,6 +88,7 @@ def test_reflow_and_nsf_batch_equals_each_alone():
     net.load_state_dict({k: torch.from_numpy(v)
                          for k, v in synth.synth_params(synth.wavenet_param_shapes(M, H, L, C), 8).items()})
     rf = RectifiedFlow(out_dims=M, denoise_fn=net, spec_min=[-12.0], spec_max=[0.0]).to(DEV)
+    rf.set_compute_dtype(dtype)
     cond = torch.from_numpy(synth.synth_inputs(81, (3, 11, H))).to(DEV)
     x = rf.sample(cond, infer_step=3, seed=5, utt_ids=[4, 1, 7])
     for i, u in enumerate([4, 1, 7]):
@@ -90,7 +96,7 @@ def test_reflow_and_nsf_batch_equals_each_alone():
     h = dict(synth.NSF_DEFAULTS, upsample_initial_channel=32, upsample_rates=(4, 4), upsample_kernel_sizes=(8, 8))
     g = Generator(h)
     g.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_params(synth.nsf_param_shapes(**h), 9).items()})
-    g = g.to(DEV).eval()
+    g = g.to(DEV).eval().set_compute_dtype(dtype)
     mel = torch.from_numpy(synth.synth_inputs(82, (3, 6, 128), loc=-2.0)).to(DEV)
     f0 = torch.full((3, 6), 220.0, device=DEV)
     f0[1, 2:] = 0.0

@@ -3,8 +3,8 @@
 * C2 (ProDiff 2-iter, B=1, T=1000, fp32) against the reference's output, eager
   and as a replayed hipGraph: |d| <= 1e-4.
 * A C3 slice (B=2 x 861 frames: ProDiff 2-iter -> FastDiff 4-iter, fp32) against
-  the reference: mel |d| <= 1e-4; waveform |d| <= 1e-4 at every 8th sample plus
-  the whole-waveform statistics (L2 norm, mean, max) to 1e-5 relative.
+  the reference: mel |d| <= 1e-4; the whole waveform (2 x 220,416 samples)
+  |d| <= 1e-4 plus its statistics (L2 norm, mean, max) to 1e-5 relative.
 * Full C3 (B=8 x 861) in bf16 against the fp32 HIP path with the SAME explicit
   draws (the fp32 path is pinned to the reference above): mel and waveform within
   the bf16 bar of tests/test_gpu_bf16.py.  This runs the grid-scale code the
@@ -130,9 +130,9 @@ def test_c3_slice_fastdiff_fp32(c3):
     xT, nz = fastdiff_draws(int(c3["draw_seed"]), B, L)
     b, a, s, st = SCHED
     wav = m.sample(tt(c3["mel"]), b, a, s, st, x_T=tt(xT), noise=tt(nz))[:, 0].cpu().numpy().astype(np.float64)
-    sub = wav[:, ::int(c3["wav_stride"])]
-    err = float(np.abs(sub - c3["wav_sub"]).max())
-    print(f"C3-slice FastDiff fp32 max|d| (every 8th sample) = {err:.3e}, max|ref| = {np.abs(c3['wav_sub']).max():.2f}")
+    assert wav.shape == c3["wav"].shape
+    err = float(np.abs(wav - c3["wav"]).max())
+    print(f"C3-slice FastDiff fp32 max|d| (whole waveform) = {err:.3e}, max|ref| = {np.abs(c3['wav']).max():.2f}")
     assert err <= ABS
     np.testing.assert_allclose(np.linalg.norm(wav, axis=1), c3["wav_l2"], rtol=1e-5)
     np.testing.assert_allclose(np.abs(wav).max(1), c3["wav_absmax"], rtol=1e-5)

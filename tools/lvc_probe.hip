@@ -1,7 +1,7 @@
 // Standalone probe for lvc_block_bf16_kernel: times the kernel alone on C3-sized
 // synthetic inputs and prints where a block spends its time (s_memtime stamps per
 // phase, LB_TRACE).  Diagnostic only (not a parity check: inputs are random).
-//   build: make -C tools lvc_probe      run: tools/build/lvc_probe [hop] [TS] [final=1]
+//   build: make -C tools lvc_probe      run: tools/bin/lvc_probe [hop] [TS] [final=1]
 #define LB_TRACE 1
 #include "../prodiff_amd/csrc/fastdiff.hip"
 

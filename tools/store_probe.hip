@@ -5,7 +5,7 @@
 // and when a wave's whole 96 KiB region is contiguous (seq).  Every wave owns 32 rows x
 // 3 KiB and sweeps them column-chunk by column-chunk, as kp_kernel's waves do; 8 waves per
 // block, 2 blocks per CU.  Plain and non-temporal stores.  Diagnostic only.
-//   build: make -C tools store_probe      run: tools/build/store_probe
+//   build: make -C tools store_probe      run: tools/bin/store_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

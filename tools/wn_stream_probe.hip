@@ -5,7 +5,7 @@
 // with no math ("stream"), or with the layer's 160 MFMAs per wave fed from registers
 // ("stream+mfma"), at the grids the C3 (216 blocks) and C2-like (54) layers launch, plus 256
 // and 512.  8 waves per block, 1 block per CU as the real kernel.  Diagnostic only.
-//   build: make -C tools wn_stream_probe      run: tools/build/wn_stream_probe
+//   build: make -C tools wn_stream_probe      run: tools/bin/wn_stream_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
