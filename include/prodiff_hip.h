@@ -211,6 +211,8 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 #define FD_OPT_KP_CHUNK 7     /* n > 0: kernel predictor + LVC block per chunk of n utterances (default 0 = whole batch) */
 /* 8, 9: reserved (r03's skewed persistent LVC kernel, removed: measured slower) */
 #define FD_OPT_LVC_TPW 10     /* 32-row tiles per wave of the 384-sample hop >= 32 LVC blocks: 2 (8 waves) or 1 (16 waves) */
+#define FD_OPT_LVC_PRIO 11    /* bit 0: s_setprio(1) for the second half of an LVC block's waves; bit 1: that half
+                                 gates its first tile before its second tile's MFMAs (stagger) */
 int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */

@@ -225,24 +225,27 @@ def test_wavenet_two_kernel_vs_fused(cyc):
 
 
 
-@pytest.mark.parametrize("pf", [0, 1])
+@pytest.mark.parametrize("opts", [dict(lvc_pf=0, lvc_tpw=1), dict(lvc_pf=1, lvc_tpw=1), dict(lvc_pf=1, lvc_prio=1),
+                                  dict(lvc_pf=1, lvc_prio=3)])
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
-def test_fastdiff_lvc_one_tile_per_wave(pf, B, Tc):
-    """FD_OPT_LVC_TPW=1 (16 waves, one 32-row tile each) computes every tile with the same
-    instructions as the 8-wave kernel (TPW=2): the sample is bit-identical, with and without
-    the next-layer kernel prefetch, and within the bf16 bar of the oracle."""
+def test_fastdiff_lvc_schedule_variants(opts, B, Tc):
+    """LVC-block variants that change only the schedule, not the arithmetic of a tile:
+    FD_OPT_LVC_TPW=1 (16 waves, one 32-row tile each; with and without the next-layer kernel
+    prefetch) and FD_OPT_LVC_PRIO (static priority, staggered tile order for half the waves).
+    The sample is bit-identical to the default kernel with the same prefetch setting, and within
+    the bf16 bar of the oracle."""
     from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
     p = G.fastdiff_params(31)
     b, a, s, st = fastdiff_infer_params(fastdiff_reverse_schedule(4), fastdiff_train_alpha())
     mel = synth.synth_inputs(60 + B, (B, Tc, 80), loc=-5.0, scale=2.0)
     xT = synth.synth_inputs(61 + B, (B, 1, Tc * 256))
     nz = synth.synth_inputs(62 + B, (3, B, 1, Tc * 256))
-    outs = {}
-    for tpw in (2, 1):
+    outs = []
+    for o in (dict(lvc_pf=opts["lvc_pf"]), opts):
         m = FastDiff()
         m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
-        m = m.to(DEV).set_compute_dtype("bf16").set_options(lvc_pf=pf, lvc_tpw=tpw)
-        outs[tpw] = m.sample(tt(mel), b, a, s, st, x_T=tt(xT), noise=tt(nz)).cpu().numpy()
-    np.testing.assert_array_equal(outs[1], outs[2])
+        m = m.to(DEV).set_compute_dtype("bf16").set_options(**o)
+        outs.append(m.sample(tt(mel), b, a, s, st, x_T=tt(xT), noise=tt(nz)).cpu().numpy())
+    np.testing.assert_array_equal(outs[1], outs[0])
     ref = OF.fastdiff_sample(OF.fold_weight_norm(p), np.transpose(mel, (0, 2, 1)), xT, nz, b, a, s, st)
-    assert_bf16_close(outs[1].reshape(ref.shape), ref, f"sampler tpw=1 pf={pf} B={B} Tc={Tc}")
+    assert_bf16_close(outs[1].reshape(ref.shape), ref, f"sampler {opts} B={B} Tc={Tc}")
