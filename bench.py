@@ -361,6 +361,8 @@ def main():
                     help="FastDiff kernel-variant option for A/B runs (fd_set_option, e.g. kp_chunk=4)")
     ap.add_argument("--wn-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="WaveNet kernel-variant option for A/B runs (pd_wavenet_set_option, e.g. layer=0)")
+    ap.add_argument("--nsf-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="NSF-HiFiGAN kernel-variant option for A/B runs (nsf_set_option, e.g. pair=0)")
     args = ap.parse_args()
 
     # ---- N ranks: re-launch under torch.distributed.run BEFORE anything touches the GPU
@@ -424,6 +426,8 @@ def main():
         syn = SvsSynthesizer.synthetic(dev, seed=0, dtype=dtype)
         if args.wn_opt:
             syn.diffusion.denoise_fn.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.wn_opt)})
+        if args.nsf_opt:
+            syn.generator.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.nsf_opt)})
         synth_fn = syn
     else:
         from prodiff_amd import _lib

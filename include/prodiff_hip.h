@@ -95,6 +95,10 @@ void pd_wavenet_destroy(pd_wavenet* h);
 /* PD_WN_OPT_L2PF (bf16 fused layer): 1 (default) each layer launch pulls the next layer's weight
  * fragments into every XCD's L2 while it runs; 0 = off. */
 #define PD_WN_OPT_L2PF 2
+/* PD_WN_OPT_STACK (bf16, C = H = 256, dilation_cycle_length 1, T >= 64): n = 1..16 residual layers per
+ * launch (wn_stack_bf16_kernel: a 64-frame window per 32 output frames stays resident for the
+ * n layers; bit-identical to the one-layer kernel); 0 = one launch per layer. */
+#define PD_WN_OPT_STACK 3
 int pd_wavenet_set_option(pd_wavenet* h, int option, int value);
 /* S = number of reverse steps the workspace must serve (1 for pd_wavenet_forward). */
 size_t pd_wavenet_workspace_size(const pd_wavenet* h, int B, int T, int S);
@@ -211,8 +215,7 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 #define FD_OPT_KP_CHUNK 7     /* n > 0: kernel predictor + LVC block per chunk of n utterances (default 0 = whole batch) */
 /* 8, 9: reserved (r03's skewed persistent LVC kernel, removed: measured slower) */
 #define FD_OPT_LVC_TPW 10     /* 32-row tiles per wave of the 384-sample hop >= 32 LVC blocks: 2 (8 waves) or 1 (16 waves) */
-#define FD_OPT_LVC_PRIO 11    /* bit 0: s_setprio(1) for the second half of an LVC block's waves; bit 1: that half
-                                 gates its first tile before its second tile's MFMAs (stagger) */
+#define FD_OPT_LVC_PRIO 11    /* 1: s_setprio(1) for the second half of an LVC block's waves */
 int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */
@@ -295,6 +298,10 @@ size_t nsf_workspace_size(const nsf_model* m, int B, int T);
  * MFMA conv kernels (input window staged once in LDS for all taps), ahead of
  * NSF_OPT_SMALL_MAX; 0 = the implicit-GEMM engine / small kernel.  No effect on the fp32 path. */
 #define NSF_OPT_WCONV 1
+/* NSF_OPT_PAIR: 1 (default) runs each ResBlock1 conv pair c2(lrelu(c1(lrelu(x)))) + x with 64 or 128
+ * channels as ONE windowed launch (the inner activation stays in LDS, x is read once); 0 = two
+ * windowed launches with the inner activation through HBM in bf16.  Same roundings either way. */
+#define NSF_OPT_PAIR 2
 int nsf_set_option(nsf_model* m, int option, int value);
 
 /* spec2wav_torch(mel, f0=f0) for a batch of independent utterances:

@@ -70,13 +70,13 @@ struct fd_model {
   bool kp_side = false;
   int kp_chunk = 0;   // FD_OPT_KP_CHUNK: utterances per kernel-predictor -> LVC chunk (0 = whole batch)
   int lvc_tpw = 2;    // FD_OPT_LVC_TPW: 32-row tiles per wave of the 384-sample hop >= 32 blocks (2 or 1)
-  int lvc_prio = 0;   // FD_OPT_LVC_PRIO: bit 0 s_setprio(1) for the second half of an LVC block's waves,
-                      // bit 1 staggered tile order for that half (prefetch variant)
+  int lvc_prio = 0;   // FD_OPT_LVC_PRIO: 1 = s_setprio(1) for the second half of an LVC block's waves
 
   mutable hipStream_t side = nullptr;
   mutable hipEvent_t ev_hidden = nullptr, ev_kp[4] = {}, ev_lvc[4] = {};
   float* pool = nullptr;
   __bf16* pool_bf = nullptr;   // bf16 mirror of `pool` (PD_DTYPE_BF16), registered with launch_gemm
+  void* kps = nullptr;         // the blocks' pre-scaled kernel-predictor weights (kks_w, kks_b)
   // step MLP
   float *fc1_w, *fc1_b, *fc2_w, *fc2_b;
   float *first_w, *first_b;          // [32][7]
@@ -88,6 +88,8 @@ struct fd_model {
     float *kin_w, *kin_b;            // [64][5*96]
     float *kres_w[6], *kres_b[6];    // [64][3*64]
     float *kk_w, *kk_b;              // [4*6144][3*64] frame-major rows
+    __bf16* kks_w = nullptr;         // bf16: kk_w rows pre-scaled for the whole-block LVC gate (gate rows
+    float* kks_b = nullptr;          //   by -log2 e, filter rows by 2 log2 e), and kk_b likewise
     float *kb_w, *kb_b;              // [256][3*64]
     float *cv_w[NLY], *cv_b[NLY];    // [32][96]
   } blk[4];
@@ -364,8 +366,7 @@ struct LvcBlockArgs {
   const int* uid;           // FIN: utterance id per batch row (null -> row index)
   int Tc, hop;
   int b_off;                // utterance index of blockIdx.y = 0 in the whole batch (Philox draws)
-  int prio;                 // FD_OPT_LVC_PRIO: bit 0 s_setprio(1), bit 1 staggered tile order, for
-                            // the second half of the waves
+  int prio;                 // FD_OPT_LVC_PRIO: s_setprio(1) for the second half of the waves
 #ifdef LB_TRACE
   unsigned long long* trace;   // tools/lvc_probe.hip: per-phase s_memtime stamps
 #endif
@@ -759,7 +760,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
   LB_STAMP(1);
   // static priority for the later-dispatched half of the waves (their SIMD partners are the
   // first half): MI355X_MICROARCH.md "Two waves per SIMD", item 4
-  if ((P.prio & 1) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (P.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int l = 0; l < NLY; ++l) {
     const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
@@ -777,6 +778,10 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
           const f32x2 v0 = lrelu2(xr[j][p]), v1 = lrelu2(xr[j][4 + p]);
           u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
           u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
+        }
+        if constexpr (PF) {   // a tile outside the utterance is the convs' zero padding (the PF gate
+          const int ts = tg + k * 32;   // updates every tile, so its x is not zero there)
+          if (ts < 0 || ts >= Lh) { u0 = bf16x8{}; u1 = bf16x8{}; }
         }
         __bf16* dst = &U[(k * 32 + n + UOFF) * LB_LD + 16 * h];
         *reinterpret_cast<bf16x8*>(dst) = u0;
@@ -873,16 +878,12 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
       }
     };
     if constexpr (PF) {
-      // the pair's 24 MFMAs as 4 interleaved chains on the shared kernel (an inactive tile
-      // of the pair computes on its own rows and is dropped), then the next layer's
+      // the pair's 24 MFMAs as 4 interleaved chains on the shared kernel, then the next layer's
       // prefetch, then the two gates.  Accumulators start from the frame's staged bias.
-      bool act[TPW];
       f32x16 g[TPW], f[TPW];
       const float* bq = &BFL[((fpair - fbase) * NLY + l) * 2 * CI];
 #pragma unroll
       for (int j = 0; j < TPW; ++j) {
-        const int k = TILE(j), ts = tg + k * 32;
-        act[j] = k >= kf && k <= kl && ts >= 0 && ts < Lh;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
@@ -891,41 +892,22 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
           f[j][4 * i] = bl.x; f[j][4 * i + 1] = bl.y; f[j][4 * i + 2] = bl.z; f[j][4 * i + 3] = bl.w;
         }
       }
-      auto chain = [&](int j) {
 #pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
+      for (int kk = 0; kk < 6; ++kk) {
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
           const bf16x8 yb = *reinterpret_cast<const bf16x8*>(
               &Y[(TILE(j) * 32 + n + (kk >> 1)) * LB_LD + 16 * (kk & 1) + 8 * h]);
           g[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g[j], 0, 0, 0);
           f[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f[j], 0, 0, 0);
         }
-      };
-      if (TPW == 2 && (P.prio & 2) && wave >= NW / 2) {
-        // stagger (FD_OPT_LVC_PRIO bit 1): the later half of the waves -- each one's SIMD partner
-        // is in the first half -- gates tile 0 before tile 1's MFMAs, so its gate VALU runs
-        // beside the partner's second chain and the partner's first gate beside its own
-        // second chain (MI355X_MICROARCH.md "Two waves per SIMD", item 9)
-        chain(0);
-        if (act[0]) gate_update(0, g[0], f[0], nullptr, true);
-        chain(TPW - 1);
-        if (l + 1 < NLY) kload(l + 1);
-        if (act[TPW - 1]) gate_update(TPW - 1, g[TPW - 1], f[TPW - 1], nullptr, true);
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
-#pragma unroll
-          for (int j = 0; j < TPW; ++j) {
-            const bf16x8 yb = *reinterpret_cast<const bf16x8*>(
-                &Y[(TILE(j) * 32 + n + (kk >> 1)) * LB_LD + 16 * (kk & 1) + 8 * h]);
-            g[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g[j], 0, 0, 0);
-            f[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f[j], 0, 0, 0);
-          }
-        }
-        if (l + 1 < NLY) kload(l + 1);
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-          if (act[j]) gate_update(j, g[j], f[j], nullptr, true);
       }
+      if (l + 1 < NLY) kload(l + 1);
+      // every tile is updated, with no branch between the tiles' gates (the compiler interleaves
+      // them): a tile outside this layer's valid range is never read by a valid row, one outside
+      // the utterance is zeroed where it is read (the u stage above, the final conv's partial sums)
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) gate_update(j, g[j], f[j], nullptr, true);
     } else {
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
@@ -1023,6 +1005,13 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
         }
 #pragma unroll
         for (int tap = 0; tap < 7; ++tap) st[tap] += __shfl_xor(st[tap], 32);
+        if constexpr (PF) {   // x is zero outside the utterance (the final conv's padding)
+          const int ts = tg + k * 32;
+          if (ts < 0 || ts >= Lh) {
+#pragma unroll
+            for (int tap = 0; tap < 7; ++tap) st[tap] = 0.f;
+          }
+        }
         if (h == 0) {
           *reinterpret_cast<float4*>(&E[row * 8]) = make_float4(st[0], st[1], st[2], st[3]);
           *reinterpret_cast<float4*>(&E[row * 8 + 4]) = make_float4(st[4], st[5], st[6], 0.f);
@@ -1459,7 +1448,8 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 // A lane of C holds 4 consecutive kernel values of one frame; a per-wave LDS transpose turns
 // them into 128-B row segments (8 frames per 1-KiB store: 6.0 TB/s in tools/store_probe.hip).
 constexpr int KP_F = 128, KP_NG = 512, KP_LDH = 200;   // 400-B LDS rows: conflict-free b128 reads
-constexpr int KP_LDO = 72;                             // output transpose rows: 64 + 8 pad
+constexpr int KP_LDO = 72;                             // output transpose rows: 64 + 8 pad (144 B: rows stay
+                                                       // 16-B aligned for the b128 reads; 68 measured 15% slower)
 constexpr int KP_NGROUPS = NLY * KPERLAYER / KP_NG;    // 48
 constexpr int KP_THREADS = 512;
 #ifndef KP_PROBE
@@ -1472,7 +1462,7 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
                                                                        const __bf16* __restrict__ W,
                                                                        const float* __restrict__ bias,
                                                                        __bf16* __restrict__ Kf, int Tc, int rows,
-                                                                       int nfg, float sg, float sf) {
+                                                                       int nfg) {
   __shared__ __attribute__((aligned(16))) __bf16 Hs[2][KP_F * KP_LDH];
   __shared__ __attribute__((aligned(16))) __bf16 Ot[8][32 * KP_LDO];
   __shared__ __attribute__((aligned(16))) float Bq[8][64];   // wave-private: its rows' biases
@@ -1492,11 +1482,15 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
   auto h_load = [&](int item) {
     const int fg = item % nfg;
     hz = 0;
+    // the item's first frame split once (wave-uniform); piece frames step forward from it
+    const int R0 = fg * KP_F, b0 = R0 / Tc, f00 = R0 - b0 * Tc;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const int c = tid + KP_THREADS * i, fl = c / 24, v = (c - fl * 24) * 8, tap = v >> 6, ch = v & 63;
-      const int R = fg * KP_F + fl, Rc = R < rows ? R : rows - 1;
-      const int b = Rc / Tc, f = Rc - b * Tc, ff = f + tap - 1;
+      const int R = R0 + fl, Rc = R < rows ? R : rows - 1;
+      int b = b0, f = f00 + (Rc - R0);
+      while (f >= Tc) { f -= Tc; ++b; }   // at most KP_F / Tc steps
+      const int ff = f + tap - 1;
       const int ffc = ff < 0 ? 0 : ff >= Tc ? Tc - 1 : ff;     // clamped: unconditional load
       hv[i] = *reinterpret_cast<const uint4*>(hin + ((long long)b * Tc + ffc) * HK + ch);
       hz |= (R >= rows || ff < 0 || ff >= Tc) ? 1u << i : 0u;
@@ -1527,16 +1521,6 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
   h_store(0);
   __syncthreads();
   __bf16* ot = Ot[wave];
-  // Software-pipelined K stores: frame tile ft's four 1-KiB row stores are issued between the
-  // MFMAs of the NEXT tile (one after every third k-step), so each wave's store stream is spread
-  // over its MFMA stream instead of arriving as a burst while the matrix pipe idles.  The pending
-  // stores carry their descriptor and offsets; "nothing pending" is an out-of-range offset, which
-  // the buffer store drops (no branch in the MFMA loop).
-  uint4 sv[4];
-  __amdgpu_buffer_rsrc_t kprev = __builtin_amdgcn_make_buffer_rsrc(Kf, 0, 0, 0x00020000);
-  unsigned soff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { sv[i] = make_uint4(0u, 0u, 0u, 0u); soff[i] = 0x7FFFFFF0u; }
   for (int item = ib; item < ie; ++item) {
     const int buf = (item - ib) & 1, ng = item / nfg, fg = item - ng * nfg;
     if (ng != ng_cur) {   // wave-uniform; once or twice per block
@@ -1545,7 +1529,6 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
     }
     h_load(min(item + 1, ie - 1));   // the next item's frames, under this item's work
     const int nb = ng * KP_NG + wave * 64, layer = nb / KPERLAYER, n0 = nb - layer * KPERLAYER;
-    const float sc = n0 < KPERLAYER / 2 ? sg : sf;           // gate rows / filter rows
 #if KP_PROBE == 2   // diagnostic build (tools/build_variant_lib.sh): every K store dropped
     const __amdgpu_buffer_rsrc_t kout = __builtin_amdgcn_make_buffer_rsrc(Kf, 0, 0, 0x00020000);
 #else
@@ -1555,11 +1538,16 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
     const __bf16* hs = Hs[buf];
 #pragma unroll
     for (int ft = 0; ft < KP_F / 32; ++ft) {   // unrolled: hipcc counts the stores in vmcnt
+      // C[n][frame]: lane owns frame r32, rows n = 32j + 8g + 4h + (0..3); the accumulators
+      // start from the rows' biases, so the epilogue is a conversion only
       f32x16 acc[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+        for (int g = 0; g < 4; ++g) {
+          const float4 bn = *reinterpret_cast<const float4*>(&bw[j * 32 + 8 * g + 4 * h]);
+          acc[j][4 * g] = bn.x; acc[j][4 * g + 1] = bn.y; acc[j][4 * g + 2] = bn.z; acc[j][4 * g + 3] = bn.w;
+        }
 #pragma unroll
       for (int kk = 0; kk < 12; ++kk) {
         const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hs[(ft * 32 + r32) * KP_LDH + kk * 16 + h * 8]);
@@ -1569,33 +1557,24 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[kk], hb, acc[0], 0, 0, 0);
         acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[12 + kk], hb, acc[1], 0, 0, 0);
 #endif
-        if (kk % 3 == 2) {   // the previous tile's stores (340 MB per launch, read back by the next launch)
-          const int i = kk / 3;
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4_{sv[i].x, sv[i].y, sv[i].z, sv[i].w}, kprev, soff[i], 0,
-                                                 KP_AUX);
-        }
       }
-      // C[n][frame]: lane owns frame r32, rows n = 32j + 8g + 4h + (0..3)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 bn = *reinterpret_cast<const float4*>(&bw[j * 32 + 8 * g + 4 * h]);
+        for (int g = 0; g < 4; ++g)
           *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + j * 32 + 8 * g + 4 * h]) =
-              bf16x4{(__bf16)((acc[j][4 * g] + bn.x) * sc), (__bf16)((acc[j][4 * g + 1] + bn.y) * sc),
-                     (__bf16)((acc[j][4 * g + 2] + bn.z) * sc), (__bf16)((acc[j][4 * g + 3] + bn.w) * sc)};
-        }
+              bf16x4{(__bf16)acc[j][4 * g], (__bf16)acc[j][4 * g + 1], (__bf16)acc[j][4 * g + 2], (__bf16)acc[j][4 * g + 3]};
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
       __builtin_amdgcn_wave_barrier();
       const int f0 = fg * KP_F + ft * 32;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
-        sv[i] = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
-        soff[i] = ((f0 + fl) * KPERLAYER + n0 + ch) * 2;
+        const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
+        // 340 MB per launch, read back by the next launch
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_{v.x, v.y, v.z, v.w}, kout,
+                                               ((f0 + fl) * KPERLAYER + n0 + ch) * 2, 0, KP_AUX);
       }
-      kprev = kout;
-      __builtin_amdgcn_s_waitcnt(0xC07F);   // the ot reads are in registers
       __builtin_amdgcn_wave_barrier();      // the next frame tile rewrites ot
     }
     // the next item's frames into the other buffer, whose readers (the previous item) are
@@ -1604,13 +1583,24 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
     h_store(buf ^ 1);
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)   // the last tile's stores
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4_{sv[i].x, sv[i].y, sv[i].z, sv[i].w}, kprev, soff[i], 0, KP_AUX);
 }
 
 // prescale: the gate half scaled by -log2(e), the filter half by 2 log2(e) (the whole-block
-// LVC kernel's gate takes exp2 arguments straight from its accumulators).
+// LVC kernel's gate takes exp2 arguments straight from its accumulators): the pre-scaled weight
+// copy, so the kernel's epilogue is a bf16 conversion only.
+// kks_w = bf16(kk_w * s(n)), kks_b = kk_b * s(n): s = -log2 e on a layer's gate rows (n % 6144 <
+// 3072: output channels 0..31), 2 log2 e on its filter rows.
+__global__ void kp_prescale_kernel(const float* __restrict__ w, const float* __restrict__ b, __bf16* __restrict__ ws,
+                                   float* __restrict__ bs) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr long long NW = (long long)NLY * KPERLAYER * 3 * HK;
+  if (i >= NW) return;
+  const int n = (int)(i / (3 * HK));
+  const float s = n % KPERLAYER < KPERLAYER / 2 ? -LOG2E : 2.f * LOG2E;
+  ws[i] = (__bf16)(w[i] * s);
+  if (i % (3 * HK) == 0) bs[n] = b[n] * s;
+}
+
 int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B, int Tc, hipStream_t st,
                    bool prescale = false) {
   const int rows = B * Tc;
@@ -1620,8 +1610,8 @@ int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B
   const int items = KP_NGROUPS * nfg;
   const int grid = items < 256 ? items : 256;   // persistent: one block per CU
   ProfScope ps("fd_kp_kernel", st);
-  hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(grid), dim3(KP_THREADS), 0, st, hk, lookup_bf16(K.kk_w), K.kk_b, Kb,
-                     Tc, rows, nfg, prescale ? -LOG2E : 1.f, prescale ? 2.f * LOG2E : 1.f);
+  hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(grid), dim3(KP_THREADS), 0, st, hk,
+                     prescale ? K.kks_w : lookup_bf16(K.kk_w), prescale ? K.kks_b : K.kk_b, Kb, Tc, rows, nfg);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -2243,6 +2233,17 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
       PD_HIP(hipMalloc((void**)&m->pool_bf, off * sizeof(__bf16)));
       PD_TRY(convert_f32_bf16(m->pool, m->pool_bf, (long long)off, st));
       register_bf16_pool(m->pool, off, m->pool_bf);
+      // pre-scaled kernel-predictor weights of every block (bf16 rows, fp32 biases)
+      const size_t nw = (size_t)NLY * KPERLAYER * 3 * HK, nbias = (size_t)NLY * KPERLAYER;
+      PD_HIP(hipMalloc(&m->kps, m->nblocks * (nw * sizeof(__bf16) + nbias * sizeof(float))));
+      for (int n = 0; n < m->nblocks; ++n) {
+        auto& K = m->blk[n];
+        K.kks_b = reinterpret_cast<float*>(m->kps) + n * nbias;
+        K.kks_w = reinterpret_cast<__bf16*>(reinterpret_cast<float*>(m->kps) + m->nblocks * nbias) + n * nw;
+        hipLaunchKernelGGL(kp_prescale_kernel, dim3(cdiv((long long)nw, 256)), dim3(256), 0, st, K.kk_w, K.kk_b, K.kks_w,
+                           K.kks_b);
+        PD_LAUNCH_CHECK();
+      }
     }
     return PD_OK;
   };
@@ -2252,6 +2253,7 @@ int fd_create(const fd_dims* dims, const float* const* params, int dtype, void* 
   if (rc != PD_OK) {
     (void)hipFree(m->pool);
     if (m->pool_bf) (void)hipFree(m->pool_bf);
+    if (m->kps) (void)hipFree(m->kps);
     delete m;
     return rc;
   }
@@ -2274,6 +2276,7 @@ void fd_destroy(fd_model* m) {
     unregister_bf16_pool(m->pool);
     (void)hipFree(m->pool_bf);
   }
+  if (m->kps) (void)hipFree(m->kps);
   (void)hipFree(m->pool);
   delete m;
 }
@@ -2314,7 +2317,7 @@ int fd_set_option(fd_model* m, int option, int value) {
       m->kp_chunk = value;
       return PD_OK;
     case FD_OPT_LVC_PRIO:
-      PD_CHECK_ARG(value >= 0 && value <= 3, "FD_OPT_LVC_PRIO in 0..3");
+      PD_CHECK_ARG(value == 0 || value == 1, "FD_OPT_LVC_PRIO in {0,1}");
       m->lvc_prio = value;
       return PD_OK;
     case FD_OPT_LVC_TPW:

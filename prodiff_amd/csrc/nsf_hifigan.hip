@@ -60,6 +60,7 @@ struct nsf_model {
   std::vector<NsfUps> ups;
   std::vector<NsfConv> res;      // [stage][kernel][conv] flattened in state-dict order
   bool ups_window = true;        // NSF_OPT_WCONV also selects the windowed ConvTranspose
+  bool pair = true;              // NSF_OPT_PAIR: a ResBlock1 conv pair in one launch (nsf_pair_kernel)
   int convs_per_block = 0;
 };
 
@@ -466,6 +467,174 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
           }
         }
   }
+}
+
+// ResBlock1 conv pair in ONE launch (models.py:57-63, one q of ResBlock1.forward):
+//   xt = c1(lrelu(x)) (dilation d), out = c2(lrelu(xt)) (dilation 1) + x [+ out when accumulating]
+// Block = TM = 32 FMO output rows of one utterance, 4 waves.  The x window (rows t0 - p2 - p1 ..
+// t0 + TM + p2 + p1, lrelu'd, bf16) is staged once; c1 runs on the 32 (FMO + 1) rows of xt that
+// c2 reads (TM + 2 p2 <= 32 (FMO + 1) for k <= 33), rounds them to bf16 exactly as the two-launch
+// path's bf16 intermediate, applies lrelu and keeps them in LDS; c2 reads that window.  Per
+// output row this drops the intermediate's HBM write and read and the second staging of x.
+// Waves: column tile ct = wave % NCT (NCT = C / 32) of both convs; with NCT = 2 the row tiles are
+// split between two wave pairs by parity.
+template <int C, int FMO>
+__global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restrict__ x, const __bf16* __restrict__ w1,
+                                                      const __bf16* __restrict__ w2, int ldw, int kpad,
+                                                      const float* __restrict__ b1, const float* __restrict__ b2,
+                                                      int taps, int dil, int Tl, float* __restrict__ out, int accum) {
+  constexpr int NCT = C / 32, RG = 4 / NCT, LDA = C + 8, KS = C / 16;
+  constexpr int TM = 32 * FMO, RT1 = FMO + 1;            // output rows; c1 row tiles
+  constexpr int MF1 = (RT1 + RG - 1) / RG, MF2 = (FMO + RG - 1) / RG;   // row tiles per wave
+  static_assert(NCT == 2 || NCT == 4, "C = 64 or 128");
+  extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int ct = wave % NCT, rg = wave / NCT;
+  const int b = blockIdx.z, t0 = blockIdx.x * TM;
+  const int p2 = (taps - 1) / 2, p1 = (taps - 1) * dil / 2;
+  const int WX = 32 * RT1 + (taps - 1) * dil;            // x window rows
+  __bf16* xwin = nsf_win;                                // [WX][LDA]: lrelu(x), time t0 - p2 - p1 + j
+  __bf16* xtw = nsf_win + WX * LDA;                      // [32 RT1][LDA]: lrelu(xt), time t0 - p2 + i
+  stage_window<C, false>(x, b, Tl, t0 - p2 - p1, WX, NSF_LRELU, 1.f, xwin, LDA, tid);
+  __syncthreads();
+  const int S = taps * KS;
+  constexpr int PF = KS >= NSF_PF ? NSF_PF : KS;
+  static_assert(KS % PF == 0, "ring depth divides the k-steps per tap");
+  const int n = ct * 32 + r32;                           // this lane's output channel (C layout column)
+  // ---- c1 on row tiles rt = rg + RG m (xt rows 32 rt ..)
+  {
+    const __bf16* wr = w1 + (long long)n * ldw + 8 * h;
+    f32x16 acc[MF1];
+#pragma unroll
+    for (int m = 0; m < MF1; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+    bf16x8 bq[PF];
+    auto bload = [&](int st) {
+      const int tn = st / KS, kn = st - tn * KS;
+      return *reinterpret_cast<const bf16x8*>(wr + tn * kpad + 16 * kn);
+    };
+#pragma unroll
+    for (int q = 0; q < PF - 1; ++q) bq[q] = bload(q);
+    for (int s0 = 0; s0 < S; s0 += PF) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int s = s0 + q;
+        bq[(q + PF - 1) % PF] = bload(min(s + PF - 1, S - 1));
+        const int tap = s / KS, kc = s - tap * KS;
+#pragma unroll
+        for (int m = 0; m < MF1; ++m) {
+          const int rt = rg + RG * m;
+          if (rt < RT1) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(xwin + (rt * 32 + r32 + tap * dil) * LDA + 16 * kc + 8 * h);
+            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bq[q], acc[m], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // xt = bf16(acc + b1) (the two-launch path's bf16 intermediate), then c2's input lrelu(xt)
+    // rounded to bf16 again; rows outside the utterance are c2's zero padding
+    const float bn = b1[n];
+#pragma unroll
+    for (int m = 0; m < MF1; ++m) {
+      const int rt = rg + RG * m;
+      if (rt < RT1) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int i = rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, t = t0 - p2 + i;
+          const float v = (float)(__bf16)(acc[m][reg] + bn);
+          const float u = (t >= 0 && t < Tl) ? (v >= 0.f ? v : NSF_LRELU * v) : 0.f;
+          xtw[i * LDA + n] = (__bf16)u;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- c2 on output row tiles rt = rg + RG m, + bias + residual x (+ out)
+  {
+    const __bf16* wr = w2 + (long long)n * ldw + 8 * h;
+    f32x16 acc[MF2];
+#pragma unroll
+    for (int m = 0; m < MF2; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+    bf16x8 bq[PF];
+    auto bload = [&](int st) {
+      const int tn = st / KS, kn = st - tn * KS;
+      return *reinterpret_cast<const bf16x8*>(wr + tn * kpad + 16 * kn);
+    };
+#pragma unroll
+    for (int q = 0; q < PF - 1; ++q) bq[q] = bload(q);
+    for (int s0 = 0; s0 < S; s0 += PF) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int s = s0 + q;
+        bq[(q + PF - 1) % PF] = bload(min(s + PF - 1, S - 1));
+        const int tap = s / KS, kc = s - tap * KS;
+#pragma unroll
+        for (int m = 0; m < MF2; ++m) {
+          const int rt = rg + RG * m;
+          if (rt < FMO) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(xtw + (rt * 32 + r32 + tap) * LDA + 16 * kc + 8 * h);
+            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bq[q], acc[m], 0, 0, 0);
+          }
+        }
+      }
+    }
+    const float bn = b2[n];
+    const int rowb = b * Tl;
+#pragma unroll
+    for (int m = 0; m < MF2; ++m) {
+      const int rt = rg + RG * m;
+      if (rt < FMO) {
+        float rv[16];
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {   // residual (and accumulator) loads in flight together
+          const int t = min(t0 + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tl - 1);
+          const int o = (rowb + t) * C + n;
+          rv[reg] = x[o] + (accum ? out[o] : 0.f);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int t = t0 + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          if (t < Tl) out[(rowb + t) * C + n] = acc[m][reg] + bn + rv[reg];
+        }
+      }
+    }
+  }
+}
+
+template <int C>
+int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
+                  hipStream_t st) {
+  constexpr int FMO = 4, TM = 32 * FMO;
+  const size_t lds = (size_t)(32 * (FMO + 1) * 2 + (c1.taps - 1) * c1.dil) * (C + 8) * sizeof(__bf16);
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&nsf_pair_kernel<C, FMO>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) { set_error("nsf pair: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
+  ProfScope ps("nsf_pair", st);
+  hipLaunchKernelGGL((nsf_pair_kernel<C, FMO>), dim3(cdiv(Tl, TM), 1, B), dim3(256), lds, st, x, lookup_bf16(c1.w),
+                     lookup_bf16(c2.w), c1.taps * c1.kpad, c1.kpad, c1.b, c2.b, c1.taps, c1.dil, Tl, out, accum);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+bool wconv_ok(const NsfConv& c);
+// The fused pair for these convs, if it has one: both windowed (bf16), 64 or 128 channels, equal taps
+// and packing, c2 undilated.
+bool pair_ok(const nsf_model* m, const NsfConv& c1, const NsfConv& c2) {
+  return m->pair && wconv_ok(c1) && wconv_ok(c2) && c1.cout == c2.cout && (c1.cout == 64 || c1.cout == 128) &&
+         c1.taps == c2.taps && c1.kpad == c2.kpad && c2.dil == 1 && c1.taps <= 33;
+}
+
+int launch_pair(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
+                hipStream_t st) {
+  if ((long long)B * Tl * c1.cout >= (1ll << 31)) {
+    set_error("nsf pair: B * T * C >= 2^31 elements (32-bit epilogue offsets)");
+    return PD_ERR_UNSUPPORTED;
+  }
+  if (c1.cout == 128) return launch_pair_c<128>(c1, c2, x, B, Tl, out, accum, st);
+  return launch_pair_c<64>(c1, c2, x, B, Tl, out, accum, st);
 }
 
 // 16-channel variant (the last upsample stage, 512 samples per frame) on
@@ -1096,6 +1265,11 @@ int nsf_set_option(nsf_model* m, int option, int value) {
     m->ups_window = value != 0;
     return PD_OK;
   }
+  if (option == NSF_OPT_PAIR) {
+    PD_CHECK_ARG(value == 0 || value == 1, "NSF_OPT_PAIR is 0 or 1");
+    m->pair = value != 0;
+    return PD_OK;
+  }
   set_error("nsf_set_option: unknown option " + std::to_string(option));
   return PD_ERR_ARG;
 }
@@ -1187,10 +1361,22 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
       float* target = j == 0 ? XS : R;
       const float* cur = X;
       bool summed = false;   // resblock_j(x) already added into XS by its last conv
-      for (int q = 0; q < d.num_dilations; ++q) {
+      const int D = d.num_dilations;
+      for (int q = 0; q < D; ++q) {
         if (d.resblock == 1) {
           const NsfConv& c1 = m->res[r + q];
-          const NsfConv& c2 = m->res[r + d.num_dilations + q];
+          const NsfConv& c2 = m->res[r + D + q];
+          if (pair_ok(m, c1, c2)) {
+            // one launch per pair; it reads neighbouring blocks' rows of cur, so it never writes
+            // cur: the pairs alternate between T1 (fp32 here) and target (XS / R), the last one
+            // landing in target -- or accumulating into XS for resblock j >= 1
+            const bool last_acc = j > 0 && q == D - 1;
+            float* dst = q == D - 1 ? (last_acc ? XS : target) : ((D - 2 - q) % 2 == 0 ? T1 : target);
+            PD_TRY(launch_pair(c1, c2, cur, B, Lc, dst, last_acc ? 1 : 0, st));
+            if (last_acc) { summed = true; continue; }
+            cur = dst;
+            continue;
+          }
           if (wconv_ok(c1) && wconv_ok(c2)) {
             // windowed bf16 convs; the inner activation xt = c1(lrelu(x)) travels as bf16; the
             // last pair of resblock j >= 1 accumulates straight into XS

@@ -36,6 +36,7 @@ struct pd_wavenet {
   int layer_mode = 2;
   int ksplit_blocks = 512;   // PD_WN_OPT_KSPLIT: fp32 layer GEMMs split K up to this many blocks
   int l2_prefetch = 1;       // PD_WN_OPT_L2PF: fused layer l pulls layer l + 1's weights into L2
+  int stack_nl = 0;          // PD_WN_OPT_STACK: residual layers per wn_stack_bf16_kernel launch (0 = off)
 };
 
 namespace {
@@ -302,6 +303,220 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
   if ((pfr[0] ^ pfr[1] ^ pfr[2] ^ pfr[3]) == 0x9E3779B9u && P.pf_lines[0] < 0)   // never true: keeps
     P.xout[0] = 0.f;                                                               // the prefetch loads
   WN_STAMP(7);
+}
+
+// ------------------------------------------------------------------ residual stack, several layers per launch (bf16)
+// Consecutive residual layers [l0, l0 + nl) of wavenet.py:115-119 in ONE launch, for dilation 1
+// (dilation_cycle_length = 1, handler/base_config.yaml).  Block = 32 output rows of the flattened
+// [B*T] batch, holding a 64-row window [R0 - 16, R0 + 48) for all nl layers: x (fp32) in registers
+// in the GEMM2 C layout, bf16(x + dp_l) and bf16(cond) in LDS.  A layer's conv reads rows t +- 1,
+// so the window's outer rows go stale one row per layer; with nl <= 16 the output rows stay exact.
+// Every layer streams its 1.3 MB of fragment-ordered weights through the same register rings as
+// wn_layer_bf16_kernel (the L2 -> CU weight stream, ~12 us per layer and block, is this design's
+// floor), but the staging, the x / skip HBM round trip and the launch happen once per nl layers.
+// Same roundings and the same MFMA order as wn_layer_bf16_kernel: the outputs are bit-identical.
+struct WnStackArgs {
+  const float* xin;       // [rows][C] layer l0's input (other blocks read its window rows)
+  float* xout;            // [rows][C] layer l0 + nl's input (output rows)
+  float* skip;            // [rows][C] running skip sum
+  const __bf16* condb;    // [rows][H] bf16(cond)
+  const float* dp;        // dp[b * dp_ld + l * C + c]
+  int dp_ld;
+  const __bf16* W1f;      // all layers: [L][2C/32][K1/16][64][8]
+  const float* b1;        // [L][2C]
+  const __bf16* W2f;      // [L][2C/32][C/16][64][8]
+  const float* b2;        // [L][2C]
+  int rows, T, l0, nl, first, L;
+};
+constexpr int WST_LD = WNF_C + 8;                    // LDS row: 528 B, conflict-free b128 reads
+#ifndef WST_WD
+#define WST_WD 6
+#endif
+// 8 waves (2 per SIMD): wave w owns gate/filter column tiles w / 8 + w of GEMM1 and residual /
+// skip tiles w / 8 + w of GEMM2, as wn_layer_bf16_kernel.  r04: a 4-wave variant (one wave per
+// SIMD, 12-deep rings) ran 24 us per layer against 21 us for this one (no partner wave to issue
+// beside a wave's MFMA-dependent epilogues).
+__global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs P) {
+  constexpr int C = WNF_C, H = WNF_C, K1 = 3 * C + H, KS1 = K1 / 16, KS2 = C / 16, WD = WST_WD, WD2 = 4;
+  constexpr int WR = 64;                             // window rows: 2 MFMA row tiles
+  __shared__ __attribute__((aligned(16))) __bf16 XW[WR * WST_LD];   // bf16(x + dp_l)
+  __shared__ __attribute__((aligned(16))) __bf16 CW[WR * WST_LD];   // bf16(cond)
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[WR * WST_LD];   // gated g
+  __shared__ float SK[32 * WNF_C];                                   // skip sum of the output rows (lane-private entries)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int rows = P.rows, T = P.T;
+  const int R0 = blockIdx.x * 32, W0 = R0 - 16;      // window row 0
+  const int n = wave * 32 + r32;                     // this lane's residual / skip column
+  // T >= 64 (the host's condition) puts at most two utterances, bA and bB, in the window
+  const int bA = min(max(W0, 0), rows - 1) / T, RB = (bA + 1) * T;   // rows >= RB: utterance bB
+  const int bB = min(bA + 1, (rows - 1) / T);
+  // ---- staging: window rows of bf16(x + dp_l0) and bf16(cond); zero outside [0, rows)
+#pragma unroll
+  for (int it = 0; it < WR * 64 / 512; ++it) {
+    const int i = tid + it * 512, wr = i >> 6, c = (i & 63) * 4, R = W0 + wr;
+    const int Rc = min(max(R, 0), rows - 1);
+    const float4 v = *reinterpret_cast<const float4*>(P.xin + (long long)Rc * C + c);
+    const int b = Rc < RB ? bA : bB;
+    const float4 d = *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + (long long)P.l0 * C + c);
+    const float m = (R >= 0 && R < rows) ? 1.f : 0.f;
+    *reinterpret_cast<bf16x4*>(&XW[wr * WST_LD + c]) =
+        bf16x4{(__bf16)((v.x + d.x) * m), (__bf16)((v.y + d.y) * m), (__bf16)((v.z + d.z) * m), (__bf16)((v.w + d.w) * m)};
+  }
+#pragma unroll
+  for (int it = 0; it < WR * 32 / 512; ++it) {
+    const int i = tid + it * 512, wr = i >> 5, c = (i & 31) * 8, R = W0 + wr;
+    uint4 v = *reinterpret_cast<const uint4*>(P.condb + (long long)min(max(R, 0), rows - 1) * H + c);
+    if (R < 0 || R >= rows) v = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(&CW[wr * WST_LD + c]) = v;
+  }
+  // x (fp32) of the lane's 32 window rows, column n, in registers (the GEMM2 C layout: tile q,
+  // register reg -> window row 32 q + (reg & 3) + 8 (reg >> 2) + 4 h); the skip sum of its 16
+  // output rows (tile 0 regs 8..15 = window rows 16..31, tile 1 regs 0..7 = window rows 32..47)
+  // in LDS, entries only this lane touches
+  float xr[2][16];
+  auto sko = [&](int i) {   // SK index of output value i
+    const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
+    return (32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h - 16) * C + n;
+  };
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      xr[q][reg] = P.xin[(long long)min(max(R, 0), rows - 1) * C + n];
+    }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
+    const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    SK[sko(i)] = P.first ? 0.f : P.skip[(long long)min(R, rows - 1) * C + n];
+  }
+  // conv zero padding: tap t-1 / t+1 of the lane's A rows (window row 32q + r32) outside its
+  // utterance (or outside the batch) reads zero -- a select at the fragment read
+  bool mlo[2], mhi[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int R = W0 + 32 * q + r32, Rc = min(max(R, 0), rows - 1), t = Rc - (Rc / T) * T;
+    mlo[q] = R >= 0 && R < rows && t >= 1;
+    mhi[q] = R >= 0 && R < rows && t <= T - 2;
+  }
+  __syncthreads();
+  const bf16x8 z8 = {};
+  for (int j = 0; j < P.nl; ++j) {
+    const int l = P.l0 + j;
+    const bf16x8* wg = reinterpret_cast<const bf16x8*>(P.W1f + (long long)l * 2 * C * K1) + (long long)wave * KS1 * 64 + lane;
+    const bf16x8* wf = reinterpret_cast<const bf16x8*>(P.W1f + (long long)l * 2 * C * K1) + (long long)(8 + wave) * KS1 * 64 + lane;
+    const bf16x8* wr = reinterpret_cast<const bf16x8*>(P.W2f + (long long)l * 2 * C * C) + (long long)wave * KS2 * 64 + lane;
+    const bf16x8* wsk = reinterpret_cast<const bf16x8*>(P.W2f + (long long)l * 2 * C * C) + (long long)(8 + wave) * KS2 * 64 + lane;
+    bf16x8 rg[WD], rf[WD], r2a[WD2], r2b[WD2];
+#pragma unroll
+    for (int i = 0; i < WD; ++i) { rg[i] = wg[i * 64]; rf[i] = wf[i * 64]; }
+    // ---- GEMM1: [x(t-1)+dp; x(t)+dp; x(t+1)+dp; cond(t)] . W1^T, both row tiles
+    f32x16 ag[2], af[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { ag[q][r] = 0.f; af[q][r] = 0.f; }
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      bf16x8 a[2];
+      const int tap = ks / 16, cc = (ks % 16) * 16 + h * 8;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (tap < 3) {
+          const int wrow = min(max(32 * q + r32 + tap - 1, 0), WR - 1);
+          a[q] = *reinterpret_cast<const bf16x8*>(&XW[wrow * WST_LD + cc]);
+          if (tap == 0) a[q] = mlo[q] ? a[q] : z8;
+          if (tap == 2) a[q] = mhi[q] ? a[q] : z8;
+        } else {
+          a[q] = *reinterpret_cast<const bf16x8*>(&CW[(32 * q + r32) * WST_LD + cc]);
+        }
+      }
+      const bf16x8 bgt = rg[ks % WD], bft = rf[ks % WD];
+      if (ks + WD < KS1) {
+        rg[ks % WD] = wg[(ks + WD) * 64];
+        rf[ks % WD] = wf[(ks + WD) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ag[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], bgt, ag[q], 0, 0, 0);
+        af[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], bft, af[q], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WD2; ++i) { r2a[i] = wr[i * 64]; r2b[i] = wsk[i * 64]; }   // GEMM2's ring, under the gate
+    {
+      const float bgv = P.b1[(long long)l * 2 * C + n], bfv = P.b1[(long long)l * 2 * C + C + n];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int r = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          Gs[r * WST_LD + n] = (__bf16)gate_fast(ag[q][reg] + bgv, af[q][reg] + bfv);
+        }
+    }
+    __syncthreads();
+    // ---- GEMM2: residual tile nt = wave, skip tile nt = 8 + wave
+    f32x16 ar[2], as_[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { ar[q][r] = 0.f; as_[q][r] = 0.f; }
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) {
+      bf16x8 a[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) a[q] = *reinterpret_cast<const bf16x8*>(&Gs[(32 * q + r32) * WST_LD + ks * 16 + h * 8]);
+      const bf16x8 b0 = r2a[ks % WD2], b1 = r2b[ks % WD2];
+      if (ks + WD2 < KS2) {
+        r2a[ks % WD2] = wr[(ks + WD2) * 64];
+        r2b[ks % WD2] = wsk[(ks + WD2) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ar[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b0, ar[q], 0, 0, 0);
+        as_[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b1, as_[q], 0, 0, 0);
+      }
+    }
+    // ---- x = (x + o_res + b) / sqrt2 on the whole window; skip += o_skip + b on the output rows;
+    //      the next layer's bf16(x + dp) into XW (every wave is past its GEMM1 reads of XW)
+    const float brv = P.b2[(long long)l * 2 * C + n], bsv = P.b2[(long long)l * 2 * C + C + n];
+    const float rs2 = 0.70710678118654752440f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) xr[q][reg] = (xr[q][reg] + ar[q][reg] + brv) * rs2;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
+      SK[sko(i)] = SK[sko(i)] + as_[q][reg] + bsv;
+    }
+    if (j + 1 < P.nl) {
+      const float dA = P.dp[(long long)bA * P.dp_ld + (long long)(l + 1) * C + n];
+      const float dB = P.dp[(long long)bB * P.dp_ld + (long long)(l + 1) * C + n];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int r = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + r;
+          const float m = (R >= 0 && R < rows) ? 1.f : 0.f;
+          XW[r * WST_LD + n] = (__bf16)((xr[q][reg] + (R < RB ? dA : dB)) * m);
+        }
+    }
+    __syncthreads();   // XW written / Gs reads done before the next layer
+  }
+  // ---- output rows: x (layer l0 + nl's input) and the skip sum
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
+    const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    if (R < rows) {
+      P.xout[(long long)R * C + n] = xr[q][reg];
+      P.skip[(long long)R * C + n] = SK[sko(i)];
+    }
+  }
 }
 
 // ------------------------------------------------------------------ two-kernel residual layer (bf16)
@@ -620,7 +835,7 @@ __global__ void wn_xa_kernel(const float* __restrict__ x, const float* __restric
                              __bf16* __restrict__ xa, const float* __restrict__ cond, __bf16* __restrict__ condb,
                              int rows, int T, int C, int H) {
   const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i < (long long)rows * C) {
+  if (x && i < (long long)rows * C) {
     const long long R = i / C;
     const int c = (int)(i - R * C), b = (int)(R / T);
     const float4 v = *reinterpret_cast<const float4*>(x + i);
@@ -763,6 +978,27 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
                            dim3(256), 0, st, P);
         PD_LAUNCH_CHECK();
       }
+    }
+  } else if (h->W1f && h->stack_nl > 0 && h->cyc == 1 && H == WNF_C && T >= 64) {
+    // bf16, dilation 1: stack_nl residual layers per launch (wn_stack_bf16_kernel), x ping-pongs
+    __bf16* condb = reinterpret_cast<__bf16*>(ws + Lw.condb);
+    {
+      ProfScope ps("wn_condb", st);
+      hipLaunchKernelGGL(wn_xa_kernel, dim3(cdiv(((long long)rows * H + 3) / 4, 256)), dim3(256), 0, st, nullptr,
+                         nullptr, 0, nullptr, cond, condb, rows, T, C, H);
+      PD_LAUNCH_CHECK();
+    }
+    float* xb[2] = {x, ws + Lw.x2};
+    int k = 0;
+    for (int l0 = 0; l0 < Ly; l0 += h->stack_nl, ++k) {
+      WnStackArgs P{};
+      P.xin = xb[k & 1]; P.xout = xb[(k + 1) & 1]; P.skip = skip; P.condb = condb;
+      P.dp = dproj; P.dp_ld = Ly * C;
+      P.W1f = h->W1f; P.b1 = h->bl1; P.W2f = h->W2f; P.b2 = h->bl2;
+      P.rows = rows; P.T = T; P.l0 = l0; P.nl = std::min(h->stack_nl, Ly - l0); P.first = l0 == 0; P.L = Ly;
+      ProfScope ps("wn_stack", st);
+      hipLaunchKernelGGL(wn_stack_bf16_kernel, dim3(cdiv(rows, 32)), dim3(512), 0, st, P);
+      PD_LAUNCH_CHECK();
     }
   } else if (h->W1f) {
     // bf16, C == 256: one fused launch per residual layer, x ping-pongs x <-> x2
@@ -958,6 +1194,11 @@ int pd_wavenet_set_option(pd_wavenet* h, int option, int value) {
   if (option == PD_WN_OPT_KSPLIT) {
     PD_CHECK_ARG(value == 0 || value == 256 || value == 512, "PD_WN_OPT_KSPLIT is 0 (no split), 256 or 512");
     h->ksplit_blocks = value == 0 ? 1 : value;
+    return PD_OK;
+  }
+  if (option == PD_WN_OPT_STACK) {
+    PD_CHECK_ARG(value >= 0 && value <= 16, "PD_WN_OPT_STACK is 0 (one launch per layer) .. 16");
+    h->stack_nl = value;
     return PD_OK;
   }
   if (option == PD_WN_OPT_L2PF) {

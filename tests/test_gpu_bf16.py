@@ -225,13 +225,12 @@ def test_wavenet_two_kernel_vs_fused(cyc):
 
 
 
-@pytest.mark.parametrize("opts", [dict(lvc_pf=0, lvc_tpw=1), dict(lvc_pf=1, lvc_tpw=1), dict(lvc_pf=1, lvc_prio=1),
-                                  dict(lvc_pf=1, lvc_prio=3)])
+@pytest.mark.parametrize("opts", [dict(lvc_pf=0, lvc_tpw=1), dict(lvc_pf=1, lvc_tpw=1), dict(lvc_pf=1, lvc_prio=1)])
 @pytest.mark.parametrize("B,Tc", [(1, 1), (3, 5), (2, 9)])
 def test_fastdiff_lvc_schedule_variants(opts, B, Tc):
     """LVC-block variants that change only the schedule, not the arithmetic of a tile:
     FD_OPT_LVC_TPW=1 (16 waves, one 32-row tile each; with and without the next-layer kernel
-    prefetch) and FD_OPT_LVC_PRIO (static priority, staggered tile order for half the waves).
+    prefetch) and FD_OPT_LVC_PRIO (static priority for half the waves).
     The sample is bit-identical to the default kernel with the same prefetch setting, and within
     the bf16 bar of the oracle."""
     from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
@@ -249,3 +248,29 @@ def test_fastdiff_lvc_schedule_variants(opts, B, Tc):
     np.testing.assert_array_equal(outs[1], outs[0])
     ref = OF.fastdiff_sample(OF.fold_weight_norm(p), np.transpose(mel, (0, 2, 1)), xT, nz, b, a, s, st)
     assert_bf16_close(outs[1].reshape(ref.shape), ref, f"sampler {opts} B={B} Tc={Tc}")
+
+
+@pytest.mark.parametrize("stack", [1, 4, 7, 10, 16])
+@pytest.mark.parametrize("B,T", [(2, 64), (3, 101), (1, 250)])
+def test_wavenet_stack_bitexact(stack, B, T):
+    """PD_WN_OPT_STACK (wn_stack_bf16_kernel: `stack` residual layers per launch on a resident
+    64-frame window) against the one-layer fused kernel (PD_WN_OPT_LAYER=0): the same bf16
+    roundings and MFMA order, so the output is bit-identical -- ragged lengths put utterance
+    boundaries inside the windows (T = 64 is the smallest T the stack path takes), and 20 layers
+    run as uneven launch groups (7: 7 + 7 + 6).  Then within the bf16 bar of the fp32 path."""
+    torch.manual_seed(11)
+    net = WaveNet(80, 256, 20, 256, 1)
+    spec = torch.randn(B, 1, 80, T, device=DEV)
+    cond = torch.randn(B, 256, T, device=DEV)
+    steps = torch.tensor([3.0, 511.0, 77.0][:B], device=DEV)
+    outs = {}
+    for name, opts in (("layer", dict(layer=0)), ("stack", dict(stack=stack))):
+        m = WaveNet(80, 256, 20, 256, 1)
+        m.load_state_dict(net.state_dict())
+        m = m.to(DEV).set_compute_dtype("bf16").set_options(**opts)
+        outs[name] = m(spec, steps, cond).float().cpu().numpy()
+    np.testing.assert_array_equal(outs["stack"], outs["layer"])
+    m32 = WaveNet(80, 256, 20, 256, 1)
+    m32.load_state_dict(net.state_dict())
+    ref = m32.to(DEV)(spec, steps, cond).float().cpu().numpy()
+    assert_bf16_close(outs["stack"], ref, f"wavenet stack={stack} B={B} T={T}")

@@ -103,3 +103,21 @@ def test_bf16_full_dims_vs_oracle(wconv, T, B):
     for b in range(B):
         ref = ON.spec2wav(p, h, mel[b:b + 1], f0[b:b + 1], ri, nz[b:b + 1])[0]
         assert_bf16_close(wav[b], ref, f"nsf full dims T={T} wconv={wconv} b={b}")
+
+
+@pytest.mark.parametrize("T,B", [(24, 1), (37, 2), (1, 3)])
+def test_bf16_resblock_pair_bitexact(T, B):
+    """NSF_OPT_PAIR (one launch per ResBlock1 conv pair, the inner activation kept in LDS) against
+    the two-launch path: same bf16 roundings and MFMA order, so the waveform is bit-identical --
+    partial tiles at every stage (T = 37), T = 1 all halo, utterances side by side (B > 1)."""
+    h = dict(synth.NSF_DEFAULTS)
+    g, _ = _gen(h, 7)
+    rng = np.random.default_rng(5)
+    mel = torch.from_numpy(rng.normal(-2.0, 1.0, size=(B, T, 128)).astype(np.float32)).to(DEV)
+    f0 = torch.from_numpy(rng.uniform(60.0, 900.0, size=(B, T)).astype(np.float32)).to(DEV)
+    outs = []
+    for pair in (0, 1):
+        g.set_compute_dtype("bf16").set_options(pair=pair)
+        outs.append(g.synthesize(mel, f0, 2.30259, seed=9).cpu().numpy())
+    assert np.isfinite(outs[1]).all()
+    np.testing.assert_array_equal(outs[1], outs[0])
