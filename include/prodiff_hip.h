@@ -95,9 +95,10 @@ void pd_wavenet_destroy(pd_wavenet* h);
 /* PD_WN_OPT_L2PF (bf16 fused layer): 1 (default) each layer launch pulls the next layer's weight
  * fragments into every XCD's L2 while it runs; 0 = off. */
 #define PD_WN_OPT_L2PF 2
-/* PD_WN_OPT_STACK (bf16, C = H = 256, dilation_cycle_length 1, T >= 64): n = 1..16 residual layers per
- * launch (wn_stack_bf16_kernel: a 64-frame window per 32 output frames stays resident for the
- * n layers; bit-identical to the one-layer kernel); 0 = one launch per layer. */
+/* PD_WN_OPT_STACK (bf16, C = H = 256, dilation_cycle_length 1, T >= 64, PD_WN_OPT_LAYER 2): n = 1..16
+ * residual layers per launch (wn_stack_bf16_kernel: a 64-frame window per 32 output frames stays
+ * resident for the n layers; bit-identical to the one-layer kernel), default 10; 0 = one launch
+ * per layer. */
 #define PD_WN_OPT_STACK 3
 int pd_wavenet_set_option(pd_wavenet* h, int option, int value);
 /* S = number of reverse steps the workspace must serve (1 for pd_wavenet_forward). */

@@ -36,7 +36,10 @@ struct pd_wavenet {
   int layer_mode = 2;
   int ksplit_blocks = 512;   // PD_WN_OPT_KSPLIT: fp32 layer GEMMs split K up to this many blocks
   int l2_prefetch = 1;       // PD_WN_OPT_L2PF: fused layer l pulls layer l + 1's weights into L2
-  int stack_nl = 0;          // PD_WN_OPT_STACK: residual layers per wn_stack_bf16_kernel launch (0 = off)
+  // PD_WN_OPT_STACK: residual layers per wn_stack_bf16_kernel launch when layer_mode is 2 (auto);
+  // 0 = off.  r04 (C3, same box): 10 layers per launch 20.7-21.0 us per layer vs 25.7-26.6 for the
+  // one-layer kernel; 7 layers 20.3 us (profiles/r04_ab/wn_stack_ab.txt)
+  int stack_nl = 10;
 };
 
 namespace {
@@ -979,7 +982,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
         PD_LAUNCH_CHECK();
       }
     }
-  } else if (h->W1f && h->stack_nl > 0 && h->cyc == 1 && H == WNF_C && T >= 64) {
+  } else if (h->W1f && h->stack_nl > 0 && h->layer_mode == 2 && h->cyc == 1 && H == WNF_C && T >= 64) {
     // bf16, dilation 1: stack_nl residual layers per launch (wn_stack_bf16_kernel), x ping-pongs
     __bf16* condb = reinterpret_cast<__bf16*>(ws + Lw.condb);
     {

@@ -264,7 +264,7 @@ def test_wavenet_stack_bitexact(stack, B, T):
     cond = torch.randn(B, 256, T, device=DEV)
     steps = torch.tensor([3.0, 511.0, 77.0][:B], device=DEV)
     outs = {}
-    for name, opts in (("layer", dict(layer=0)), ("stack", dict(stack=stack))):
+    for name, opts in (("layer", dict(layer=0, stack=0)), ("stack", dict(stack=stack))):
         m = WaveNet(80, 256, 20, 256, 1)
         m.load_state_dict(net.state_dict())
         m = m.to(DEV).set_compute_dtype("bf16").set_options(**opts)
