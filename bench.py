@@ -177,6 +177,34 @@ def traffic_workload(d, fname):
     return ("C5" if "c5" in os.path.basename(fname) else "C3"), 8, 861
 
 
+def sq_utilisation(config):
+    """Per-kernel MFMA-busy / VALU-busy fractions of the newest SQ-counter summary of this config
+    (profiles/rNN_*/<config>_sq.json, written by tools/sq_summary.py from separate rocprofv3 SQ
+    passes over a short bench of the same workload).  None when no summary covers the config."""
+    import glob
+    import re
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "r*", "*_sq.json")):
+        m = re.search(r"profiles/r(\d+)_", f.replace(os.sep, "/"))
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") != config or not m:
+            continue
+        key = (int(m.group(1)), os.path.getmtime(f))
+        if best is None or key > best[0]:
+            best = (key, f, d)
+    if best is None:
+        return None
+    _, f, d = best
+    ks = [{k: r.get(k) for k in ("kernel", "avg_us_profiled", "mfma_busy", "valu_busy", "wait_any", "wait_inst")}
+          for r in d["kernels"]]
+    return {"source": os.path.relpath(f, ROOT), "kernels": ks,
+            "note": "rocprofv3 SQ counters, separate passes: mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x cycles), "
+                    "valu_busy = 4 SQ_ACTIVE_INST_VALU / (SIMDs x cycles), wait_* = fractions of SQ_WAVE_CYCLES"}
+
+
 def pmc_traffic(tag, config, batch, frames, path=None):
     """HBM bytes per launch of `tag`'s kernel(s) from the newest committed PMC summary
     measured on the SAME workload (config, per-GPU batch, frames) -- profiles/rNN_vMM_traffic.json,
@@ -583,7 +611,9 @@ def main():
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
                         "frac": round(ach / peak_tf, 4)}
         traffic, tsrc = pmc_traffic(dom, cfg_name, B, T, args.traffic)
-        roofline.update({"traffic": round(traffic) if traffic else None, "traffic_source": tsrc, "kernel": dom,
+        roofline.update({"bound_basis": "model estimate: algorithmic intensity vs the ridge; the measured limiter "
+                                        "is in `utilisation` (MFMA / VALU busy, wait fractions)",
+                         "traffic": round(traffic) if traffic else None, "traffic_source": tsrc, "kernel": dom,
                          "flop_per_launch": fl[dom], "bytes_per_launch": by.get(dom),
                          "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(ridge, 1),
                          "avg_launch_us": round(ms / cnt * 1e3, 2), "launches": cnt,
@@ -619,6 +649,7 @@ def main():
         "x_realtime": round(audio_s / dt, 1),
         "model_tflops": round(step_fl * args.steps / dt / 1e12, 2),
         "roofline": roofline,
+        "utilisation": sq_utilisation(cfg_name) if not dry else None,
         "kernels": kernels,
         "phases": phases,
         "kernels_source": (f"untimed {'eager ' if graph_prof else ''}pass of {nprof} steps, every launch bracketed by "

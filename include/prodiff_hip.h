@@ -217,6 +217,7 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 /* 8, 9: reserved (r03's skewed persistent LVC kernel, removed: measured slower) */
 #define FD_OPT_LVC_TPW 10     /* 32-row tiles per wave of the 384-sample hop >= 32 LVC blocks: 2 (8 waves) or 1 (16 waves) */
 #define FD_OPT_LVC_PRIO 11    /* 1: s_setprio(1) for the second half of an LVC block's waves */
+/* 12: reserved (r04's persistent LVC kernel with LDS-DMA prefetch, removed: measured slower) */
 int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */

@@ -1062,9 +1062,14 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
 // r03 (SQ counters, C3): the audio block was issue-bound -- 1.1k VALU + 0.6k SALU instructions
 // per wave at 3 waves per SIMD -- so the first conv keeps its weights in registers and the
 // conv epilogues apply the utterance-edge mask only on edge tiles.
-constexpr int DB_TS = 128, DB_ROWS = 168, DB_LD = 40;
+// r04: 5 waves -- the two dilated stages are 5 row tiles each, so with 4 waves one wave ran
+// two tiles while three idled at the barrier; the 5th wave sits out only the 4-tile final conv.
+#ifndef DB_NW
+#define DB_NW 5
+#endif
+constexpr int DB_TS = 128, DB_ROWS = 168, DB_LD = 40, DB_NT = 64 * DB_NW;
 template <int AF>
-__global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restrict__ in, float* __restrict__ out,
+__global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(4))) void dblock_bf16_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                           const __bf16* __restrict__ W0, const float* __restrict__ b0,
                                                           const __bf16* __restrict__ W1, const float* __restrict__ b1,
                                                           const __bf16* __restrict__ W2, const float* __restrict__ b2,
@@ -1078,21 +1083,18 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   __bf16* H2 = U0;
   // audio input (the first DBlock): the block's samples t = f i + k - 3 of its rows, staged once
   constexpr int DB_AUM = (DB_TS + 14) * AF + 8;
-  constexpr int DB_AUI = (DB_AUM + 255) / 256;
+  constexpr int DB_AUI = (DB_AUM + DB_NT - 1) / DB_NT;
   __shared__ float AU[DB_AUM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, i0 = blockIdx.x * DB_TS, ib = i0 - 7;
   const long long Lin = (long long)Lout * f;
   const float* src = in + (long long)b * Lin * CI;
-  // every stage's weight fragments first: their L2 round trip overlaps the staging's
+  // the first stage's weight fragments first: their L2 round trip overlaps the staging's;
+  // the later stages' are issued after the staging stores (r04: all 20 fragments live across
+  // the staging kept the kernel at 148 VGPRs, 3 waves per SIMD)
   bf16x8 wf0[6], wf1[6], wf2[8];
 #pragma unroll
-  for (int kk = 0; kk < 6; ++kk) {
-    wf0[kk] = *reinterpret_cast<const bf16x8*>(W0 + r32 * 96 + kk * 16 + h * 8);
-    wf1[kk] = *reinterpret_cast<const bf16x8*>(W1 + r32 * 96 + kk * 16 + h * 8);
-  }
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) wf2[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
+  for (int kk = 0; kk < 6; ++kk) wf0[kk] = *reinterpret_cast<const bf16x8*>(W0 + r32 * 96 + kk * 16 + h * 8);
   const float bv0 = b0[r32], bv1 = b1[r32], bv2 = b2[r32];
   if (audio) {
     // input = first_conv(audio) at t = f ii (FastDiff_model.py:90), recomputed: no a0 tensor.
@@ -1106,12 +1108,12 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
     float av[DB_AUI];
 #pragma unroll
     for (int it = 0; it < DB_AUI; ++it) {
-      const long long t = t0 + tid + 256 * it;
+      const long long t = t0 + tid + DB_NT * it;
       av[it] = au[t < 0 ? 0 : t >= Lin ? Lin - 1 : t];
     }
 #pragma unroll
     for (int it = 0; it < DB_AUI; ++it) {
-      const int i = tid + 256 * it;
+      const int i = tid + DB_NT * it;
       const long long t = t0 + i;
       if (i < na) AU[i] = (t >= 0 && t < Lin) ? av[it] : 0.f;
     }
@@ -1119,7 +1121,7 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   }
   // staging: every thread's (<= DB_NI) items are loaded before any is converted, so their
   // strided HBM reads are in flight together (one round trip per block, not one per item)
-  constexpr int DB_NI = (DB_ROWS * 8 + 255) / 256;
+  constexpr int DB_NI = (DB_ROWS * 8 + DB_NT - 1) / DB_NT;
   float4 sv[DB_NI];
   // a thread's channel quad q is the same for all its items: its first-conv weights (7 taps x
   // 4 channels, fw is [c][tap]) and biases live in registers
@@ -1135,7 +1137,7 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   }
 #pragma unroll
   for (int u = 0; u < DB_NI; ++u) {
-    const int i = tid + 256 * u;
+    const int i = tid + DB_NT * u;
     const int p = i >> 3, q = (i & 7) * 4, ii = ib + p;
     const bool ok = i < DB_ROWS * 8 && p < DB_TS + 14 && ii >= 0 && ii < Lout;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1163,7 +1165,7 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   }
 #pragma unroll
   for (int u = 0; u < DB_NI; ++u) {
-    const int i = tid + 256 * u;
+    const int i = tid + DB_NT * u;
     if (i >= DB_ROWS * 8) continue;
     const int p = i >> 3, q = (i & 7) * 4;
     float4 v = sv[u];
@@ -1172,10 +1174,14 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
     v.z = v.z >= 0.f ? v.z : 0.2f * v.z; v.w = v.w >= 0.f ? v.w : 0.2f * v.w;
     *reinterpret_cast<bf16x4*>(&U0[p * DB_LD + q]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
   }
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) wf1[kk] = *reinterpret_cast<const bf16x8*>(W1 + r32 * 96 + kk * 16 + h * 8);
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) wf2[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
   __syncthreads();
   // one dilated 32->32 conv stage over 5 row tiles starting at local row `first`
   auto stage = [&](const __bf16* In, __bf16* Out, const bf16x8 (&wf)[6], float bv, int first, int dil) {
-    for (int mt = wave; mt < 5; mt += 4) {
+    for (int mt = wave; mt < 5; mt += DB_NW) {
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -1207,7 +1213,7 @@ __global__ __launch_bounds__(256) void dblock_bf16_kernel(const float* __restric
   stage(H1, H2, wf1, bv1, 3, 2);    // h2 on p in [3, 163)
   __syncthreads();
   // out on p in [7, 135): conv_d4(h2) ++ residual_dense(x), K = 96 + 32
-  {
+  if (wave < 4) {
     const bf16x8 (&wf)[8] = wf2;
     const float bv = bv2;
     const int mt = wave;   // 4 tiles, one per wave
@@ -1455,6 +1461,9 @@ constexpr int KP_THREADS = 512;
 #ifndef KP_PROBE
 #define KP_PROBE 0
 #endif
+#ifndef KP_STAGGER
+#define KP_STAGGER 1
+#endif
 #ifndef KP_AUX
 #define KP_AUX 0   // plain K stores: the lines stay on-die for the LVC block that reads them next (r03 A/B: non-temporal (2) made kp ~4% and the next LVC launch ~4% slower)
 #endif
@@ -1489,7 +1498,14 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
       const int c = tid + KP_THREADS * i, fl = c / 24, v = (c - fl * 24) * 8, tap = v >> 6, ch = v & 63;
       const int R = R0 + fl, Rc = R < rows ? R : rows - 1;
       int b = b0, f = f00 + (Rc - R0);
-      while (f >= Tc) { f -= Tc; ++b; }   // at most KP_F / Tc steps
+      if (Tc >= KP_F) {                   // (uniform) the item crosses at most one utterance end
+        const bool nx = f >= Tc;
+        f -= nx ? Tc : 0;
+        b += nx ? 1 : 0;
+      } else {
+        b = Rc / Tc;
+        f = Rc - b * Tc;
+      }
       const int ff = f + tap - 1;
       const int ffc = ff < 0 ? 0 : ff >= Tc ? Tc - 1 : ff;     // clamped: unconditional load
       hv[i] = *reinterpret_cast<const uint4*>(hin + ((long long)b * Tc + ffc) * HK + ch);
@@ -1536,11 +1552,9 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
         __builtin_amdgcn_make_buffer_rsrc(Kf + (long long)layer * rows * KPERLAYER, 0, rows * KPERLAYER * 2, 0x00020000);
 #endif
     const __bf16* hs = Hs[buf];
-#pragma unroll
-    for (int ft = 0; ft < KP_F / 32; ++ft) {   // unrolled: hipcc counts the stores in vmcnt
-      // C[n][frame]: lane owns frame r32, rows n = 32j + 8g + 4h + (0..3); the accumulators
-      // start from the rows' biases, so the epilogue is a conversion only
-      f32x16 acc[2];
+    // C[n][frame]: lane owns frame r32, rows n = 32j + 8g + 4h + (0..3); the accumulators start
+    // from the rows' biases, so the epilogue is a conversion only
+    auto mma = [&](int ft, f32x16 (&acc)[2]) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1558,6 +1572,8 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
         acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[12 + kk], hb, acc[1], 0, 0, 0);
 #endif
       }
+    };
+    auto epi = [&](int ft, const f32x16 (&acc)[2]) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1576,6 +1592,27 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
                                                ((f0 + fl) * KPERLAYER + n0 + ch) * 2, 0, KP_AUX);
       }
       __builtin_amdgcn_wave_barrier();      // the next frame tile rewrites ot
+    };
+    // (unrolled: hipcc counts the stores in vmcnt.)  Waves 4..7 -- each one's SIMD partner is
+    // wave - 4 -- run one frame tile behind on their epilogues (KP_STAGGER): a tile's
+    // conversion, LDS transpose and stores then issue beside the partner's MFMAs instead of in
+    // the same phase (MI355X_MICROARCH.md "Two waves per SIMD", item 9).
+    f32x16 acc0[2], acc1[2];
+    if (!KP_STAGGER || wave < 4) {
+#pragma unroll
+      for (int ft = 0; ft < KP_F / 32; ++ft) {
+        mma(ft, acc0);
+        epi(ft, acc0);
+      }
+    } else {
+      mma(0, acc0);
+#pragma unroll
+      for (int ft = 1; ft < KP_F / 32; ++ft) {
+        if (ft & 1) { mma(ft, acc1); epi(ft - 1, acc0); }
+        else { mma(ft, acc0); epi(ft - 1, acc1); }
+      }
+      if ((KP_F / 32 - 1) & 1) epi(KP_F / 32 - 1, acc1);
+      else epi(KP_F / 32 - 1, acc0);
     }
     // the next item's frames into the other buffer, whose readers (the previous item) are
     // past the last barrier; the barrier makes them visible
@@ -1777,11 +1814,11 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
   if (const __bf16* w0 = lookup_bf16(D.c0_w)) {   // bf16: one fused launch, intermediates in LDS
     ProfScope ps("fd_dblock_fused", st);
     if (audio && f <= 4)
-      hipLaunchKernelGGL(dblock_bf16_kernel<4>, dim3(cdiv(Tout, DB_TS), B), dim3(256), 0, st, in, out, w0, D.c0_b,
+      hipLaunchKernelGGL(dblock_bf16_kernel<4>, dim3(cdiv(Tout, DB_TS), B), dim3(DB_NT), 0, st, in, out, w0, D.c0_b,
                          lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, audio, m->first_w,
                          m->first_b);
     else
-      hipLaunchKernelGGL(dblock_bf16_kernel<16>, dim3(cdiv(Tout, DB_TS), B), dim3(256), 0, st, in, out, w0, D.c0_b,
+      hipLaunchKernelGGL(dblock_bf16_kernel<16>, dim3(cdiv(Tout, DB_TS), B), dim3(DB_NT), 0, st, in, out, w0, D.c0_b,
                          lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, audio,
                          audio ? m->first_w : nullptr, audio ? m->first_b : nullptr);
     PD_LAUNCH_CHECK();

@@ -230,7 +230,7 @@ def test_wavenet_two_kernel_vs_fused(cyc):
 def test_fastdiff_lvc_schedule_variants(opts, B, Tc):
     """LVC-block variants that change only the schedule, not the arithmetic of a tile:
     FD_OPT_LVC_TPW=1 (16 waves, one 32-row tile each; with and without the next-layer kernel
-    prefetch) and FD_OPT_LVC_PRIO (static priority for half the waves).
+    prefetch), and FD_OPT_LVC_PRIO (static priority for half the waves).
     The sample is bit-identical to the default kernel with the same prefetch setting, and within
     the bf16 bar of the oracle."""
     from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
