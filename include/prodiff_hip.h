@@ -100,6 +100,13 @@ void pd_wavenet_destroy(pd_wavenet* h);
  * resident for the n layers; bit-identical to the one-layer kernel), default 10; 0 = one launch
  * per layer. */
 #define PD_WN_OPT_STACK 3
+/* PD_WN_OPT_STACK_RO: output frames per wn_stack_bf16_kernel block, 16..32; 0 (default) = 32. */
+#define PD_WN_OPT_STACK_RO 4
+/* 5: reserved (r04's in-kernel split-K reduction by arrival counters, removed: measured slower) */
+/* PD_WN_OPT_STACK_FUSE (bf16 stack path): 1 (default) the input projection runs inside the first
+ * stack launch and, in pd_prodiff_sample, the skip head + output projection + posterior update
+ * inside the last one (same roundings and k order as the separate launches); 0 = separate launches. */
+#define PD_WN_OPT_STACK_FUSE 6
 int pd_wavenet_set_option(pd_wavenet* h, int option, int value);
 /* S = number of reverse steps the workspace must serve (1 for pd_wavenet_forward). */
 size_t pd_wavenet_workspace_size(const pd_wavenet* h, int B, int T, int S);
@@ -218,6 +225,7 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 #define FD_OPT_LVC_TPW 10     /* 32-row tiles per wave of the 384-sample hop >= 32 LVC blocks: 2 (8 waves) or 1 (16 waves) */
 #define FD_OPT_LVC_PRIO 11    /* 1: s_setprio(1) for the second half of an LVC block's waves */
 /* 12: reserved (r04's persistent LVC kernel with LDS-DMA prefetch, removed: measured slower) */
+/* 13: reserved (r04's multi-tile fused-DBlock blocks, removed: measured slower) */
 int fd_set_option(fd_model* m, int option, int value);
 
 /* w[co,:] = g[co] * v[co,:] / ||v[co,:]||  (torch.nn.utils.weight_norm, dim 0). */

@@ -40,6 +40,8 @@ struct pd_wavenet {
   // 0 = off.  r04 (C3, same box): 10 layers per launch 20.7-21.0 us per layer vs 25.7-26.6 for the
   // one-layer kernel; 7 layers 20.3 us (profiles/r04_ab/wn_stack_ab.txt)
   int stack_nl = 10;
+  int stack_ro = 0;          // PD_WN_OPT_STACK_RO: output rows per stack block (0 = auto, else 16..32)
+  int stack_fuse = 1;        // PD_WN_OPT_STACK_FUSE: input projection / sampler output stage inside the stack launches
 };
 
 namespace {
@@ -331,6 +333,27 @@ struct WnStackArgs {
   const __bf16* W2f;      // [L][2C/32][C/16][64][8]
   const float* b2;        // [L][2C]
   int rows, T, l0, nl, first, L;
+  int ro;                 // output rows per block (<= 32): window rows [16, 16 + ro)
+  // PD_WN_OPT_STACK_FUSE, first launch: x = relu(W_in spec + b_in) of the window rows computed
+  // here (spec [rows][M] fp32, Winb [C][ldw_in] bf16, M <= ldw_in <= 128) instead of read
+  const float* spec;
+  const __bf16* Winb;
+  const float* b_in;
+  int M, ldw_in;
+  // last launch of a sampler pass: hs = relu(W_s (skip / sqrt L) + b_s), x0 = W_o hs + b_o and
+  // the posterior mel = c1 x0 + c2 mel + sigma n on the output rows (Wsb [C][C], Wob [M][C] bf16)
+  const __bf16* Wsb;
+  const float* bs;
+  const __bf16* Wob;
+  const float* bo;
+  float* mel;
+  float skip_scale, c1, c2, sigma;
+  const float* noise;
+  long long noise_bs;
+  int noise_ld;
+  unsigned long long seed;
+  unsigned stream_id;
+  const int* uid;
 };
 constexpr int WST_LD = WNF_C + 8;                    // LDS row: 528 B, conflict-free b128 reads
 #ifndef WST_WD
@@ -340,6 +363,8 @@ constexpr int WST_LD = WNF_C + 8;                    // LDS row: 528 B, conflict
 // skip tiles w / 8 + w of GEMM2, as wn_layer_bf16_kernel.  r04: a 4-wave variant (one wave per
 // SIMD, 12-deep rings) ran 24 us per layer against 21 us for this one (no partner wave to issue
 // beside a wave's MFMA-dependent epilogues).
+// IN: the fused input projection (first launch); TAIL: the fused sampler output stage (last launch)
+template <bool IN, bool TAIL>
 __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs P) {
   constexpr int C = WNF_C, H = WNF_C, K1 = 3 * C + H, KS1 = K1 / 16, KS2 = C / 16, WD = WST_WD, WD2 = 4;
   constexpr int WR = 64;                             // window rows: 2 MFMA row tiles
@@ -349,22 +374,34 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   __shared__ float SK[32 * WNF_C];                                   // skip sum of the output rows (lane-private entries)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int rows = P.rows, T = P.T;
-  const int R0 = blockIdx.x * 32, W0 = R0 - 16;      // window row 0
+  const int R0 = blockIdx.x * P.ro, W0 = R0 - 16;    // window row 0
   const int n = wave * 32 + r32;                     // this lane's residual / skip column
   // T >= 64 (the host's condition) puts at most two utterances, bA and bB, in the window
   const int bA = min(max(W0, 0), rows - 1) / T, RB = (bA + 1) * T;   // rows >= RB: utterance bB
   const int bB = min(bA + 1, (rows - 1) / T);
   // ---- staging: window rows of bf16(x + dp_l0) and bf16(cond); zero outside [0, rows)
+  if constexpr (!IN) {
 #pragma unroll
-  for (int it = 0; it < WR * 64 / 512; ++it) {
-    const int i = tid + it * 512, wr = i >> 6, c = (i & 63) * 4, R = W0 + wr;
-    const int Rc = min(max(R, 0), rows - 1);
-    const float4 v = *reinterpret_cast<const float4*>(P.xin + (long long)Rc * C + c);
-    const int b = Rc < RB ? bA : bB;
-    const float4 d = *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + (long long)P.l0 * C + c);
-    const float m = (R >= 0 && R < rows) ? 1.f : 0.f;
-    *reinterpret_cast<bf16x4*>(&XW[wr * WST_LD + c]) =
-        bf16x4{(__bf16)((v.x + d.x) * m), (__bf16)((v.y + d.y) * m), (__bf16)((v.z + d.z) * m), (__bf16)((v.w + d.w) * m)};
+    for (int it = 0; it < WR * 64 / 512; ++it) {
+      const int i = tid + it * 512, wr = i >> 6, c = (i & 63) * 4, R = W0 + wr;
+      const int Rc = min(max(R, 0), rows - 1);
+      const float4 v = *reinterpret_cast<const float4*>(P.xin + (long long)Rc * C + c);
+      const int b = Rc < RB ? bA : bB;
+      const float4 d = *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + (long long)P.l0 * C + c);
+      const float m = (R >= 0 && R < rows) ? 1.f : 0.f;
+      *reinterpret_cast<bf16x4*>(&XW[wr * WST_LD + c]) =
+          bf16x4{(__bf16)((v.x + d.x) * m), (__bf16)((v.y + d.y) * m), (__bf16)((v.z + d.z) * m), (__bf16)((v.w + d.w) * m)};
+    }
+  } else {
+    // fused input projection: bf16(spec) of the window rows into Gs (k >= M zero, as the GEMM
+    // engine's padded K chunks)
+    const int nq = P.ldw_in / 4;
+    for (int i = tid; i < WR * nq; i += 512) {
+      const int wr = i / nq, c = (i - wr * nq) * 4, Rc = min(max(W0 + wr, 0), rows - 1);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c < P.M) v = *reinterpret_cast<const float4*>(P.spec + (long long)Rc * P.M + c);
+      *reinterpret_cast<bf16x4*>(&Gs[wr * WST_LD + c]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    }
   }
 #pragma unroll
   for (int it = 0; it < WR * 32 / 512; ++it) {
@@ -378,17 +415,55 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   // output rows (tile 0 regs 8..15 = window rows 16..31, tile 1 regs 0..7 = window rows 32..47)
   // in LDS, entries only this lane touches
   float xr[2][16];
+  if constexpr (IN) {
+    // x = relu(W_in . bf16(spec) + b_in): the GEMM engine's k order (ldw_in / 16 k-steps)
+    bf16x8 wi[8];
+    const int nks = P.ldw_in / 16;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      if (ks < nks) wi[ks] = *reinterpret_cast<const bf16x8*>(P.Winb + (long long)n * P.ldw_in + ks * 16 + h * 8);
+    __syncthreads();
+    const float bi = P.b_in[n];
+    const float dA0 = P.dp[(long long)bA * P.dp_ld + (long long)P.l0 * C + n];
+    const float dB0 = P.dp[(long long)bB * P.dp_ld + (long long)P.l0 * C + n];
+    // lane column / half through opaque moves: the XW addresses and row masks below equal the
+    // layer epilogue's, and hipcc kept them live across the layer loop (spills)
+    int no, ho;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(no) : "v"(n));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ho) : "v"(h));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        if (ks < nks)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              *reinterpret_cast<const bf16x8*>(&Gs[(32 * q + r32) * WST_LD + ks * 16 + h * 8]), wi[ks], acc, 0, 0, 0);
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int r = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * ho, R = W0 + r;
+        const float x = act_apply(acc[reg] + bi, ACT_RELU, 0.f);
+        const float m = (R >= 0 && R < rows) ? 1.f : 0.f;
+        xr[q][reg] = x;
+        XW[r * WST_LD + no] = (__bf16)((x + (min(max(R, 0), rows - 1) < RB ? dA0 : dB0)) * m);
+      }
+    }
+  }
   auto sko = [&](int i) {   // SK index of output value i
     const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
     return (32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h - 16) * C + n;
   };
+  if constexpr (!IN) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      xr[q][reg] = P.xin[(long long)min(max(R, 0), rows - 1) * C + n];
-    }
+      for (int reg = 0; reg < 16; ++reg) {
+        const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        xr[q][reg] = P.xin[(long long)min(max(R, 0), rows - 1) * C + n];
+      }
+  }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
@@ -511,12 +586,74 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
     }
     __syncthreads();   // XW written / Gs reads done before the next layer
   }
-  // ---- output rows: x (layer l0 + nl's input) and the skip sum
+  if constexpr (TAIL) {
+    // ---- fused tail: skip head, output projection and posterior on the output rows, with the
+    //      GEMM engine's roundings and k order (A = bf16(activation), 16 k-steps of 16)
+    bf16x8 wsf[16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) wsf[ks] = *reinterpret_cast<const bf16x8*>(P.Wsb + (long long)n * C + ks * 16 + h * 8);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {   // window rows 16..47 -> XW rows 0..31
+      const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
+      const int wrow = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      XW[(wrow - 16) * WST_LD + n] = (__bf16)(SK[sko(i)] * P.skip_scale);
+    }
+    __syncthreads();
+    {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&XW[r32 * WST_LD + ks * 16 + h * 8]),
+                                                      wsf[ks], acc, 0, 0, 0);
+      const float bsv = P.bs[n];
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg)
+        Gs[((reg & 3) + 8 * (reg >> 2) + 4 * h) * WST_LD + n] = (__bf16)act_apply(acc[reg] + bsv, ACT_RELU, 0.f);
+    }
+    __syncthreads();
+    const int col = wave * 32 + r32, M = P.M;
+    if (wave * 32 < M) {   // wave-uniform
+      const int colc = min(col, M - 1);
+      bf16x8 wof[16];
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) wof[ks] = *reinterpret_cast<const bf16x8*>(P.Wob + (long long)colc * C + ks * 16 + h * 8);
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&Gs[r32 * WST_LD + ks * 16 + h * 8]),
+                                                      wof[ks], acc, 0, 0, 0);
+      const float bov = P.bo[colc];
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + 16 + row;
+        if (row < P.ro && R < rows && col < M) {
+          // prodiff.py:106-126 (gemm.h EPI_POSTERIOR): x = c1 x0 + c2 x_t + sigma n
+          const int b = R / T, t = R - b * T;
+          const float v = acc[reg] + bov;
+          const float xt = P.mel[(long long)R * M + col];
+          float x = P.c1 * v + P.c2 * xt;
+          if (P.sigma != 0.f) {
+            const float z = P.noise ? P.noise[(long long)b * P.noise_bs + (long long)t * P.noise_ld + col]
+                                    : philox_normal_u(P.seed, utt_id(P.uid, b), (unsigned)(t * M + col), P.stream_id);
+            x += P.sigma * z;
+          }
+          P.mel[(long long)R * M + col] = x;
+        }
+      }
+    }
+  }
+  // ---- output rows: x (layer l0 + nl's input) and the skip sum (not after a fused tail: the
+  //      last layer's x feeds nothing, and the skip sum was consumed here)
+  if constexpr (TAIL) return;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
-    const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-    if (R < rows) {
+    const int wrow = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + wrow;
+    if (R < rows && wrow - 16 < P.ro) {
       P.xout[(long long)R * C + n] = xr[q][reg];
       P.skip[(long long)R * C + n] = SK[sko(i)];
     }
@@ -922,17 +1059,41 @@ int launch_small_gemm(const GemmArgs& a, hipStream_t st, const char* tag) {
   return launch_gemm<1, 1, 1, 4, EPI, ID>(a, st, tag);
 }
 
+// A ProDiff sampler pass's output stage (prodiff.py:106-126) for wavenet_core to fuse into the
+// last stack launch: x0 = W_out relu(W_skip skip / sqrt(L) + b) + b_out, then the posterior update.
+struct StackTail {
+  float* mel;
+  float c1, c2, sigma;
+  const float* noise;
+  long long noise_bs;
+  int noise_ld;
+  unsigned long long seed;
+  unsigned stream_id;
+  const int* uid;
+};
+
 // Input projection + residual stack + skip head.  xin: time-major [B][T][M];
-// cond: time-major [B][T][H]; dproj: [B][L][C].  Leaves relu(skip head) in ws.hs.
+// cond: time-major [B][T][H]; dproj: [B][L][C].  Leaves relu(skip head) in ws.hs -- or, when
+// `tail` is given and the stack kernel fuses it (PD_WN_OPT_STACK_FUSE), applies the whole output
+// stage itself and sets *tail_done.
 int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float* xin,
-                 const float* cond, const float* dproj, int B, int T, hipStream_t st) {
+                 const float* cond, const float* dproj, int B, int T, hipStream_t st,
+                 const StackTail* tail = nullptr, bool* tail_done = nullptr) {
   const int M = h->M, H = h->H, C = h->C, Ly = h->L;
   const long long BTs = (long long)T;
   float* x = ws + Lw.x;
   float* g = ws + Lw.g;
   float* skip = ws + Lw.skip;
   float* hs = ws + Lw.hs;
-  {  // x = relu(W_in spec + b)   (wavenet.py:108-111)
+  if (tail_done) *tail_done = false;
+  const bool stack = h->W1f && h->stack_nl > 0 && h->layer_mode == 2 && h->cyc == 1 && H == WNF_C && T >= 64;
+  // fused input projection / output stage: bf16 mirrors of W_in, W_skip, W_out present
+  const __bf16* Winb = lookup_bf16(h->Win);
+  const __bf16* Wsb = lookup_bf16(h->Ws);
+  const __bf16* Wob = lookup_bf16(h->Wo);
+  const bool fuse_in = stack && h->stack_fuse && Winb && h->ldw_in <= 128 && M % 4 == 0;
+  const bool fuse_tail = fuse_in && tail && Wsb && Wob && M <= 8 * 32 && C == WNF_C && Ly > h->stack_nl;
+  if (!fuse_in) {  // x = relu(W_in spec + b)   (wavenet.py:108-111)
     GemmArgs a = make_gemm(B, T, C, h->Win, h->ldw_in, h->b_in, x, BTs * C, C);
     add_seg(a, make_seg(xin, BTs * M, M, M, 0));
     a.act = ACT_RELU;
@@ -983,7 +1144,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
         PD_LAUNCH_CHECK();
       }
     }
-  } else if (h->W1f && h->stack_nl > 0 && h->layer_mode == 2 && h->cyc == 1 && H == WNF_C && T >= 64) {
+  } else if (stack) {
     // bf16, dilation 1: stack_nl residual layers per launch (wn_stack_bf16_kernel), x ping-pongs
     __bf16* condb = reinterpret_cast<__bf16*>(ws + Lw.condb);
     {
@@ -1000,8 +1161,26 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       P.dp = dproj; P.dp_ld = Ly * C;
       P.W1f = h->W1f; P.b1 = h->bl1; P.W2f = h->W2f; P.b2 = h->bl2;
       P.rows = rows; P.T = T; P.l0 = l0; P.nl = std::min(h->stack_nl, Ly - l0); P.first = l0 == 0; P.L = Ly;
+      // output rows per block (PD_WN_OPT_STACK_RO, default 32).  r04: spreading C3's 6888 rows over
+      // all 256 CUs (27 rows per block) measured slower than 216 blocks of 32 (214 vs 202-205 us per
+      // 10 layers, profiles/r04_ab/): every block streams each layer's 1.3 MB of weights from its
+      // XCD's L2, and 32 blocks per XCD instead of 27 share that L2's bandwidth
+      P.ro = h->stack_ro > 0 ? h->stack_ro : 32;
+      if (fuse_in && l0 == 0) {
+        P.spec = xin; P.Winb = Winb; P.b_in = h->b_in; P.M = M; P.ldw_in = h->ldw_in;
+      }
+      if (fuse_tail && l0 + P.nl >= Ly) {   // (not the first launch: it reads mel, this one writes it)
+        P.Wsb = Wsb; P.bs = h->bs; P.Wob = Wob; P.bo = h->bo; P.M = M;
+        P.skip_scale = 1.0f / sqrtf((float)Ly);   // the skip head's segment scale below
+        P.mel = tail->mel; P.c1 = tail->c1; P.c2 = tail->c2; P.sigma = tail->sigma;
+        P.noise = tail->noise; P.noise_bs = tail->noise_bs; P.noise_ld = tail->noise_ld;
+        P.seed = tail->seed; P.stream_id = tail->stream_id; P.uid = tail->uid;
+      }
       ProfScope ps("wn_stack", st);
-      hipLaunchKernelGGL(wn_stack_bf16_kernel, dim3(cdiv(rows, 32)), dim3(512), 0, st, P);
+      const dim3 grid((unsigned)cdiv(rows, P.ro));
+      if (P.spec) hipLaunchKernelGGL((wn_stack_bf16_kernel<true, false>), grid, dim3(512), 0, st, P);
+      else if (P.Wsb) hipLaunchKernelGGL((wn_stack_bf16_kernel<false, true>), grid, dim3(512), 0, st, P);
+      else hipLaunchKernelGGL((wn_stack_bf16_kernel<false, false>), grid, dim3(512), 0, st, P);
       PD_LAUNCH_CHECK();
     }
   } else if (h->W1f) {
@@ -1060,6 +1239,10 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       a.part = ws + Lw.part;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_RESSKIP, U_WN_RESSKIP>(a, st, "wn_resskip")));
     }
+  }
+  if (fuse_tail) {   // skip head, output projection and posterior ran in the last stack launch
+    *tail_done = true;
+    return PD_OK;
   }
   {  // hs = relu(W_skip (sum skip / sqrt(L)) + b)   (wavenet.py:119-121)
     GemmArgs a = make_gemm(B, T, C, h->Ws, C, h->bs, hs, BTs * C, C);
@@ -1205,6 +1388,16 @@ int pd_wavenet_set_option(pd_wavenet* h, int option, int value) {
     h->stack_nl = value;
     return PD_OK;
   }
+  if (option == PD_WN_OPT_STACK_FUSE) {
+    PD_CHECK_ARG(value == 0 || value == 1, "PD_WN_OPT_STACK_FUSE is 0 or 1");
+    h->stack_fuse = value;
+    return PD_OK;
+  }
+  if (option == PD_WN_OPT_STACK_RO) {
+    PD_CHECK_ARG(value == 0 || (value >= 16 && value <= 32), "PD_WN_OPT_STACK_RO is 0 (auto) or 16 .. 32");
+    h->stack_ro = value;
+    return PD_OK;
+  }
   if (option == PD_WN_OPT_L2PF) {
     PD_CHECK_ARG(value == 0 || value == 1, "PD_WN_OPT_L2PF is 0 or 1");
     h->l2_prefetch = value;
@@ -1275,8 +1468,14 @@ int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1
   const long long BTs = T;
   for (int j = 0; j < S; ++j) {
     const int i = S - 1 - j;
-    PD_TRY(wavenet_core(h, ws, Lw, mel, cond, ws + Lw.dproj + (size_t)j * B * Ly * C, B, T, st));
     // x0 = W_out hs + b ; x = c1[i] x0 + c2[i] x + [i>0] exp(.5 logvar[i]) n   (prodiff.py:106-126)
+    StackTail tl{};
+    tl.mel = mel; tl.c1 = coef1[i]; tl.c2 = coef2[i]; tl.sigma = (i == 0) ? 0.f : sigma[i];
+    tl.noise = noise ? noise + (size_t)j * BTM : nullptr; tl.noise_bs = BTs * M; tl.noise_ld = M;
+    tl.seed = seed; tl.stream_id = (unsigned)j; tl.uid = utt_ids;
+    bool done = false;
+    PD_TRY(wavenet_core(h, ws, Lw, mel, cond, ws + Lw.dproj + (size_t)j * B * Ly * C, B, T, st, &tl, &done));
+    if (done) continue;
     GemmArgs a = make_gemm(B, T, M, h->Wo, C, h->bo, mel, BTs * M, M);
     add_seg(a, make_seg(ws + Lw.hs, BTs * C, C, C, 0));
     a.res = mel; a.res_bs = BTs * M; a.res_ld = M;

@@ -274,3 +274,53 @@ def test_wavenet_stack_bitexact(stack, B, T):
     m32.load_state_dict(net.state_dict())
     ref = m32.to(DEV)(spec, steps, cond).float().cpu().numpy()
     assert_bf16_close(outs["stack"], ref, f"wavenet stack={stack} B={B} T={T}")
+
+
+@pytest.mark.parametrize("ro", [16, 23, 27, 32])
+@pytest.mark.parametrize("B,T", [(3, 101), (2, 300)])
+def test_wavenet_stack_rows_bitexact(ro, B, T):
+    """PD_WN_OPT_STACK_RO: stack blocks writing `ro` of their 64 window rows compute every frame
+    exactly as 32-row blocks do (the block boundaries move, the halo grows): bit-identical to the
+    one-layer kernel."""
+    torch.manual_seed(12)
+    net = WaveNet(80, 256, 20, 256, 1)
+    spec = torch.randn(B, 1, 80, T, device=DEV)
+    cond = torch.randn(B, 256, T, device=DEV)
+    steps = torch.tensor([5.0, 300.0, 17.0][:B], device=DEV)
+    outs = {}
+    for name, opts in (("layer", dict(layer=0, stack=0)), ("stack", dict(stack=10, stack_ro=ro))):
+        m = WaveNet(80, 256, 20, 256, 1)
+        m.load_state_dict(net.state_dict())
+        m = m.to(DEV).set_compute_dtype("bf16").set_options(**opts)
+        outs[name] = m(spec, steps, cond).float().cpu().numpy()
+    np.testing.assert_array_equal(outs["stack"], outs["layer"])
+
+
+@pytest.mark.parametrize("draws", ["explicit", "philox"])
+@pytest.mark.parametrize("M,B,T,S", [(80, 2, 101, 2), (80, 3, 64, 4), (80, 1, 250, 3), (128, 2, 90, 4)])
+def test_prodiff_stack_fuse_bitexact(draws, M, B, T, S):
+    """PD_WN_OPT_STACK_FUSE: the input projection inside the first stack launch and the skip head +
+    output projection + posterior update inside the last one (prodiff.py:106-126) use the separate
+    launches' roundings and k order: the whole bf16 sample is bit-identical to stack_fuse=0, with
+    explicit draws and with on-device Philox draws (utterance ids shuffled), at the C3 (M=80) and
+    SVS (M=128) mel sizes; and a single forward (input projection fused, no posterior) matches too."""
+    torch.manual_seed(41 + B)
+    gd = GaussianDiffusion(M, WaveNet(M, 256, 20, 256, 1), timesteps=4, time_scale=1000, max_beta=0.7)
+    sd = gd.state_dict()
+    cond = torch.randn(B, T, 256, device=DEV)
+    xT = torch.rand(B, 1, M, T, device=DEV) if draws == "explicit" else None
+    nz = torch.randn(S, B, 1, M, T, device=DEV) if draws == "explicit" else None
+    ids = list(range(7, 7 + B))[::-1]
+    spec = torch.randn(B, 1, M, T, device=DEV)
+    steps = torch.tensor([3.0, 1.0, 2.0][:B], device=DEV)
+    outs, fwd = [], []
+    for fuse in (0, 1):
+        g = GaussianDiffusion(M, WaveNet(M, 256, 20, 256, 1), timesteps=4, time_scale=1000, max_beta=0.7)
+        g.load_state_dict(sd)
+        g = g.to(DEV).set_compute_dtype("bf16")
+        g.denoise_fn.set_options(stack_fuse=fuse)
+        outs.append(g.sample(cond, infer_step=S, x_T=xT, noise=nz, seed=1234, utt_ids=ids).cpu().numpy())
+        fwd.append(g.denoise_fn(spec, steps, cond.transpose(1, 2)).float().cpu().numpy())
+    assert np.isfinite(outs[1]).all()
+    np.testing.assert_array_equal(outs[1], outs[0])
+    np.testing.assert_array_equal(fwd[1], fwd[0])
