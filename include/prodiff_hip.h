@@ -107,6 +107,10 @@ void pd_wavenet_destroy(pd_wavenet* h);
  * stack launch and, in pd_prodiff_sample, the skip head + output projection + posterior update
  * inside the last one (same roundings and k order as the separate launches); 0 = separate launches. */
 #define PD_WN_OPT_STACK_FUSE 6
+/* PD_WN_OPT_F32_LAYER (fp32 path): 1 (default) residual layers whose GEMMs would split K (small
+ * batches, e.g. B = 1) run as two launches of 32-frame x 32-channel-pair blocks with no split-K
+ * partials (wn_f32_layer_kernel); 2 = always; 0 = the split-K GEMM engine. */
+#define PD_WN_OPT_F32_LAYER 7
 int pd_wavenet_set_option(pd_wavenet* h, int option, int value);
 /* S = number of reverse steps the workspace must serve (1 for pd_wavenet_forward). */
 size_t pd_wavenet_workspace_size(const pd_wavenet* h, int B, int T, int S);

@@ -42,6 +42,7 @@ struct pd_wavenet {
   int stack_nl = 10;
   int stack_ro = 0;          // PD_WN_OPT_STACK_RO: output rows per stack block (0 = auto, else 16..32)
   int stack_fuse = 1;        // PD_WN_OPT_STACK_FUSE: input projection / sampler output stage inside the stack launches
+  int f32_layer = 1;         // PD_WN_OPT_F32_LAYER: fp32 layers on wn_f32_layer_kernel (0 off, 1 where K would split, 2 always)
 };
 
 namespace {
@@ -660,6 +661,123 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   }
 }
 
+// ------------------------------------------------------------------ fp32 residual layer, small batches
+// PD_WN_OPT_F32_LAYER: wavenet.py:60-72 in fp32 as two launches of (frames / 32) x (C / 32) blocks
+// with no split-K partials -- the B = 1 case (C2: T = 1000 gives 256 blocks), where the GEMM
+// engine split K eight ways and paid a reduce launch per GEMM:
+//   GATE     block = 32 frames x 32 gate/filter pairs; wave w sums K segment w (x(t-d)+dp, x(t)+dp,
+//            x(t+d)+dp, cond: wavenet.py:60-66) on 32x32x2 f32 MFMAs, operands streamed from
+//            L2 / HBM straight into registers through a 3-deep ring of 32-deep chunks; the four
+//            segment partials meet in LDS and are summed in segment order; then the gate.
+//   RESSKIP  block = 32 frames x 32 residual/skip pairs; wave w sums g channels [wC/4, (w+1)C/4).
+// A lane holds 16 consecutive k of its A row / weight row per chunk: MFMA kk pairs k = kk (lanes
+// h = 0) with k = 16 + kk (h = 1), as gemm.h's fp32 path.
+struct WnF32Args {
+  const float* a;           // GATE: x [rows][C]; RESSKIP: g [rows][C]
+  const float* cond;        // GATE: [rows][H]
+  const float* dp;          // GATE: dp[b * dp_ld + c] (this layer's diffusion projection)
+  int dp_ld;
+  const float* W;           // [2C][ldw]: rows n (gate / residual) and C + n (filter / skip)
+  int ldw;
+  const float* bias;        // [2C]
+  float* g;                 // GATE: out [rows][C]
+  float* x;                 // RESSKIP: residual stream, updated in place
+  float* skip;              // RESSKIP: skip sum
+  int first;                // RESSKIP: first layer (skip = value)
+  int rows, T, C, H, dil;
+};
+
+template <int NCH>
+__device__ __forceinline__ void wf32_seg(const float* arow, const float* aadd, bool aok, const float* w0, const float* w1,
+                                         int h, f32x16& acc0, f32x16& acc1) {
+  constexpr int D = NCH < 3 ? NCH : 3;
+  float4 ra[D][4], rb0[D][4], rb1[D][4];
+  auto load = [&](int s, int ch) {
+    const int k = ch * 32 + 16 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 v = *reinterpret_cast<const float4*>(arow + k + 4 * q);   // clamped row: always in bounds
+      if (aadd) {
+        const float4 d = *reinterpret_cast<const float4*>(aadd + k + 4 * q);
+        v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
+      }
+      ra[s][q] = aok ? v : make_float4(0.f, 0.f, 0.f, 0.f);              // conv zero padding
+      rb0[s][q] = *reinterpret_cast<const float4*>(w0 + k + 4 * q);
+      rb1[s][q] = *reinterpret_cast<const float4*>(w1 + k + 4 * q);
+    }
+  };
+#pragma unroll
+  for (int ch = 0; ch < D; ++ch) load(ch, ch);
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int s = ch % D;
+    float a[16], b0[16], b1[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[4 * q] = ra[s][q].x; a[4 * q + 1] = ra[s][q].y; a[4 * q + 2] = ra[s][q].z; a[4 * q + 3] = ra[s][q].w;
+      b0[4 * q] = rb0[s][q].x; b0[4 * q + 1] = rb0[s][q].y; b0[4 * q + 2] = rb0[s][q].z; b0[4 * q + 3] = rb0[s][q].w;
+      b1[4 * q] = rb1[s][q].x; b1[4 * q + 1] = rb1[s][q].y; b1[4 * q + 2] = rb1[s][q].z; b1[4 * q + 3] = rb1[s][q].w;
+    }
+    if (ch + D < NCH) load(s, ch + D);
+    __builtin_amdgcn_sched_barrier(0);   // the ring's loads stay D chunks ahead
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk], b0[kk], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk], b1[kk], acc1, 0, 0, 0);
+    }
+  }
+}
+
+template <bool GATE, int NCH>
+__global__ __launch_bounds__(256) void wn_f32_layer_kernel(const WnF32Args P) {
+  __shared__ float red[4][2][16][64];   // the waves' partial sums, [wave][half][reg][lane]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int R0 = blockIdx.x * 32, n0 = blockIdx.y * 32, C = P.C;
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
+  {
+    const int R = R0 + r32, Rc = min(R, P.rows - 1), b = Rc / P.T, t = Rc - b * P.T;
+    const float* w0 = P.W + (long long)(n0 + r32) * P.ldw;
+    const float* w1 = P.W + (long long)(C + n0 + r32) * P.ldw;
+    if constexpr (GATE) {
+      if (wave < 3) {   // tap wave: x(t + (wave - 1) d) + dp, zero outside the utterance
+        const int tt = t + (wave - 1) * P.dil, ok = R < P.rows && tt >= 0 && tt < P.T;
+        const float* arow = P.a + ((long long)b * P.T + min(max(tt, 0), P.T - 1)) * C;
+        wf32_seg<NCH>(arow, P.dp + (long long)b * P.dp_ld, ok, w0 + wave * C, w1 + wave * C, h, acc0, acc1);
+      } else {          // conditioner: cond(t)
+        wf32_seg<NCH>(P.cond + (long long)Rc * P.H, nullptr, R < P.rows, w0 + 3 * C, w1 + 3 * C, h, acc0, acc1);
+      }
+    } else {
+      const int k0 = wave * (C / 4);
+      wf32_seg<NCH>(P.a + (long long)Rc * C + k0, nullptr, R < P.rows, w0 + k0, w1 + k0, h, acc0, acc1);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    red[wave][0][r][lane] = acc0[r];
+    red[wave][1][r][lane] = acc1[r];
+  }
+  __syncthreads();
+  const float rs2 = 0.70710678118654752440f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = tid + 256 * i, reg = p >> 6, ln = p & 63;
+    const int R = R0 + (reg & 3) + 8 * (reg >> 2) + 4 * (ln >> 5), n = n0 + (ln & 31);
+    if (R >= P.rows) continue;
+    const float v0 = ((red[0][0][reg][ln] + red[1][0][reg][ln]) + red[2][0][reg][ln]) + red[3][0][reg][ln] + P.bias[n];
+    const float v1 = ((red[0][1][reg][ln] + red[1][1][reg][ln]) + red[2][1][reg][ln]) + red[3][1][reg][ln] + P.bias[C + n];
+    if constexpr (GATE) {
+      P.g[(long long)R * C + n] = sigmoidf_(v0) * tanhf_(v1);
+    } else {
+      float* xp = P.x + (long long)R * C + n;
+      *xp = (*xp + v0) * rs2;
+      float* sp = P.skip + (long long)R * C + n;
+      *sp = P.first ? v1 : (*sp + v1);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ two-kernel residual layer (bf16)
 // The same layer as wn_layer_bf16_kernel as two launches (wavenet.py:60-72), PD_WN_OPT_LAYER = 1:
 //   GATE     g = sigmoid(W1_g . a + b_g) * tanh(W1_f . a + b_f),  a = [xa(t-d); xa(t); xa(t+d); cond(t)]
@@ -1213,6 +1331,32 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
   } else
   for (int l = 0; l < Ly; ++l) {
     const int dil = 1 << (l % h->cyc);
+    // fp32, small batches: the dedicated two-launch layer (wn_f32_layer_kernel) where the GEMM
+    // engine would split K (PD_WN_OPT_F32_LAYER 1), or always (2)
+    const bool f32k = h->f32_layer && C == 256 && H == 256 && h->ldw1 == 3 * C + H &&
+                      (h->f32_layer == 2 || wn_ksplit((long long)B * T, C, h->ldw1, h->ksplit_blocks) > 1);
+    if (f32k) {
+      const dim3 grid((unsigned)cdiv(rows, 32), C / 32);
+      WnF32Args F{};
+      F.rows = rows; F.T = T; F.C = C; F.H = H; F.dil = dil;
+      F.a = x; F.cond = cond; F.dp = dproj + (size_t)l * C; F.dp_ld = Ly * C;
+      F.W = h->Wl1 + (size_t)l * 2 * C * h->ldw1; F.ldw = h->ldw1; F.bias = h->bl1 + (size_t)l * 2 * C; F.g = g;
+      {
+        ProfScope ps("wn_gate", st);
+        hipLaunchKernelGGL((wn_f32_layer_kernel<true, 8>), grid, dim3(256), 0, st, F);
+        PD_LAUNCH_CHECK();
+      }
+      WnF32Args Q{};
+      Q.rows = rows; Q.T = T; Q.C = C; Q.H = H;
+      Q.a = g; Q.W = h->Wl2 + (size_t)l * 2 * C * C; Q.ldw = C; Q.bias = h->bl2 + (size_t)l * 2 * C;
+      Q.x = x; Q.skip = skip; Q.first = l == 0;
+      {
+        ProfScope ps("wn_resskip", st);
+        hipLaunchKernelGGL((wn_f32_layer_kernel<false, 2>), grid, dim3(256), 0, st, Q);
+        PD_LAUNCH_CHECK();
+      }
+      continue;
+    }
     {  // z = dilconv(x + dproj) + condproj ; g = sigmoid(z[:C]) * tanh(z[C:])   (wavenet.py:60-67)
       GemmArgs a = make_gemm(B, T, 2 * C, h->Wl1 + (size_t)l * 2 * C * h->ldw1, h->ldw1,
                              h->bl1 + (size_t)l * 2 * C, g, BTs * C, C);
@@ -1386,6 +1530,11 @@ int pd_wavenet_set_option(pd_wavenet* h, int option, int value) {
   if (option == PD_WN_OPT_STACK) {
     PD_CHECK_ARG(value >= 0 && value <= 16, "PD_WN_OPT_STACK is 0 (one launch per layer) .. 16");
     h->stack_nl = value;
+    return PD_OK;
+  }
+  if (option == PD_WN_OPT_F32_LAYER) {
+    PD_CHECK_ARG(value >= 0 && value <= 2, "PD_WN_OPT_F32_LAYER is 0, 1 or 2");
+    h->f32_layer = value;
     return PD_OK;
   }
   if (option == PD_WN_OPT_STACK_FUSE) {

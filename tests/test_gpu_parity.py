@@ -290,3 +290,24 @@ def test_reflow_forward_api():
     torch.manual_seed(0)
     b = rf(cond, infer=True)
     assert a.shape == (2, 40, 80) and torch.isfinite(a).all() and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("cyc,B,T", [(1, 1, 1000), (5, 3, 101), (1, 2, 37), (2, 2, 1)])
+def test_wavenet_fp32_layer_kernel(cyc, B, T):
+    """PD_WN_OPT_F32_LAYER: the fp32 residual layers as wn_f32_layer_kernel launches (GATE: four
+    K segments -- the three dilated taps of x + dp and cond -- summed per wave, then in segment
+    order; RESSKIP) against the split-K GEMM engine, at C2's shape (B=1 x 1000), a dilation cycle
+    of 5 (taps crossing utterance edges at d = 1..16), ragged lengths and T = 1.  Different fp32
+    summation order, so the bar is the north-star 1e-4."""
+    torch.manual_seed(22)
+    net = WaveNet(80, 256, 20, 256, cyc)
+    spec = torch.randn(B, 1, 80, T, device=DEV)
+    cond = torch.randn(B, 256, T, device=DEV)
+    steps = torch.tensor([7.0, 250.0, 99.0][:B], device=DEV)
+    outs = []
+    for mode in (0, 2):
+        m = WaveNet(80, 256, 20, 256, cyc)
+        m.load_state_dict(net.state_dict())
+        m = m.to(DEV).set_options(f32_layer=mode)
+        outs.append(m(spec, steps, cond).float().cpu().numpy())
+    assert_close(outs[1], outs[0])
