@@ -728,9 +728,14 @@ __device__ __forceinline__ void wf32_seg(const float* arow, const float* aadd, b
   }
 }
 
-template <bool GATE, int NCH>
-__global__ __launch_bounds__(256) void wn_f32_layer_kernel(const WnF32Args P) {
-  __shared__ float red[4][2][16][64];   // the waves' partial sums, [wave][half][reg][lane]
+// NW waves: GATE -- waves 2s and 2s + 1 split K segment s in halves (NW = 8) or wave s sums it
+// (NW = 4); RESSKIP -- wave w sums g channels [wC/NW, (w+1)C/NW).  NCH = 32-deep chunks per wave.
+#ifndef WF32_NW
+#define WF32_NW 8
+#endif
+template <bool GATE, int NCH, int NW>
+__global__ __launch_bounds__(NW * 64) void wn_f32_layer_kernel(const WnF32Args P) {
+  __shared__ float red[NW][2][16][64];   // the waves' partial sums, [wave][half][reg][lane]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int R0 = blockIdx.x * 32, n0 = blockIdx.y * 32, C = P.C;
   f32x16 acc0, acc1;
@@ -741,15 +746,17 @@ __global__ __launch_bounds__(256) void wn_f32_layer_kernel(const WnF32Args P) {
     const float* w0 = P.W + (long long)(n0 + r32) * P.ldw;
     const float* w1 = P.W + (long long)(C + n0 + r32) * P.ldw;
     if constexpr (GATE) {
-      if (wave < 3) {   // tap wave: x(t + (wave - 1) d) + dp, zero outside the utterance
-        const int tt = t + (wave - 1) * P.dil, ok = R < P.rows && tt >= 0 && tt < P.T;
-        const float* arow = P.a + ((long long)b * P.T + min(max(tt, 0), P.T - 1)) * C;
-        wf32_seg<NCH>(arow, P.dp + (long long)b * P.dp_ld, ok, w0 + wave * C, w1 + wave * C, h, acc0, acc1);
-      } else {          // conditioner: cond(t)
-        wf32_seg<NCH>(P.cond + (long long)Rc * P.H, nullptr, R < P.rows, w0 + 3 * C, w1 + 3 * C, h, acc0, acc1);
+      const int sg = wave / (NW / 4), k0 = (wave % (NW / 4)) * (C / (NW / 4));   // segment, offset in it
+      if (sg < 3) {   // tap segment: x(t + (sg - 1) d) + dp, zero outside the utterance
+        const int tt = t + (sg - 1) * P.dil, ok = R < P.rows && tt >= 0 && tt < P.T;
+        const float* arow = P.a + ((long long)b * P.T + min(max(tt, 0), P.T - 1)) * C + k0;
+        wf32_seg<NCH>(arow, P.dp + (long long)b * P.dp_ld + k0, ok, w0 + sg * C + k0, w1 + sg * C + k0, h, acc0, acc1);
+      } else {        // conditioner: cond(t)
+        wf32_seg<NCH>(P.cond + (long long)Rc * P.H + k0, nullptr, R < P.rows, w0 + 3 * C + k0, w1 + 3 * C + k0, h,
+                      acc0, acc1);
       }
     } else {
-      const int k0 = wave * (C / 4);
+      const int k0 = wave * (C / NW);
       wf32_seg<NCH>(P.a + (long long)Rc * C + k0, nullptr, R < P.rows, w0 + k0, w1 + k0, h, acc0, acc1);
     }
   }
@@ -761,12 +768,15 @@ __global__ __launch_bounds__(256) void wn_f32_layer_kernel(const WnF32Args P) {
   __syncthreads();
   const float rs2 = 0.70710678118654752440f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = tid + 256 * i, reg = p >> 6, ln = p & 63;
+  for (int i = 0; i < 1024 / (NW * 64); ++i) {
+    const int p = tid + NW * 64 * i, reg = p >> 6, ln = p & 63;
     const int R = R0 + (reg & 3) + 8 * (reg >> 2) + 4 * (ln >> 5), n = n0 + (ln & 31);
     if (R >= P.rows) continue;
-    const float v0 = ((red[0][0][reg][ln] + red[1][0][reg][ln]) + red[2][0][reg][ln]) + red[3][0][reg][ln] + P.bias[n];
-    const float v1 = ((red[0][1][reg][ln] + red[1][1][reg][ln]) + red[2][1][reg][ln]) + red[3][1][reg][ln] + P.bias[C + n];
+    float v0 = red[0][0][reg][ln], v1 = red[0][1][reg][ln];   // partials in wave (= K) order
+#pragma unroll
+    for (int w = 1; w < NW; ++w) { v0 += red[w][0][reg][ln]; v1 += red[w][1][reg][ln]; }
+    v0 += P.bias[n];
+    v1 += P.bias[C + n];
     if constexpr (GATE) {
       P.g[(long long)R * C + n] = sigmoidf_(v0) * tanhf_(v1);
     } else {
@@ -774,6 +784,104 @@ __global__ __launch_bounds__(256) void wn_f32_layer_kernel(const WnF32Args P) {
       *xp = (*xp + v0) * rs2;
       float* sp = P.skip + (long long)R * C + n;
       *sp = P.first ? v1 : (*sp + v1);
+    }
+  }
+}
+
+// fp32 sampler output stage at small batches (prodiff.py:106-126 after wavenet.py:119-123), one launch
+// per 32 frames instead of the skip-head and output-projection GEMM launches: hs = relu(W_s (skip /
+// sqrt L) + b_s) (wave w: channels [32w, 32w + 32)), kept in LDS, then x0 = W_o hs + b_o (waves
+// 0 .. M/32) and the posterior x = c1 x0 + c2 x + sigma n.  Each output sums K in the GEMM engine's
+// order (32-deep chunks, k = kk and 16 + kk per MFMA step), so it equals the two launches' result.
+struct WnF32TailArgs {
+  const float* skip;        // [rows][C]
+  float scale;              // 1 / sqrt(L)
+  const float* Ws;          // [C][C]
+  const float* bs;
+  const float* Wo;          // [M][C]
+  const float* bo;
+  float* mel;               // [rows][M]: x_t in, x_{t-1} out
+  float c1, c2, sigma;
+  const float* noise;
+  long long noise_bs;
+  int noise_ld;
+  unsigned long long seed;
+  unsigned stream_id;
+  const int* uid;
+  int rows, T, C, M;
+};
+
+template <int NCH>
+__device__ __forceinline__ void wf32_seg1(const float* arow, float ascale, bool aok, const float* w0, int h, f32x16& acc) {
+  constexpr int D = NCH < 3 ? NCH : 3;
+  float4 ra[D][4], rb[D][4];
+  auto load = [&](int s, int ch) {
+    const int k = ch * 32 + 16 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 v = *reinterpret_cast<const float4*>(arow + k + 4 * q);
+      v.x *= ascale; v.y *= ascale; v.z *= ascale; v.w *= ascale;
+      ra[s][q] = aok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[s][q] = *reinterpret_cast<const float4*>(w0 + k + 4 * q);
+    }
+  };
+#pragma unroll
+  for (int ch = 0; ch < D; ++ch) load(ch, ch);
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int s = ch % D;
+    float a[16], b[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[4 * q] = ra[s][q].x; a[4 * q + 1] = ra[s][q].y; a[4 * q + 2] = ra[s][q].z; a[4 * q + 3] = ra[s][q].w;
+      b[4 * q] = rb[s][q].x; b[4 * q + 1] = rb[s][q].y; b[4 * q + 2] = rb[s][q].z; b[4 * q + 3] = rb[s][q].w;
+    }
+    if (ch + D < NCH) load(s, ch + D);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk], b[kk], acc, 0, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(512) void wn_f32_tail_kernel(const WnF32TailArgs P) {
+  constexpr int C = 256, LDH = C + 4;
+  __shared__ __attribute__((aligned(16))) float Hs[32 * LDH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int R0 = blockIdx.x * 32, R = R0 + r32, Rc = min(R, P.rows - 1);
+  {
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int n = wave * 32 + r32;
+    wf32_seg1<C / 32>(P.skip + (long long)Rc * C, P.scale, R < P.rows, P.Ws + (long long)n * C, h, acc);
+    const float b = P.bs[n];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg)
+      Hs[((reg & 3) + 8 * (reg >> 2) + 4 * h) * LDH + n] = act_apply(acc[reg] + b, ACT_RELU, 0.f);
+  }
+  __syncthreads();
+  if (wave * 32 < P.M) {   // wave-uniform
+    const int col = wave * 32 + r32, colc = min(col, P.M - 1);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    wf32_seg1<C / 32>(&Hs[r32 * LDH], 1.f, true, P.Wo + (long long)colc * C, h, acc);
+    const float bo = P.bo[colc];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int Ro = R0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (Ro < P.rows && col < P.M) {   // gemm.h EPI_POSTERIOR
+        const int b = Ro / P.T, t = Ro - b * P.T;
+        const float v = acc[reg] + bo;
+        const float xt = P.mel[(long long)Ro * P.M + col];
+        float x = P.c1 * v + P.c2 * xt;
+        if (P.sigma != 0.f) {
+          const float z = P.noise ? P.noise[(long long)b * P.noise_bs + (long long)t * P.noise_ld + col]
+                                  : philox_normal_u(P.seed, utt_id(P.uid, b), (unsigned)(t * P.M + col), P.stream_id);
+          x += P.sigma * z;
+        }
+        P.mel[(long long)Ro * P.M + col] = x;
+      }
     }
   }
 }
@@ -1343,7 +1451,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       F.W = h->Wl1 + (size_t)l * 2 * C * h->ldw1; F.ldw = h->ldw1; F.bias = h->bl1 + (size_t)l * 2 * C; F.g = g;
       {
         ProfScope ps("wn_gate", st);
-        hipLaunchKernelGGL((wn_f32_layer_kernel<true, 8>), grid, dim3(256), 0, st, F);
+        hipLaunchKernelGGL((wn_f32_layer_kernel<true, 32 / WF32_NW, WF32_NW>), grid, dim3(WF32_NW * 64), 0, st, F);
         PD_LAUNCH_CHECK();
       }
       WnF32Args Q{};
@@ -1352,7 +1460,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       Q.x = x; Q.skip = skip; Q.first = l == 0;
       {
         ProfScope ps("wn_resskip", st);
-        hipLaunchKernelGGL((wn_f32_layer_kernel<false, 2>), grid, dim3(256), 0, st, Q);
+        hipLaunchKernelGGL((wn_f32_layer_kernel<false, 8 / WF32_NW, WF32_NW>), grid, dim3(WF32_NW * 64), 0, st, Q);
         PD_LAUNCH_CHECK();
       }
       continue;
@@ -1385,6 +1493,21 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     }
   }
   if (fuse_tail) {   // skip head, output projection and posterior ran in the last stack launch
+    *tail_done = true;
+    return PD_OK;
+  }
+  // fp32 at small batches: skip head + output projection + posterior in one launch per 32 frames
+  if (tail && !h->W1f && h->f32_layer && C == 256 && M <= 256 &&
+      (h->f32_layer == 2 || wn_ksplit((long long)B * T, C, h->ldw1, h->ksplit_blocks) > 1)) {
+    WnF32TailArgs F{};
+    F.skip = skip; F.scale = 1.0f / sqrtf((float)Ly); F.Ws = h->Ws; F.bs = h->bs; F.Wo = h->Wo; F.bo = h->bo;
+    F.mel = tail->mel; F.c1 = tail->c1; F.c2 = tail->c2; F.sigma = tail->sigma;
+    F.noise = tail->noise; F.noise_bs = tail->noise_bs; F.noise_ld = tail->noise_ld;
+    F.seed = tail->seed; F.stream_id = tail->stream_id; F.uid = tail->uid;
+    F.rows = rows; F.T = T; F.C = C; F.M = M;
+    ProfScope ps("wn_f32_tail", st);
+    hipLaunchKernelGGL(wn_f32_tail_kernel, dim3(cdiv(rows, 32)), dim3(512), 0, st, F);
+    PD_LAUNCH_CHECK();
     *tail_done = true;
     return PD_OK;
   }

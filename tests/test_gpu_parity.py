@@ -311,3 +311,22 @@ def test_wavenet_fp32_layer_kernel(cyc, B, T):
         m = m.to(DEV).set_options(f32_layer=mode)
         outs.append(m(spec, steps, cond).float().cpu().numpy())
     assert_close(outs[1], outs[0])
+
+
+@pytest.mark.parametrize("B,T,S", [(1, 1000, 4), (3, 101, 2)])
+def test_prodiff_fp32_small_batch_kernels(B, T, S):
+    """The fp32 sampler at small batches on wn_f32_layer_kernel + wn_f32_tail_kernel (skip head,
+    output projection and posterior in one launch; PD_WN_OPT_F32_LAYER=2 forces them) against
+    the split-K GEMM engine path (=0), Philox draws: within the north-star 1e-4."""
+    torch.manual_seed(23)
+    gd = GaussianDiffusion(80, WaveNet(80, 256, 20, 256, 1), timesteps=4, time_scale=1000, max_beta=0.7)
+    sd = gd.state_dict()
+    cond = torch.randn(B, T, 256, device=DEV)
+    outs = []
+    for mode in (0, 2):
+        g = GaussianDiffusion(80, WaveNet(80, 256, 20, 256, 1), timesteps=4, time_scale=1000, max_beta=0.7)
+        g.load_state_dict(sd)
+        g = g.to(DEV)
+        g.denoise_fn.set_options(f32_layer=mode)
+        outs.append(g.sample(cond, infer_step=S, seed=99).cpu().numpy())
+    assert_close(outs[1], outs[0])
