@@ -687,21 +687,26 @@ struct WnF32Args {
   int rows, T, C, H, dil;
 };
 
-template <int NCH>
+// ADD: A = row + aadd (the taps' x + dp).  A compile-time choice: a runtime `if (aadd)` around
+// the loads made the compiler wait for each chunk's loads at the branch join (no ring at all).
+template <int NCH, bool ADD>
 __device__ __forceinline__ void wf32_seg(const float* arow, const float* aadd, bool aok, const float* w0, const float* w1,
                                          int h, f32x16& acc0, f32x16& acc1) {
   constexpr int D = NCH < 3 ? NCH : 3;
   float4 ra[D][4], rb0[D][4], rb1[D][4];
+  // conv zero padding as a multiply by 0 / 1 (the row is clamped, so its values are finite): a
+  // select let hipcc put the load under an exec branch and wait for it at the join
+  const float am = aok ? 1.f : 0.f;
   auto load = [&](int s, int ch) {
     const int k = ch * 32 + 16 * h;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float4 v = *reinterpret_cast<const float4*>(arow + k + 4 * q);   // clamped row: always in bounds
-      if (aadd) {
+      if constexpr (ADD) {
         const float4 d = *reinterpret_cast<const float4*>(aadd + k + 4 * q);
         v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
       }
-      ra[s][q] = aok ? v : make_float4(0.f, 0.f, 0.f, 0.f);              // conv zero padding
+      ra[s][q] = make_float4(v.x * am, v.y * am, v.z * am, v.w * am);
       rb0[s][q] = *reinterpret_cast<const float4*>(w0 + k + 4 * q);
       rb1[s][q] = *reinterpret_cast<const float4*>(w1 + k + 4 * q);
     }
@@ -750,14 +755,15 @@ __global__ __launch_bounds__(NW * 64) void wn_f32_layer_kernel(const WnF32Args P
       if (sg < 3) {   // tap segment: x(t + (sg - 1) d) + dp, zero outside the utterance
         const int tt = t + (sg - 1) * P.dil, ok = R < P.rows && tt >= 0 && tt < P.T;
         const float* arow = P.a + ((long long)b * P.T + min(max(tt, 0), P.T - 1)) * C + k0;
-        wf32_seg<NCH>(arow, P.dp + (long long)b * P.dp_ld + k0, ok, w0 + sg * C + k0, w1 + sg * C + k0, h, acc0, acc1);
+        wf32_seg<NCH, true>(arow, P.dp + (long long)b * P.dp_ld + k0, ok, w0 + sg * C + k0, w1 + sg * C + k0, h, acc0,
+                            acc1);
       } else {        // conditioner: cond(t)
-        wf32_seg<NCH>(P.cond + (long long)Rc * P.H + k0, nullptr, R < P.rows, w0 + 3 * C + k0, w1 + 3 * C + k0, h,
-                      acc0, acc1);
+        wf32_seg<NCH, false>(P.cond + (long long)Rc * P.H + k0, nullptr, R < P.rows, w0 + 3 * C + k0, w1 + 3 * C + k0,
+                             h, acc0, acc1);
       }
     } else {
       const int k0 = wave * (C / NW);
-      wf32_seg<NCH>(P.a + (long long)Rc * C + k0, nullptr, R < P.rows, w0 + k0, w1 + k0, h, acc0, acc1);
+      wf32_seg<NCH, false>(P.a + (long long)Rc * C + k0, nullptr, R < P.rows, w0 + k0, w1 + k0, h, acc0, acc1);
     }
   }
 #pragma unroll
@@ -815,13 +821,14 @@ template <int NCH>
 __device__ __forceinline__ void wf32_seg1(const float* arow, float ascale, bool aok, const float* w0, int h, f32x16& acc) {
   constexpr int D = NCH < 3 ? NCH : 3;
   float4 ra[D][4], rb[D][4];
+  const float am = aok ? 1.f : 0.f;   // (as wf32_seg: a multiply, not a select)
   auto load = [&](int s, int ch) {
     const int k = ch * 32 + 16 * h;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float4 v = *reinterpret_cast<const float4*>(arow + k + 4 * q);
       v.x *= ascale; v.y *= ascale; v.z *= ascale; v.w *= ascale;
-      ra[s][q] = aok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      ra[s][q] = make_float4(v.x * am, v.y * am, v.z * am, v.w * am);
       rb[s][q] = *reinterpret_cast<const float4*>(w0 + k + 4 * q);
     }
   };
