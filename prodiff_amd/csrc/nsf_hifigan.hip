@@ -477,7 +477,8 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
 // path's bf16 intermediate, applies lrelu and keeps them in LDS; c2 reads that window.  Per
 // output row this drops the intermediate's HBM write and read and the second staging of x.
 // Waves: column tile ct = wave % NCT (NCT = C / 32) of both convs; with NCT = 2 the row tiles are
-// split between two wave pairs by parity.
+// split between two wave pairs by parity, with NCT = 1 (C = 32, r04) between all four waves (FMO = 7:
+// 8 c1 row tiles and 7 c2 row tiles over 4 waves).
 template <int C, int FMO>
 __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restrict__ x, const __bf16* __restrict__ w1,
                                                       const __bf16* __restrict__ w2, int ldw, int kpad,
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
   constexpr int NCT = C / 32, RG = 4 / NCT, LDA = C + 8, KS = C / 16;
   constexpr int TM = 32 * FMO, RT1 = FMO + 1;            // output rows; c1 row tiles
   constexpr int MF1 = (RT1 + RG - 1) / RG, MF2 = (FMO + RG - 1) / RG;   // row tiles per wave
-  static_assert(NCT == 2 || NCT == 4, "C = 64 or 128");
+  static_assert(NCT == 1 || NCT == 2 || NCT == 4, "C = 32, 64 or 128");
   extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int ct = wave % NCT, rg = wave / NCT;
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
 template <int C>
 int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
                   hipStream_t st) {
-  constexpr int FMO = 4, TM = 32 * FMO;
+  constexpr int FMO = C == 32 ? 7 : 4, TM = 32 * FMO;
   const size_t lds = (size_t)(32 * (FMO + 1) * 2 + (c1.taps - 1) * c1.dil) * (C + 8) * sizeof(__bf16);
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&nsf_pair_kernel<C, FMO>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -620,10 +621,11 @@ int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, i
 }
 
 bool wconv_ok(const NsfConv& c);
-// The fused pair for these convs, if it has one: both windowed (bf16), 64 or 128 channels, equal taps
-// and packing, c2 undilated.
+// The fused pair for these convs, if it has one: both windowed (bf16), 32, 64 or 128 channels, equal
+// taps and packing, c2 undilated.
 bool pair_ok(const nsf_model* m, const NsfConv& c1, const NsfConv& c2) {
-  return m->pair && wconv_ok(c1) && wconv_ok(c2) && c1.cout == c2.cout && (c1.cout == 64 || c1.cout == 128) &&
+  return m->pair && wconv_ok(c1) && wconv_ok(c2) && c1.cout == c2.cout &&
+         (c1.cout == 32 || c1.cout == 64 || c1.cout == 128) &&
          c1.taps == c2.taps && c1.kpad == c2.kpad && c2.dil == 1 && c1.taps <= 33;
 }
 
@@ -634,6 +636,7 @@ int launch_pair(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int
     return PD_ERR_UNSUPPORTED;
   }
   if (c1.cout == 128) return launch_pair_c<128>(c1, c2, x, B, Tl, out, accum, st);
+  if (c1.cout == 32) return launch_pair_c<32>(c1, c2, x, B, Tl, out, accum, st);
   return launch_pair_c<64>(c1, c2, x, B, Tl, out, accum, st);
 }
 
