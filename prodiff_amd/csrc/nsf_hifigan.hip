@@ -300,6 +300,31 @@ int launch_conv_small(const NsfConv& c, const float* in, float alpha, float scal
 // of the windowed convs.  Each thread keeps NSF_WB 16-byte items in flight: all loads of a batch
 // are issued before any is converted (r02: C5 21.6 -> 21.0 ms/step).
 constexpr int NSF_WB = 4;
+// Epilogue stores without a row-range branch (r04: with `if (t < Tl)` around each store the waitcnt
+// pass put a full vmcnt(0) before every one, so a lane's 16 stores ran one round trip apart): a
+// buffer resource spanning exactly one utterance's rows of `out`; stores past its last row are
+// dropped by the hardware range check.
+template <bool OUT_BF>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t nsf_utt_rsrc(void* out, int rowb, int Tl, int C) {
+  const int es = OUT_BF ? 2 : 4;
+  char* base = reinterpret_cast<char*>(out) + (long long)rowb * C * es;
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, Tl * C * es, 0x00020000);
+}
+template <bool OUT_BF>
+__device__ __forceinline__ void nsf_store_utt(__amdgpu_buffer_rsrc_t r, int elem, float v) {
+  if constexpr (OUT_BF) {
+    const __bf16 hv = (__bf16)v;
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, hv), r, elem * 2, 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, elem * 4, 0, 0);
+  }
+}
+
+// Stages window rows r0 .. r0 + W - 1 of `in` (lrelu(alpha) * scale, bf16) into win; rows outside
+// [0, Tl) are zero.  r04: loads unconditional (clamped row), zero rows by a multiply, and every LDS
+// store unconditional -- items past the window go to row W, one spare row the callers allocate
+// (or that the next stage overwrites): with `if (ok)` loads / `if (i < nitems)` stores hipcc sank
+// the loads into the branches and waited for each one, a round trip per item instead of per batch.
 template <int C, bool IN_BF>
 __device__ __forceinline__ void stage_window(const void* __restrict__ in, int b, int Tl, int r0, int W, float alpha,
                                              float scale, __bf16* __restrict__ win, int lda, int tid) {
@@ -313,35 +338,28 @@ __device__ __forceinline__ void stage_window(const void* __restrict__ in, int b,
       const int row = i / C8, c8 = i - row * C8;
       const int t = r0 + row;
       const bool ok = i < nitems && t >= 0 && t < Tl;
+      const float m = ok ? 1.f : 0.f;
       const long long e = ((long long)b * Tl + (ok ? t : 0)) * C + 8 * c8;
       if constexpr (IN_BF) {
-        bf16x8 x;
-        if (ok) x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(in) + e);
-        else
+        const bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(in) + e);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = (__bf16)0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[u][j] = (float)x[j];
+        for (int j = 0; j < 8; ++j) f[u][j] = (float)x[j] * m;
       } else {
-        float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
-        if (ok) {
-          x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e);
-          x1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e + 4);
-        }
-        f[u][0] = x0.x; f[u][1] = x0.y; f[u][2] = x0.z; f[u][3] = x0.w;
-        f[u][4] = x1.x; f[u][5] = x1.y; f[u][6] = x1.z; f[u][7] = x1.w;
+        const float4 x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e);
+        const float4 x1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in) + e + 4);
+        f[u][0] = x0.x * m; f[u][1] = x0.y * m; f[u][2] = x0.z * m; f[u][3] = x0.w * m;
+        f[u][4] = x1.x * m; f[u][5] = x1.y * m; f[u][6] = x1.z * m; f[u][7] = x1.w * m;
       }
     }
 #pragma unroll
     for (int u = 0; u < NSF_WB; ++u) {
       const int i = base + 256 * u;
-      if (i < nitems) {
-        const int row = i / C8, c8 = i - row * C8;
-        bf16x8 v;
+      const bool in_w = i < nitems;
+      const int row = in_w ? i / C8 : W, c8 = in_w ? i - (i / C8) * C8 : 0;
+      bf16x8 v;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[u][j] >= 0.f ? f[u][j] : alpha * f[u][j]) * scale);
-        *reinterpret_cast<bf16x8*>(win + row * lda + 8 * c8) = v;
-      }
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)((f[u][j] >= 0.f ? f[u][j] : alpha * f[u][j]) * scale);
+      *reinterpret_cast<bf16x8*>(win + row * lda + 8 * c8) = v;
     }
   }
 }
@@ -431,6 +449,7 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
   // instead of two per fragment (r02: the residual convs ran ~1.5x their plain twins).
   // 32-bit element offsets (the host checks B*Tl*C < 2^31) keep one VGPR per address
   const int rowb = b * Tl;
+  const __amdgpu_buffer_rsrc_t ors = nsf_utt_rsrc<OUT_BF>(out, rowb, Tl, C);
   float bn[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) bn[j] = bias[n0 + (wn * FN + j) * 32 + r32];
@@ -446,9 +465,14 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
           const int reg = hb + q, n = n0 + (wn * FN + j) * 32 + r32;
           const int t = min(t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tl - 1);
           const int o = (rowb + t) * C + n;
-          float v = res ? res[o] : 0.f;
-          if constexpr (!OUT_BF)
-            if (accum) v += reinterpret_cast<const float*>(out)[o];
+          // branch-free (r04): a load under `res ?` / `if (accum)` made the waitcnt pass wait for
+          // each one in turn (16 round trips per lane); an fp32 output always has a residual
+          float v = 0.f;
+          if constexpr (!OUT_BF) {
+            const float a = reinterpret_cast<const float*>(out)[o];
+            v = res[o];
+            v = accum ? v + a : v;
+          }
           rv[i][j][q] = v;
         }
 #pragma unroll
@@ -459,12 +483,8 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
         for (int q = 0; q < 8; ++q) {
           const int reg = hb + q, n = n0 + (wn * FN + j) * 32 + r32;
           const int t = t0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-          const int o = (rowb + t) * C + n;
           const float v = acc[i][j][reg] + bn[j] + rv[i][j][q];
-          if (t < Tl) {
-            if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
-            else reinterpret_cast<float*>(out)[o] = v;
-          }
+          nsf_store_utt<OUT_BF>(ors, t * C + n, v);   // rows t >= Tl fall outside ors and are dropped
         }
   }
 }
@@ -664,13 +684,15 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
   stage_window<C, IN_BF>(in, b, Tl, t0 - pad, W, alpha, scale, nsf_win16, LDA, tid);
   const int r16 = lane & 15, g = lane >> 4, kg = g & 1, tg = g >> 1;
   const int npair = (taps + 1) >> 1;
+  // every pair's fragment loaded unconditionally (clamped tap) and zeroed by a bit mask: a load
+  // under `if (tap < taps)` was waited for on its own, six L2 round trips in a row (r04)
   bf16x8 bw[MAXP];
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
-    const int tap = 2 * p + tg;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bw[p][j] = (__bf16)0.f;
-    if (p < npair && tap < taps) bw[p] = *reinterpret_cast<const bf16x8*>(w + (long long)r16 * (taps * kpad) + tap * kpad + 8 * kg);
+    const int tap = 2 * p + tg, tc = min(tap, taps - 1);
+    const uint4 raw = *reinterpret_cast<const uint4*>(w + (long long)r16 * (taps * kpad) + tc * kpad + 8 * kg);
+    const unsigned mk = (p < npair && tap < taps) ? 0xffffffffu : 0u;
+    bw[p] = __builtin_bit_cast(bf16x8, make_uint4(raw.x & mk, raw.y & mk, raw.z & mk, raw.w & mk));
   }
   // the epilogue's residual / accumulator operands, loaded now so they land under the MFMAs
   float rv[4][4];
@@ -680,9 +702,12 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
     for (int r = 0; r < 4; ++r) {
       const int t = min(t0 + wave * 64 + i * 16 + 4 * g + r, Tl - 1);
       const long long o = ((long long)b * Tl + t) * C + r16;
-      float v = res ? res[o] : 0.f;
-      if constexpr (!OUT_BF)
-        if (accum) v += reinterpret_cast<const float*>(out)[o];
+      float v = 0.f;   // branch-free, as nsf_wconv_kernel's epilogue
+      if constexpr (!OUT_BF) {
+        const float a = reinterpret_cast<const float*>(out)[o];
+        v = res[o];
+        v = accum ? v + a : v;
+      }
       rv[i][r] = v;
     }
   __syncthreads();
@@ -708,17 +733,14 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
     }
   }
   const float bn = bias[r16];
+  const __amdgpu_buffer_rsrc_t ors = nsf_utt_rsrc<OUT_BF>(out, b * Tl, Tl, C);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int t = t0 + wave * 64 + i * 16 + 4 * g + r;
-      const long long o = ((long long)b * Tl + t) * C + r16;
       const float v = acc[i][r] + bn + rv[i][r];
-      if (t < Tl) {
-        if constexpr (OUT_BF) reinterpret_cast<__bf16*>(out)[o] = (__bf16)v;
-        else reinterpret_cast<float*>(out)[o] = v;
-      }
+      nsf_store_utt<OUT_BF>(ors, t * C + r16, v);   // rows t >= Tl dropped by the range check
     }
   }
 }
@@ -726,7 +748,7 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
 int launch_wconv16(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
                    int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum) {
   if (c.taps > 12) { set_error("nsf wconv16: at most 12 taps"); return PD_ERR_UNSUPPORTED; }
-  const size_t lds = (size_t)(256 + (c.taps - 1) * c.dil) * 24 * sizeof(__bf16);
+  const size_t lds = (size_t)(256 + (c.taps - 1) * c.dil + 1) * 24 * sizeof(__bf16);   // + stage_window's spare row
   dim3 grid(cdiv(Tl, 256), B);
   ProfScope ps("nsf_res_small", st);
 #define PD_WCONV16(IB, OB)                                                                                      \
@@ -885,7 +907,7 @@ int launch_ups_c(const NsfUps& U, const __bf16* wb, const float* in, float scale
                  float* out, hipStream_t st) {
   constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN;
   const int p = (U.k - U.u) / 2;
-  const size_t lds = (size_t)(TQ + U.ntap) * (CIN + 8) * sizeof(__bf16);
+  const size_t lds = (size_t)(TQ + U.ntap + 1) * (CIN + 8) * sizeof(__bf16);   // + stage_window's spare row
   static const hipError_t attr = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD>),
       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -932,7 +954,7 @@ template <int C, int FM, int FN, int WM, int WN>
 int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
                    int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum) {
   constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN;
-  const size_t lds = (size_t)(TM + (c.taps - 1) * c.dil) * (C + 8) * sizeof(__bf16);
+  const size_t lds = (size_t)(TM + (c.taps - 1) * c.dil + 1) * (C + 8) * sizeof(__bf16);   // + stage_window's spare row
   if (lds > 160 * 1024) { set_error("nsf conv: LDS window too large"); return PD_ERR_UNSUPPORTED; }
   dim3 grid(cdiv(Tl, TM), C / TN, B);
   const int ldw = c.taps * c.kpad;
@@ -970,6 +992,10 @@ int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, floa
   if ((long long)B * Tl * c.cout >= (1ll << 31)) {
     set_error("nsf wconv: B * T * C >= 2^31 elements (32-bit epilogue offsets)");
     return PD_ERR_UNSUPPORTED;
+  }
+  if (out_bf == (res != nullptr)) {   // the kernels' epilogue: fp32 outputs add a residual, bf16 ones none
+    set_error("nsf wconv: an fp32 output needs a residual and a bf16 output takes none");
+    return PD_ERR_ARG;
   }
   switch (c.cout) {
     // Tilings: a wave owns all TM rows of its 32-channel column tiles (WM = 1), so each weight
