@@ -1286,6 +1286,15 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   // run through a KH0-deep register ring, primed here so the first ones land with the
   // staging loads: a load right before each MFMA made stage 0 thirty L2 round trips per job.
   constexpr int KH0 = 10;
+  // every stage's bias for this lane's column, loaded up front (r04: each stage's bias load right
+  // before its epilogue was a round trip of its own): stages 0..6 use column (wave & 1) 32 + r32,
+  // the bias_conv tiles 2w and 2w + 1
+  const int nw = (wave & 1) * 32 + r32;
+  const float bias_in = A.bin[nblk][nw];
+  float bias_r[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) bias_r[j] = A.br[nblk][j][nw];
+  const float bias_b[2] = {A.bb[nblk][2 * wave * 32 + r32], A.bb[nblk][(2 * wave + 1) * 32 + r32]};
   const __bf16* wrow0 = A.Win[nblk] + ((wave & 1) * 32 + r32) * 480 + h * 8;
   bf16x8 w0r[KH0];
 #pragma unroll
@@ -1349,7 +1358,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
     }
     if (job >= 6) continue;
     const int n = nt * 32 + r32;
-    const float bias = A.bin[nblk][n];
+    const float bias = bias_in;   // (n == nw)
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int p = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, f = f0 - 16 + p;
@@ -1391,7 +1400,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bwf[kk], acc, 0, 0, 0);
       }
       const int n = nt * 32 + r32;
-      const float bias = A.br[nblk][j][n];
+      const float bias = bias_r[j];   // (n == nw)
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int p = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, f = f0 - 16 + p;
@@ -1432,7 +1441,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bwb[kk], acc, 0, 0, 0);
     }
     const int n = nt * 32 + r32;
-    const float bias = A.bb[nblk][n];
+    const float bias = bias_b[job >> 1];
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int f = f0 + mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;

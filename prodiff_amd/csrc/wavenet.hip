@@ -396,20 +396,26 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   } else {
     // fused input projection: bf16(spec) of the window rows into Gs (k >= M zero, as the GEMM
     // engine's padded K chunks)
-    const int nq = P.ldw_in / 4;
-    for (int i = tid; i < WR * nq; i += 512) {
-      const int wr = i / nq, c = (i - wr * nq) * 4, Rc = min(max(W0 + wr, 0), rows - 1);
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (c < P.M) v = *reinterpret_cast<const float4*>(P.spec + (long long)Rc * P.M + c);
-      *reinterpret_cast<bf16x4*>(&Gs[wr * WST_LD + c]) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    // 64 rows x 32 column quads (128 columns, zero past M), unrolled with unconditional loads
+    // (clamped column, zeroed by a multiply; spec is finite) so all of them are in flight together
+#pragma unroll
+    for (int it = 0; it < WR * 32 / 512; ++it) {
+      const int i = tid + 512 * it, wr = i >> 5, c = (i & 31) * 4;
+      const int Rc = min(max(W0 + wr, 0), rows - 1);
+      const float4 v = *reinterpret_cast<const float4*>(P.spec + (long long)Rc * P.M + min(c, P.M - 4));
+      const float m = c < P.M ? 1.f : 0.f;
+      *reinterpret_cast<bf16x4*>(&Gs[wr * WST_LD + c]) =
+          bf16x4{(__bf16)(v.x * m), (__bf16)(v.y * m), (__bf16)(v.z * m), (__bf16)(v.w * m)};
     }
   }
+  // (rows outside the batch zeroed by a bit mask, not a select: hipcc turned the select into a
+  // branch and waited for each load at its join -- four round trips instead of one, r04)
 #pragma unroll
   for (int it = 0; it < WR * 32 / 512; ++it) {
     const int i = tid + it * 512, wr = i >> 5, c = (i & 31) * 8, R = W0 + wr;
-    uint4 v = *reinterpret_cast<const uint4*>(P.condb + (long long)min(max(R, 0), rows - 1) * H + c);
-    if (R < 0 || R >= rows) v = make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(&CW[wr * WST_LD + c]) = v;
+    const uint4 v = *reinterpret_cast<const uint4*>(P.condb + (long long)min(max(R, 0), rows - 1) * H + c);
+    const unsigned mk = (R >= 0 && R < rows) ? 0xffffffffu : 0u;
+    *reinterpret_cast<uint4*>(&CW[wr * WST_LD + c]) = make_uint4(v.x & mk, v.y & mk, v.z & mk, v.w & mk);
   }
   // x (fp32) of the lane's 32 window rows, column n, in registers (the GEMM2 C layout: tile q,
   // register reg -> window row 32 q + (reg & 3) + 8 (reg >> 2) + 4 h); the skip sum of its 16
@@ -465,11 +471,15 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
         xr[q][reg] = P.xin[(long long)min(max(R, 0), rows - 1) * C + n];
       }
   }
+  {   // (unconditional loads, the first launch's zero by a bit mask: see the cond staging above)
+    const unsigned mk = P.first ? 0u : 0xffffffffu;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
-    const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-    SK[sko(i)] = P.first ? 0.f : P.skip[(long long)min(R, rows - 1) * C + n];
+    for (int i = 0; i < 16; ++i) {
+      const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
+      const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      const float sv = P.skip[(long long)min(max(R, 0), rows - 1) * C + n];
+      SK[sko(i)] = __uint_as_float(__float_as_uint(sv) & mk);
+    }
   }
   // conv zero padding: tap t-1 / t+1 of the lane's A rows (window row 32q + r32) outside its
   // utterance (or outside the batch) reads zero -- a select at the fragment read
