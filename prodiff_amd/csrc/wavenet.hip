@@ -699,10 +699,13 @@ struct WnF32Args {
 
 // ADD: A = row + aadd (the taps' x + dp).  A compile-time choice: a runtime `if (aadd)` around
 // the loads made the compiler wait for each chunk's loads at the branch join (no ring at all).
+#ifndef WF32_RING
+#define WF32_RING 2
+#endif
 template <int NCH, bool ADD>
 __device__ __forceinline__ void wf32_seg(const float* arow, const float* aadd, bool aok, const float* w0, const float* w1,
                                          int h, f32x16& acc0, f32x16& acc1) {
-  constexpr int D = NCH < 3 ? NCH : 3;
+  constexpr int D = NCH < WF32_RING ? NCH : WF32_RING;
   float4 ra[D][4], rb0[D][4], rb1[D][4];
   // conv zero padding as a multiply by 0 / 1 (the row is clamped, so its values are finite): a
   // select let hipcc put the load under an exec branch and wait for it at the join
@@ -781,25 +784,45 @@ __global__ __launch_bounds__(NW * 64) void wn_f32_layer_kernel(const WnF32Args P
     red[wave][0][r][lane] = acc0[r];
     red[wave][1][r][lane] = acc1[r];
   }
+  // epilogue: a thread's column n is the same for all its elements (NW * 64 is a multiple of 64);
+  // biases and the residual / skip operands are loaded before any is used and the stores go through
+  // buffer resources spanning `rows` rows, so rows past the end are dropped without a branch (r04:
+  // loads and stores under `if (R < rows)` were each waited for on their own)
+  constexpr int NE = 1024 / (NW * 64);
+  const int ln = tid & 63, n = n0 + (ln & 31);
   __syncthreads();
-  const float rs2 = 0.70710678118654752440f;
+  // (everything below after the barrier: before it, the gate kernel's register file is full)
+  float xo[NE], so[NE];
+  int Re[NE], rege[NE];
 #pragma unroll
-  for (int i = 0; i < 1024 / (NW * 64); ++i) {
-    const int p = tid + NW * 64 * i, reg = p >> 6, ln = p & 63;
-    const int R = R0 + (reg & 3) + 8 * (reg >> 2) + 4 * (ln >> 5), n = n0 + (ln & 31);
-    if (R >= P.rows) continue;
+  for (int i = 0; i < NE; ++i) {
+    rege[i] = (tid + NW * 64 * i) >> 6;
+    Re[i] = R0 + (rege[i] & 3) + 8 * (rege[i] >> 2) + 4 * (ln >> 5);
+    if constexpr (!GATE) {
+      const long long o = (long long)min(Re[i], P.rows - 1) * C + n;
+      xo[i] = P.x[o];
+      so[i] = P.skip[o];
+    }
+  }
+  const float bias0 = P.bias[n], bias1 = P.bias[C + n];
+  const float rs2 = 0.70710678118654752440f;
+  const int nbytes = P.rows * C * 4;
+  const __amdgpu_buffer_rsrc_t rg_ = __builtin_amdgcn_make_buffer_rsrc(GATE ? P.g : P.x, 0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_ = __builtin_amdgcn_make_buffer_rsrc(GATE ? P.g : P.skip, 0, nbytes, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int reg = rege[i];
     float v0 = red[0][0][reg][ln], v1 = red[0][1][reg][ln];   // partials in wave (= K) order
 #pragma unroll
     for (int w = 1; w < NW; ++w) { v0 += red[w][0][reg][ln]; v1 += red[w][1][reg][ln]; }
-    v0 += P.bias[n];
-    v1 += P.bias[C + n];
+    v0 += bias0;
+    v1 += bias1;
+    const int off = (Re[i] * C + n) * 4;   // >= nbytes past the last row: dropped
     if constexpr (GATE) {
-      P.g[(long long)R * C + n] = sigmoidf_(v0) * tanhf_(v1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, sigmoidf_(v0) * tanhf_(v1)), rg_, off, 0, 0);
     } else {
-      float* xp = P.x + (long long)R * C + n;
-      *xp = (*xp + v0) * rs2;
-      float* sp = P.skip + (long long)R * C + n;
-      *sp = P.first ? v1 : (*sp + v1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, (xo[i] + v0) * rs2), rg_, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, P.first ? v1 : (so[i] + v1)), rs_, off, 0, 0);
     }
   }
 }
