@@ -155,12 +155,13 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
 
 
 # bench tag -> kernel symbols that can serve it (the default kernel first) for the PMC
-# traffic lookup; the first one present in a summary is used
+# traffic lookup; the first one present in a summary is used.  The LVC prefixes stop before
+# the last template arguments (r04 added the tiles-per-wave argument).
 TAG_KERNEL = {
-    "fd_lvc_block_final": ("lvc_block_bf16_kernel<384, true, true, true, true, false>",),
-    "fd_lvc_block_ups": ("lvc_block_bf16_kernel<384, true, false, false, true, false>",),
-    "fd_lvc_block_sub": ("lvc_block_bf16_kernel<256, true, false, false, false, true>",
-                         "lvc_block_bf16_kernel<128, true, false, false, false, true>"),
+    "fd_lvc_block_final": ("lvc_block_bf16_kernel<384, true, true, true, true, false,",),
+    "fd_lvc_block_ups": ("lvc_block_bf16_kernel<384, true, false, false, true, false,",),
+    "fd_lvc_block_sub": ("lvc_block_bf16_kernel<256, true, false, false, false, true,",
+                         "lvc_block_bf16_kernel<128, true, false, false, false, true,"),
     "fd_kp_kernel": ("kp_kernel_bf16_kernel",),
     "wn_layer": ("wn_layer_bf16_kernel",),
     "wn_gate2": ("wn_gate_bf16_kernel",),

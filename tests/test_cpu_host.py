@@ -208,7 +208,9 @@ def test_bench_traffic_keyed_by_workload(tmp_path):
     import json
     import bench
     f = tmp_path / "r09_v1_traffic.json"
-    sym = "void (anonymous namespace)::lvc_block_bf16_kernel<384, true, true, true, true, false>((anonymous namespace)::LvcBlockArgs)"
+    # the current instantiation (r04 added the tiles-per-wave argument; a pattern that ended at
+    # `false>` matched only round-3 summaries)
+    sym = "void (anonymous namespace)::lvc_block_bf16_kernel<384, true, true, true, true, false, 2>((anonymous namespace)::LvcBlockArgs)"
     json.dump({"bench_tag": "fd_lvc_block_final", "config": "C3", "batch": 8, "frames": 861,
                "kernels": {sym: {"traffic_bytes_per_launch": 1.0e8, "launches": 4}}}, open(f, "w"))
     assert bench.pmc_traffic("fd_lvc_block_final", "C3", 8, 861, str(f))[0] == 1.0e8
