@@ -1067,16 +1067,20 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
 #ifndef DB_NW
 #define DB_NW 5
 #endif
+#ifndef DB_WPE
+#define DB_WPE 5   // waves per SIMD: 4 blocks of 5 waves per CU (<= 96 VGPRs; the LDS allows 4);
+                   // the AF = 16 window (8 loads per thread) keeps 4 (it spilled at 96)
+#endif
 constexpr int DB_TS = 128, DB_ROWS = 168, DB_LD = 40, DB_NT = 64 * DB_NW;
 template <int AF>
-__global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(4))) void dblock_bf16_kernel(const float* __restrict__ in, float* __restrict__ out,
+__global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(AF > 4 ? 4 : DB_WPE))) void dblock_bf16_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                           const __bf16* __restrict__ W0, const float* __restrict__ b0,
                                                           const __bf16* __restrict__ W1, const float* __restrict__ b1,
                                                           const __bf16* __restrict__ W2, const float* __restrict__ b2,
                                                           int Lout, int f, const float* __restrict__ audio,
                                                           const float* __restrict__ fw, const float* __restrict__ fb) {
   // U0 = lrelu(x[f i]) is dead after the first conv, so h2 reuses its rows: 3 x 13 KB of
-  // bf16 images (+ the audio window) let 3 blocks share a CU
+  // bf16 images
   __shared__ __attribute__((aligned(16))) __bf16 U0[DB_ROWS * DB_LD];   // lrelu(x[f i]), then h2
   __shared__ __attribute__((aligned(16))) __bf16 R0[DB_ROWS * DB_LD];   // x[f i] (residual input)
   __shared__ __attribute__((aligned(16))) __bf16 H1[DB_ROWS * DB_LD];
@@ -1087,7 +1091,11 @@ __global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(4))) void
                                  // waits at every branch join of the staging
   constexpr int DB_AUM = (DB_TS + 14) * (AUD ? AF : 0) + 8;
   constexpr int DB_AUI = (DB_AUM + DB_NT - 1) / DB_NT;
-  __shared__ float AU[DB_AUM];
+  // the audio window is dead once the staging has read it (before the barrier that precedes the
+  // first write of H1), so it lives in H1's rows: 3 images (40.3 KB) let 4 blocks share a CU
+  // where a separate window (43 KB) left room for 3
+  static_assert(DB_AUM * 4 <= DB_ROWS * DB_LD * 2, "audio window must fit in H1");
+  float* AU = reinterpret_cast<float*>(H1);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, i0 = blockIdx.x * DB_TS, ib = i0 - 7;
   const long long Lin = (long long)Lout * f;
@@ -1181,8 +1189,6 @@ __global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(4))) void
   }
 #pragma unroll
   for (int kk = 0; kk < 6; ++kk) wf1[kk] = *reinterpret_cast<const bf16x8*>(W1 + r32 * 96 + kk * 16 + h * 8);
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) wf2[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
   __syncthreads();
   // one dilated 32->32 conv stage over 5 row tiles starting at local row `first`
   auto stage = [&](const __bf16* In, __bf16* Out, const bf16x8 (&wf)[6], float bv, int first, int dil) {
@@ -1214,6 +1220,10 @@ __global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(4))) void
     }
   };
   stage(U0, H1, wf0, bv0, 1, 1);    // h1 on p in [1, 161)
+  // the last stage's fragments only now (wf0 is dead): all three sets live at once needed
+  // 109 VGPRs, over the 96 that 5 waves per SIMD (4 blocks per CU) allow
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) wf2[kk] = *reinterpret_cast<const bf16x8*>(W2 + r32 * 128 + kk * 16 + h * 8);
   __syncthreads();
   stage(H1, H2, wf1, bv1, 3, 2);    // h2 on p in [3, 163)
   __syncthreads();
