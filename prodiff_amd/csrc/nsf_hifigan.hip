@@ -515,7 +515,10 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
   const int p2 = (taps - 1) / 2, p1 = (taps - 1) * dil / 2;
   const int WX = 32 * RT1 + (taps - 1) * dil;            // x window rows
   __bf16* xwin = nsf_win;                                // [WX][LDA]: lrelu(x), time t0 - p2 - p1 + j
-  __bf16* xtw = nsf_win + WX * LDA;                      // [32 RT1][LDA]: lrelu(xt), time t0 - p2 + i
+  // [32 RT1][LDA]: lrelu(xt), time t0 - p2 + i.  It takes x's window rows (32 RT1 <= WX) once every
+  // wave's c1 is done (a barrier between c1's MFMAs and its epilogue): one window per block, so 2
+  // blocks share a CU at C = 128 (r04: x and xt side by side, 88-101 KB, left room for one)
+  __bf16* xtw = nsf_win;
   stage_window<C, false>(x, b, Tl, t0 - p2 - p1, WX, NSF_LRELU, 1.f, xwin, LDA, tid);
   __syncthreads();
   const int S = taps * KS;
@@ -556,6 +559,7 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
     // xt = bf16(acc + b1) (the two-launch path's bf16 intermediate), then c2's input lrelu(xt)
     // rounded to bf16 again; rows outside the utterance are c2's zero padding
     const float bn = b1[n];
+    __syncthreads();   // x's window is dead: xt overwrites it
 #pragma unroll
     for (int m = 0; m < MF1; ++m) {
       const int rt = rg + RG * m;
@@ -629,7 +633,8 @@ template <int C>
 int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
                   hipStream_t st) {
   constexpr int FMO = C == 32 ? 7 : 4, TM = 32 * FMO;
-  const size_t lds = (size_t)(32 * (FMO + 1) * 2 + (c1.taps - 1) * c1.dil) * (C + 8) * sizeof(__bf16);
+  // x / xt window + stage_window's spare row
+  const size_t lds = (size_t)(32 * (FMO + 1) + (c1.taps - 1) * c1.dil + 1) * (C + 8) * sizeof(__bf16);
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&nsf_pair_kernel<C, FMO>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) { set_error("nsf pair: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
