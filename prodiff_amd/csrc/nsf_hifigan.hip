@@ -497,8 +497,8 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
 // path's bf16 intermediate, applies lrelu and keeps them in LDS; c2 reads that window.  Per
 // output row this drops the intermediate's HBM write and read and the second staging of x.
 // Waves: column tile ct = wave % NCT (NCT = C / 32) of both convs; with NCT = 2 the row tiles are
-// split between two wave pairs by parity, with NCT = 1 (C = 32, r04) between all four waves (FMO = 7:
-// 8 c1 row tiles and 7 c2 row tiles over 4 waves).
+// split between two wave pairs by parity, with NCT = 1 (C = 32, r04) between all four waves (FMO = 15:
+// 16 c1 row tiles and 15 c2 row tiles over 4 waves).
 template <int C, int FMO>
 __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restrict__ x, const __bf16* __restrict__ w1,
                                                       const __bf16* __restrict__ w2, int ldw, int kpad,
