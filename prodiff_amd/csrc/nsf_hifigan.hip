@@ -635,7 +635,10 @@ int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, i
 #ifndef NSF_PAIR_FMO32
 #define NSF_PAIR_FMO32 15   // C = 32 output row tiles per block (r04: 7 -> 15, C5 -3%)
 #endif
-  constexpr int FMO = C == 32 ? NSF_PAIR_FMO32 : 4, TM = 32 * FMO;
+#ifndef NSF_PAIR_FMO64
+#define NSF_PAIR_FMO64 4
+#endif
+  constexpr int FMO = C == 32 ? NSF_PAIR_FMO32 : C == 64 ? NSF_PAIR_FMO64 : 4, TM = 32 * FMO;
   // x / xt window + stage_window's spare row
   const size_t lds = (size_t)(32 * (FMO + 1) + (c1.taps - 1) * c1.dil + 1) * (C + 8) * sizeof(__bf16);
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&nsf_pair_kernel<C, FMO>),
