@@ -67,6 +67,10 @@ CONFIGS = {
 }
 
 
+WN_LAYERS, WN_STACK_NL = 20, 10          # residual layers; layers per wn_stack_bf16_kernel launch
+FD_STEPS, FD_BLOCKS = 4, 3                # FastDiff sampler passes per call; LVC blocks (hop 8, 64, 256)
+
+
 def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256):
     """Algorithmic FLOPs (2 x MAC) of ONE launch of each tagged kernel.
     Tags used by several block sizes report the mean over their launches in one call."""
@@ -75,10 +79,19 @@ def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256):
     d_rows = [F * 64, F * 8, F]                       # DBlock output rates (L/4, L/32, L/256)
     dblock = sum(2 * r * 32 * 96 * 2 + 2 * r * 32 * 128 for r in d_rows) / 9.0
     kp_layers = 4 if dtype == "bf16" else 1           # bf16: one launch computes all 4 layers' kernels
+    gate, resskip = 2 * F * 2 * C * (3 * C + H), 2 * F * 2 * C * C
+    nstack = -(-WN_LAYERS // WN_STACK_NL)
     return {
         "wn_inproj": 2 * F * M * C,
-        "wn_gate": 2 * F * 2 * C * (3 * C + H),
-        "wn_resskip": 2 * F * 2 * C * C,
+        "wn_gate": gate,
+        "wn_resskip": resskip,
+        # one sampler pass = nstack launches: the first also computes the input projection, the
+        # last the skip head + output projection (+ posterior); mean over the pass's launches
+        "wn_stack": (WN_LAYERS * (gate + resskip) + 2 * F * M * C + 2 * F * C * C + 2 * F * M * C) / nstack,
+        "wn_condb": 0.0,
+        # kernel-predictor hidden stacks of every (step, block) of one sampler call in one launch:
+        # conv5 80 -> 64, 6 x conv3 64 -> 64, bias conv3 64 -> 256
+        "fd_kp_hidden": FD_STEPS * FD_BLOCKS * 2 * F * (64 * 80 * 5 + 6 * 64 * 64 * 3 + 256 * 64 * 3),
         "wn_layer": 2 * F * 2 * C * (3 * C + H) + 2 * F * 2 * C * C,     # fused gate + res/skip (bf16)
         "wn_gate2": 2 * F * 2 * C * (3 * C + H),                            # two-kernel layer (bf16)
         "wn_resskip2": 2 * F * 2 * C * C * 39 / 40,                          # last of 20 layers: skip half only
@@ -121,8 +134,16 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
     # fused LVC (hop >= 64): x read+write, audio_down read, this layer's kernels+biases
     lvc_f = [r * 3 * per_row_io + F * kf_frame for r in rows[1:]]
     lvc_v = [r * 4 * per_row_io + F * kf_frame for r in rows]          # unfused: x r/w, a, y
+    layer_w = 2 * C * (4 * C + H) * wb
+    nstack = -(-WN_LAYERS // WN_STACK_NL)
     return {
         "wn_inproj": F * (M + C) * 4 + C * M * wb,
+        # first launch: spec in, bf16 cond in, x and skip out; last: x and skip in, bf16 cond in,
+        # mel read + written (posterior); inner launches (none at 20 layers / 10): x, skip in + out.
+        # Plus each launch's layers' weights once (the compulsory HBM bytes; blocks re-read them from L2)
+        "wn_stack": (F * (M * 4 + H * 2 + 2 * C * 4) + F * (2 * C * 4 + H * 2 + 2 * M * 4) +
+                     max(nstack - 2, 0) * F * (4 * C * 4 + H * 2)) / nstack + WN_STACK_NL * layer_w,
+        "wn_condb": F * H * (4 + 2),
         "wn_gate": F * (C + H + C) * 4 + 2 * C * (3 * C + H) * wb,
         "wn_resskip": F * (C + 2 * C + 2 * C) * 4 + 2 * C * C * wb,
         "wn_layer": F * (C + H + C + 2 * C) * 4 + 2 * C * (4 * C + H) * wb,
@@ -139,7 +160,9 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
         "fd_dblock_fused": sum(r * 2 * per_row_io for r in (F * 64, F * 8, F)) / 3.0,
         # h in (bf16 / fp32), every layer's 6144 kernel values per frame out, weights once
         "fd_kp_kernel": F * (64 * wb + kp_layers * 6144 * wb) + kp_layers * 6144 * 192 * wb,
-        "fd_kp_hidden": F * (80 + 64 + 256) * 4 + (64 * 480 + 6 * 64 * 192 + 256 * 192) * wb,
+        # per (step, block) job: mel in, bf16 h out, fp32 LVC biases out, the block's weights
+        "fd_kp_hidden": FD_STEPS * FD_BLOCKS * (F * (80 * 4 + 64 * 2 + 256 * 4) +
+                                                (64 * 480 + 6 * 64 * 192 + 256 * 192) * wb),
         "fd_lvc_fused": sum(lvc_f) / 2.0,
         # x in + a in + x out once per block, plus all 4 layers' kernels and biases
         "fd_lvc_block": sum(r * 3 * per_row_io + F * 4 * kf_frame for r in rows[1:]) / 2.0,
@@ -158,16 +181,50 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
 # traffic lookup; the first one present in a summary is used.  The LVC prefixes stop before
 # the last template arguments (r04 added the tiles-per-wave argument).
 TAG_KERNEL = {
-    "fd_lvc_block_final": ("lvc_block_bf16_kernel<384, true, true, true, true, false,",),
-    "fd_lvc_block_ups": ("lvc_block_bf16_kernel<384, true, false, false, true, false,",),
+    # the default (two tiles per wave) instantiation first: a summary may hold both
+    "fd_lvc_block_final": ("lvc_block_bf16_kernel<384, true, true, true, true, false, 2>",
+                           "lvc_block_bf16_kernel<384, true, true, true, true, false,"),
+    "fd_lvc_block_ups": ("lvc_block_bf16_kernel<384, true, false, false, true, false, 2>",
+                         "lvc_block_bf16_kernel<384, true, false, false, true, false,"),
     "fd_lvc_block_sub": ("lvc_block_bf16_kernel<256, true, false, false, false, true,",
                          "lvc_block_bf16_kernel<128, true, false, false, false, true,"),
     "fd_kp_kernel": ("kp_kernel_bf16_kernel",),
+    "fd_kp_hidden": ("kp_hidden_bf16_kernel",),
+    "fd_dblock_fused": ("dblock_bf16_kernel",),
+    "wn_stack": ("wn_stack_bf16_kernel",),
     "wn_layer": ("wn_layer_bf16_kernel",),
     "wn_gate2": ("wn_gate_bf16_kernel",),
     "wn_resskip2": ("wn_resskip_bf16_kernel",),
+    "nsf_pair": ("nsf_pair_kernel<",),
     "nsf_res": ("nsf_wconv_kernel<",),
+    "nsf_ups": ("nsf_ups_kernel<",),
 }
+DENOISER_TAGS = ("wn_stack", "wn_condb", "wn_layer", "wn_gate", "wn_resskip", "wn_gate2", "wn_resskip2", "wn_xa",
+                 "wn_inproj", "wn_skiphead", "wn_outproj", "wn_outproj_posterior", "wn_f32_tail")
+
+
+def dominant_kernel(kern_all, fl, by):
+    """The tag with the most GPU time in the all-launch profile.  Every tag that can be the slowest
+    must be in the FLOP and byte tables: an untagged slowest kernel is an error, not a reason to
+    report the roofline of a smaller one."""
+    dom = max(kern_all.items(), key=lambda kv: kv[1][1])[0]
+    if dom not in fl or dom not in by:
+        raise SystemExit(f"bench.py: the slowest kernel tag {dom!r} has no FLOP/byte entry "
+                         f"(flops_per_launch / bytes_per_launch / svs_tables)")
+    return dom
+
+
+def lib_sha16(path=None):
+    """First 16 hex digits of the loaded library's sha256 (profile summaries record the one they
+    were measured on)."""
+    import hashlib
+    if path is None:
+        from prodiff_amd import _lib
+        path = _lib.LIB_PATH
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
 
 
 def traffic_workload(d, fname):
@@ -201,7 +258,10 @@ def sq_utilisation(config):
     _, f, d = best
     ks = [{k: r.get(k) for k in ("kernel", "avg_us_profiled", "mfma_busy", "valu_busy", "wait_any", "wait_inst")}
           for r in d["kernels"]]
+    src_lib = d.get("lib_sha16")
     return {"source": os.path.relpath(f, ROOT), "kernels": ks,
+            "source_lib_sha16": src_lib, "running_lib_sha16": lib_sha16(),
+            "same_library": bool(src_lib) and src_lib == lib_sha16(),
             "note": "rocprofv3 SQ counters, separate passes: mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x cycles), "
                     "valu_busy = 4 SQ_ACTIVE_INST_VALU / (SIMDs x cycles), wait_* = fractions of SQ_WAVE_CYCLES"}
 
@@ -211,12 +271,13 @@ def pmc_traffic(tag, config, batch, frames, path=None):
     measured on the SAME workload (config, per-GPU batch, frames) -- profiles/rNN_vMM_traffic.json,
     written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
     of the bench command.  A tag served by several template instantiations (nsf_res) gets the
-    launch-weighted mean.  (None, None) when no summary of this workload holds the kernel."""
+    launch-weighted mean.  Returns (bytes per launch, summary path, the library sha16 the summary
+    records); (None, None, None) when no summary of this workload holds the kernel."""
     import glob
     import re
     syms = TAG_KERNEL.get(tag)
     if syms is None:
-        return None, None
+        return None, None, None
     if path is None:
         def ver(f):
             m = re.search(r"r(\d+)_v(\d+)[a-z0-9_]*_traffic\.json$", f)
@@ -237,8 +298,8 @@ def pmc_traffic(tag, config, batch, frames, path=None):
             if hits:
                 n = sum(v["launches"] for v in hits)
                 tb = sum(v["traffic_bytes_per_launch"] * v["launches"] for v in hits) / n
-                return float(tb), os.path.relpath(fpath, ROOT)
-    return None, None
+                return float(tb), os.path.relpath(fpath, ROOT), d.get("lib_sha16")
+    return None, None, None
 
 
 def nsf_stage_dims(h=None):
@@ -251,35 +312,79 @@ def nsf_stage_dims(h=None):
     return out
 
 
-def svs_flops_per_launch(B, T, Tt, small_max=16, H=256, k_ffn=9):
-    """Condition-encoder and NSF-HiFiGAN launch FLOPs (per launch; nsf_res = mean over its launches)."""
-    rows = B * Tt
-    F = B * T
-    res = [(2 * F * r * 6 * c * c * (3 + 7 + 11), c) for r, c in nsf_stage_dims()]   # 6 convs x 3 kernels / stage
-    big = [f for f, c in res if c > small_max]
-    small = [f for f, c in res if c <= small_max]
-    return {"enc_qkv": 2 * rows * H * 3 * H, "enc_outproj": 2 * rows * H * H, "enc_ffn1": 2 * rows * H * 4 * H * k_ffn,
-            "enc_ffn2": 2 * rows * 4 * H * H, "enc_attn": 2 * 2 * B * Tt * Tt * H,
-            "nsf_res": sum(big) / (18 * len(big)) if big else 0.0,
-            "nsf_res_small": sum(small) / (18 * len(small)) if small else 0.0}
+NSF_PAIR_C = (32, 64, 128)     # ResBlock1 conv pairs fused into one nsf_pair launch (bf16, NSF_OPT_PAIR)
+NSF_KS = (3, 7, 11)            # resblock kernel sizes; 3 dilation pairs each (ResBlock1)
+NSF_HOP, NSF_MELS, NSF_C0, NSF_HARM = 512, 128, 512, 9
 
 
-def svs_bytes_per_launch(B, T, Tt, dtype, small_max=16, H=256):
+def _mean(xs):
+    return sum(xs) / len(xs) if xs else 0.0
+
+
+def svs_tables(B, T, Tt, dtype, small_max=16, H=256, k_ffn=9):
+    """(FLOPs, compulsory HBM bytes) of ONE launch of each condition-encoder / NSF-HiFiGAN tag;
+    a tag launched at several stages reports the mean over its launches in one forward.
+    NSF stage s (nsf_stage_dims) runs at r_s samples per mel frame with C_s channels: its 3
+    ResBlock1s (k = 3, 7, 11) hold 3 (c1, c2) conv pairs each; pairs with C in NSF_PAIR_C run as
+    one nsf_pair launch (bf16), the other stages' convs as single launches (nsf_res for
+    C > small_max, nsf_res_small otherwise)."""
     wb = 2 if dtype == "bf16" else 4
     F = B * T
     rows = B * Tt
-    res = [(F * r * c * 4 * 2.5 * 18 + 6 * c * c * 21 * wb, c) for r, c in nsf_stage_dims()]   # in, out, 1/2 res
-    big = [b for b, c in res if c > small_max]
-    small = [b for b, c in res if c <= small_max]
-    return {"enc_qkv": rows * 4 * H * 4 + 3 * H * H * wb, "enc_outproj": rows * 3 * H * 4 + H * H * wb,
-            "enc_ffn1": rows * 5 * H * 4 + 4 * H * H * 9 * wb, "enc_ffn2": rows * 6 * H * 4 + 4 * H * H * wb,
-            "enc_attn": rows * 4 * H * 4,
-            "nsf_res": sum(big) / (18 * len(big)) if big else 0.0,
-            "nsf_res_small": sum(small) / (18 * len(small)) if small else 0.0}
+    st = nsf_stage_dims()
+    paired = [(r, c) for r, c in st if dtype == "bf16" and c in NSF_PAIR_C]
+    single = [(r, c) for r, c in st if (r, c) not in paired]
+    fl, by = {}, {}
+    # pair (k, d): c1 (k, dil d) and c2 (k, dil 1) over F r rows; x read once (fp32), the pair's
+    # output written once (fp32), the last pair of resblocks 1, 2 also reads + writes the ResBlock sum
+    pf, pb = [], []
+    for r, c in paired:
+        for k in NSF_KS:
+            for q in range(3):
+                pf.append(2 * 2 * F * r * c * c * k)
+                acc = q == 2 and k != NSF_KS[0]
+                pb.append(F * r * c * 4 * (2 + (1 if acc else 0)) + 2 * c * c * k * wb)
+    fl["nsf_pair"], by["nsf_pair"] = _mean(pf), _mean(pb)
+    for tag, sel in (("nsf_res", lambda c: c > small_max), ("nsf_res_small", lambda c: c <= small_max)):
+        cf, cb = [], []
+        for r, c in single:
+            if not sel(c):
+                continue
+            for k in NSF_KS:
+                for _ in range(6):          # 3 pairs x (c1, c2), one launch each
+                    cf.append(2 * F * r * c * c * k)
+                    cb.append(F * r * c * 4 * 2.5 + c * c * k * wb)     # in, out, half of them a residual
+        fl[tag], by[tag] = _mean(cf), _mean(cb)
+    # ConvTranspose1d (k = 2u: 2 taps per output row) + the noise-conv add
+    uf, ub, nf, nb_ = [], [], [], []
+    r_in, c_in = 1, NSF_C0
+    for r, c in st:
+        uf.append(2 * F * r * c_in * c * 2)
+        ub.append(F * r_in * c_in * 4 + 2 * F * r * c * 4 + c_in * c * 2 * (r // r_in) * wb)
+        sf = NSF_HOP // r
+        K = 2 * sf if sf > 1 else 1
+        nf.append(2 * F * r * c * K)
+        nb_.append(F * NSF_HOP * 4 + F * r * c * 4)
+        r_in, c_in = r, c
+    fl["nsf_ups"], by["nsf_ups"] = _mean(uf), _mean(ub)
+    fl["nsf_noise_conv"], by["nsf_noise_conv"] = _mean(nf), _mean(nb_)
+    rl, cl = st[-1]
+    fl["nsf_post"], by["nsf_post"] = 2 * F * rl * cl * 7, F * rl * (cl + 1) * 4
+    fl["nsf_conv_pre"], by["nsf_conv_pre"] = 2 * F * NSF_MELS * NSF_C0 * 7, F * (NSF_MELS + NSF_C0) * 4
+    # SineGen + SourceModule: 9 harmonics per sample (sin on the VALU), har written once
+    fl["nsf_source"], by["nsf_source"] = 2 * F * NSF_HOP * NSF_HARM * 2, F * NSF_HOP * 4 + F * 8
+    fl.update({"enc_qkv": 2 * rows * H * 3 * H, "enc_outproj": 2 * rows * H * H,
+               "enc_ffn1": 2 * rows * H * 4 * H * k_ffn, "enc_ffn2": 2 * rows * 4 * H * H,
+               "enc_attn": 2 * 2 * B * Tt * Tt * H, "enc_ln": 0.0, "enc_embed": 0.0, "enc_cond": 0.0})
+    by.update({"enc_qkv": rows * 4 * H * 4 + 3 * H * H * wb, "enc_outproj": rows * 3 * H * 4 + H * H * wb,
+               "enc_ffn1": rows * 5 * H * 4 + 4 * H * H * 9 * wb, "enc_ffn2": rows * 6 * H * 4 + 4 * H * H * wb,
+               "enc_attn": rows * 4 * H * 4, "enc_ln": rows * H * 8, "enc_embed": rows * H * 4,
+               "enc_cond": F * H * 4})
+    return fl, by
 
 
 def svs_step_flops(B, T, Tt):
-    f = svs_flops_per_launch(B, T, Tt, small_max=0)
+    f, _ = svs_tables(B, T, Tt, "fp32", small_max=0)
     enc = 4 * (f["enc_qkv"] + f["enc_outproj"] + f["enc_ffn1"] + f["enc_ffn2"] + f["enc_attn"])
     nsf = 18 * 5 * f["nsf_res"]
     ups = 0
@@ -352,6 +457,34 @@ def port_cpu_baseline(frames, vocoder=True):
                       f"({audio_s:.2f} s audio), 2-iter ProDiff" + (" + 4-iter FastDiff" if vocoder else "") +
                       f", median of 3 after 1 warm-up: {dt:.2f} s",
             "rtf": round(dt / audio_s, 4)}
+
+
+def denoiser_roofline(kern_all, nprof, B, T, cfg, dtype, peak_tf, cfg_name):
+    """The north star's denoiser figure: the WaveNet residual stack (every launch of the ProDiff
+    sampler's denoiser, tags DENOISER_TAGS) against the MFMA roof at its algorithmic FLOPs
+    (26.43 MFLOP per mel frame per pass at M = 80), and -- where a PMC summary of
+    this workload holds the stack kernel -- its measured HBM bytes against the 8 TB/s roof."""
+    M = 128 if cfg.get("svs") else 80
+    tags = [t for t in kern_all if t in DENOISER_TAGS]
+    if not tags:
+        return None
+    ms = sum(kern_all[t][1] for t in tags)
+    passes = cfg["timesteps"]
+    flop = passes * prodiff_step_flops(B, T, M=M) * nprof
+    ach = flop / (ms * 1e-3) / 1e12
+    out = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
+           "frac": round(ach / peak_tf, 4), "kernels": sorted(tags), "ms_per_step": round(ms / nprof, 3),
+           "flop_per_step": passes * prodiff_step_flops(B, T, M=M),
+           "timing": "the untimed all-launch pass (HIP events around every launch)"}
+    if "wn_stack" in kern_all:
+        tb, src, tlib = pmc_traffic("wn_stack", cfg_name, B, T)
+        if tb:
+            cnt, sms = kern_all["wn_stack"]
+            gbs = tb * cnt / (sms * 1e-3) / 1e9
+            out["hbm"] = {"kernel": "wn_stack", "traffic_bytes_per_launch": round(tb), "achieved": round(gbs, 1),
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                          "source": src, "same_library": bool(tlib) and tlib == lib_sha16()}
+    return out
 
 
 def free_port():
@@ -495,8 +628,9 @@ def main():
     if svs:
         fl = flops_per_launch(B, T, dtype, M=128)
         by = bytes_per_launch(B, T, dtype, M=128)
-        fl.update(svs_flops_per_launch(B, T, cfg["tokens"]))
-        by.update(svs_bytes_per_launch(B, T, cfg["tokens"], dtype))
+        sf, sb = svs_tables(B, T, cfg["tokens"], dtype)
+        fl.update(sf)
+        by.update(sb)
     else:
         fl = flops_per_launch(B, T, dtype)
         by = bytes_per_launch(B, T, dtype)
@@ -518,8 +652,7 @@ def main():
         torch.cuda.synchronize()
         kern_all = _lib.profile_summary()
         _lib.profile_enable(False)
-        known = {k: v for k, v in kern_all.items() if k in fl and k in by}
-        dom = max(known.items(), key=lambda kv: kv[1][1])[0]
+        dom = dominant_kernel(kern_all, fl, by)
         _lib.profile_filter([dom])
         _lib.profile_enable(True)
     if not dry:
@@ -552,8 +685,7 @@ def main():
             gd.sample(cond_b, seed=10_000 * i)
         torch.cuda.synchronize()
         kern_all = _lib.profile_summary()
-        known = {k: v for k, v in kern_all.items() if k in fl and k in by}
-        dom = max(known.items(), key=lambda kv: kv[1][1])[0]
+        dom = dominant_kernel(kern_all, fl, by)
         _lib.profile_filter([dom])
         _lib.profile_enable(True)
         for i in range(args.steps):
@@ -611,10 +743,11 @@ def main():
             ach = fl[dom] * cnt / sec / 1e12
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
                         "frac": round(ach / peak_tf, 4)}
-        traffic, tsrc = pmc_traffic(dom, cfg_name, B, T, args.traffic)
+        traffic, tsrc, tlib = pmc_traffic(dom, cfg_name, B, T, args.traffic)
         roofline.update({"bound_basis": "model estimate: algorithmic intensity vs the ridge; the measured limiter "
                                         "is in `utilisation` (MFMA / VALU busy, wait fractions)",
-                         "traffic": round(traffic) if traffic else None, "traffic_source": tsrc, "kernel": dom,
+                         "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
+                         "traffic_same_library": bool(tlib) and tlib == lib_sha16(), "kernel": dom,
                          "flop_per_launch": fl[dom], "bytes_per_launch": by.get(dom),
                          "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(ridge, 1),
                          "avg_launch_us": round(ms / cnt * 1e3, 2), "launches": cnt,
@@ -622,6 +755,7 @@ def main():
                          "timing": ("HIP events around this kernel only, over untimed eager runs of the same "
                                     "sampler (the timed steps replay a hipGraph)") if graph_prof else
                                    "HIP events around this kernel only, over the timed steps"})
+        roofline["denoiser"] = denoiser_roofline(kern_all, nprof, B, T, cfg, dtype, peak_tf, cfg_name)
     if svs:
         step_fl = svs_step_flops(n_total, T, cfg["tokens"])
     else:
@@ -657,6 +791,7 @@ def main():
                            f"HIP events") if kernels else None,
         "cpu_baseline": None,
         "cpu_baseline_port": None,
+        "build": None if dry else {"pd_build_config": _lib.lib().pd_build_config().decode(), "lib_sha16": lib_sha16()},
         "dry_run": dry,
     }
     if rank == 0 and world == 1 and not dry:

@@ -40,6 +40,10 @@ extern "C" {
 
 const char* pd_last_error(void);
 int pd_version(void);
+/* "default" for the shipped build; otherwise the non-default compile-time knobs it was built with
+ * (A/B variant libraries, tools/build_variant_lib.sh).  bench.py records it; the GPU tests refuse a
+ * variant library unless PRODIFF_ALLOW_VARIANT=1. */
+const char* pd_build_config(void);
 
 /* Per-launch timing for benchmarks: when enabled, HIP events are recorded on the
  * launch stream around every hot-path kernel (tagged by use, e.g. "fd_kp_kernel").
@@ -350,7 +354,7 @@ typedef struct {
   int use_dur_embed, use_spk_id, use_gender_id, use_lang_id, use_voicing_embed, use_breath_embed;
   int rel_pos;               /* > 0: RelPositionalEncoding (tts_modules.py:299-300,324-325,
                                 espnet_positional_embedding.py:89-115) instead of the sinusoid,
-                                with a table of max(rel_pos, 5000 if rel_pos == 1) rows: the
+                                with a table of max(rel_pos, 5000) rows (< 0 rejected): the
                                 reference's table starts at 5000 rows and extend_pe (:24-45)
                                 keeps the longest input's length, which then sets the
                                 reversed positions of every later, shorter batch         */

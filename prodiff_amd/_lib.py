@@ -66,6 +66,7 @@ _VP = C.c_void_p
 _SIGS = {
     "pd_last_error": (C.c_char_p, []),
     "pd_version": (C.c_int, []),
+    "pd_build_config": (C.c_char_p, []),
     "pd_profile_enable": (C.c_int, [C.c_int]),
     "pd_profile_summary": (C.c_int, [C.c_char_p, C.c_int]),
     "pd_profile_filter": (C.c_int, [C.c_char_p]),

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void enc_embed_kernel(
       if (lr) extra = extra + lr[c];
       float v;
       if (rel_pos) {
-        const int P = rel_pos > 1 ? rel_pos : 5000;
+        const int P = rel_pos > 5000 ? rel_pos : 5000;   // the reference table never has fewer than 5000 rows
         const float q = (float)((Tt > P ? Tt : P) - 1 - t);
         const float arg = q * expf((float)(c & ~1) * neg_rel);
         v = (scale * er[c] + extra) * scale + ((c & 1) ? cosf(arg) : sinf(arg));
@@ -412,6 +412,7 @@ int pd_cond_create(const pd_cond_dims* dims, const float* const* params, int dty
   PD_CHECK_ARG(dtype == PD_DTYPE_F32 || dtype == PD_DTYPE_BF16, "dtype must be PD_DTYPE_F32 or PD_DTYPE_BF16");
   PD_CHECK_ARG(d.hidden_size > 0 && d.hidden_size % 64 == 0, "hidden_size must be a positive multiple of 64");
   PD_CHECK_ARG(d.num_heads > 0 && d.hidden_size % d.num_heads == 0, "hidden_size % num_heads != 0");
+  PD_CHECK_ARG(d.rel_pos >= 0, "rel_pos must be >= 0 (0: sinusoid; > 0: table of max(rel_pos, 5000) rows)");
   const int D = d.hidden_size / d.num_heads;
   if (D != 64 && D != 128 && D != 256) {
     set_error("pd_cond: head dim (hidden_size / num_heads) must be 64, 128 or 256");

@@ -1482,9 +1482,6 @@ constexpr int KP_LDO = 72;                             // output transpose rows:
                                                        // 16-B aligned for the b128 reads; 68 measured 15% slower)
 constexpr int KP_NGROUPS = NLY * KPERLAYER / KP_NG;    // 48
 constexpr int KP_THREADS = 512;
-#ifndef KP_PROBE
-#define KP_PROBE 0
-#endif
 #ifndef KP_STAGGER
 #define KP_STAGGER 1
 #endif
@@ -1569,12 +1566,8 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
     }
     h_load(min(item + 1, ie - 1));   // the next item's frames, under this item's work
     const int nb = ng * KP_NG + wave * 64, layer = nb / KPERLAYER, n0 = nb - layer * KPERLAYER;
-#if KP_PROBE == 2   // diagnostic build (tools/build_variant_lib.sh): every K store dropped
-    const __amdgpu_buffer_rsrc_t kout = __builtin_amdgcn_make_buffer_rsrc(Kf, 0, 0, 0x00020000);
-#else
     const __amdgpu_buffer_rsrc_t kout =
         __builtin_amdgcn_make_buffer_rsrc(Kf + (long long)layer * rows * KPERLAYER, 0, rows * KPERLAYER * 2, 0x00020000);
-#endif
     const __bf16* hs = Hs[buf];
     // C[n][frame]: lane owns frame r32, rows n = 32j + 8g + 4h + (0..3); the accumulators start
     // from the rows' biases, so the epilogue is a conversion only
@@ -1589,12 +1582,8 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
 #pragma unroll
       for (int kk = 0; kk < 12; ++kk) {
         const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&hs[(ft * 32 + r32) * KP_LDH + kk * 16 + h * 8]);
-#if KP_PROBE == 1   // diagnostic build: no MFMAs (the store path and the epilogue alone)
-        acc[0][kk] += (float)hb[0];
-#else
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[kk], hb, acc[0], 0, 0, 0);
         acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[12 + kk], hb, acc[1], 0, 0, 0);
-#endif
       }
     };
     auto epi = [&](int ft, const f32x16 (&acc)[2]) {
@@ -2521,6 +2510,32 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
 }
 
 }  // extern "C"
+
+// Non-default compile-time knobs of this file (pd_build_config): "" for the shipped build.
+namespace pd {
+const char* fastdiff_build_flags() {
+  return ""
+#ifdef LB_TRACE
+         " LB_TRACE"
+#endif
+#ifdef LVC_SCALAR_F32
+         " LVC_SCALAR_F32"
+#endif
+#if DB_NW != 5
+         " DB_NW"
+#endif
+#if DB_WPE != 5
+         " DB_WPE"
+#endif
+#if KP_STAGGER != 1
+         " KP_STAGGER"
+#endif
+#if KP_AUX != 0
+         " KP_AUX"
+#endif
+      ;
+}
+}  // namespace pd
 
 extern "C" int fd_fold_weight_norm(float* w, const float* g, const float* v, int cout, int per_row,
                                    void* stream) {

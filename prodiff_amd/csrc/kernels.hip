@@ -484,4 +484,21 @@ extern "C" int pd_profile_summary(char* buf, int buflen) {
 }
 
 extern "C" const char* pd_last_error(void) { return pd::get_error(); }
-extern "C" int pd_version(void) { return 1; }
+extern "C" int pd_version(void) { return 2; }
+
+namespace pd {
+const char* fastdiff_build_flags();
+const char* nsf_build_flags();
+const char* wavenet_build_flags();
+}  // namespace pd
+
+// "default" for the shipped build, else the non-default compile-time knobs (A/B variant libraries
+// built by tools/build_variant_lib.sh): bench.py records it, the GPU tests refuse a variant build
+// unless PRODIFF_ALLOW_VARIANT=1.
+extern "C" const char* pd_build_config(void) {
+  static const std::string s = [] {
+    std::string f = std::string(pd::fastdiff_build_flags()) + pd::nsf_build_flags() + pd::wavenet_build_flags();
+    return f.empty() ? std::string("default") : f.substr(1);
+  }();
+  return s.c_str();
+}

@@ -304,19 +304,21 @@ constexpr int NSF_WB = 4;
 // pass put a full vmcnt(0) before every one, so a lane's 16 stores ran one round trip apart): a
 // buffer resource spanning exactly one utterance's rows of `out`; stores past its last row are
 // dropped by the hardware range check.
+// The range and the byte offsets are unsigned 32-bit: the host guards (nsf_check_rows) keep one
+// utterance's Tl * C * sizeof(out) below 2^32.
 template <bool OUT_BF>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t nsf_utt_rsrc(void* out, int rowb, int Tl, int C) {
-  const int es = OUT_BF ? 2 : 4;
+  const unsigned es = OUT_BF ? 2u : 4u;
   char* base = reinterpret_cast<char*>(out) + (long long)rowb * C * es;
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, Tl * C * es, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (unsigned)Tl * (unsigned)C * es, 0x00020000);
 }
 template <bool OUT_BF>
 __device__ __forceinline__ void nsf_store_utt(__amdgpu_buffer_rsrc_t r, int elem, float v) {
   if constexpr (OUT_BF) {
     const __bf16 hv = (__bf16)v;
-    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, hv), r, elem * 2, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, hv), r, (unsigned)elem * 2u, 0, 0);
   } else {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, elem * 4, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, (unsigned)elem * 4u, 0, 0);
   }
 }
 
@@ -629,15 +631,15 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
   }
 }
 
-template <int C>
-int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
-                  hipStream_t st) {
 #ifndef NSF_PAIR_FMO32
 #define NSF_PAIR_FMO32 15   // C = 32 output row tiles per block (r04: 7 -> 15, C5 -3%)
 #endif
 #ifndef NSF_PAIR_FMO64
 #define NSF_PAIR_FMO64 8   // C = 64 output row tiles per block (r04: 4 -> 8, C5 -4%)
 #endif
+template <int C>
+int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
+                  hipStream_t st) {
   constexpr int FMO = C == 32 ? NSF_PAIR_FMO32 : C == 64 ? NSF_PAIR_FMO64 : 4, TM = 32 * FMO;
   // x / xt window + stage_window's spare row
   const size_t lds = (size_t)(32 * (FMO + 1) + (c1.taps - 1) * c1.dil + 1) * (C + 8) * sizeof(__bf16);
@@ -1000,8 +1002,9 @@ bool wconv_ok(const NsfConv& c) {
 int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, float scale, int B, int Tl, void* out,
                  bool out_bf, const float* res, hipStream_t st, int accum = 0) {
   const __bf16* wb = lookup_bf16(c.w);
-  if ((long long)B * Tl * c.cout >= (1ll << 31)) {
-    set_error("nsf wconv: B * T * C >= 2^31 elements (32-bit epilogue offsets)");
+  // 32-bit element offsets, and one utterance's bytes inside the unsigned buffer-resource range
+  if ((long long)B * Tl * c.cout >= (1ll << 31) || (long long)Tl * c.cout * 4 >= (1ll << 32)) {
+    set_error("nsf wconv: B * T * C >= 2^31 elements or T * C * 4 >= 2^32 bytes (32-bit epilogue offsets)");
     return PD_ERR_UNSUPPORTED;
   }
   if (out_bf == (res != nullptr)) {   // the kernels' epilogue: fp32 outputs add a residual, bf16 ones none
@@ -1468,3 +1471,23 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
 }
 
 }  // extern "C"
+
+// Non-default compile-time knobs of this file (pd_build_config): "" for the shipped build.
+namespace pd {
+const char* nsf_build_flags() {
+  return ""
+#if NSF_PF_DEPTH != 4
+         " NSF_PF_DEPTH"
+#endif
+#if NSF_RING_PIN != 0
+         " NSF_RING_PIN"
+#endif
+#if NSF_PAIR_FMO32 != 15
+         " NSF_PAIR_FMO32"
+#endif
+#if NSF_PAIR_FMO64 != 8
+         " NSF_PAIR_FMO64"
+#endif
+      ;
+}
+}  // namespace pd

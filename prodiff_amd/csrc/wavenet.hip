@@ -471,14 +471,18 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
         xr[q][reg] = P.xin[(long long)min(max(R, 0), rows - 1) * C + n];
       }
   }
-  {   // (unconditional loads, the first launch's zero by a bit mask: see the cond staging above)
+  {   // (unconditional loads, the first launch's zero by a bit mask: see the cond staging above).
+      // Only this block's output rows [R0, R0 + ro) are read: with ro < 32 the window's rows past
+      // them belong to the next block, which writes them in this launch -- their loads are clamped
+      // to the block's last row and the values masked to zero (they are never stored anyway)
     const unsigned mk = P.first ? 0u : 0xffffffffu;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
-      const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      const float sv = P.skip[(long long)min(max(R, 0), rows - 1) * C + n];
-      SK[sko(i)] = __uint_as_float(__float_as_uint(sv) & mk);
+      const int wrow = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + wrow;
+      const unsigned mo = wrow - 16 < P.ro ? mk : 0u;
+      const float sv = P.skip[(long long)min(max(min(R, R0 + P.ro - 1), 0), rows - 1) * C + n];
+      SK[sko(i)] = __uint_as_float(__float_as_uint(sv) & mo);
     }
   }
   // conv zero padding: tap t-1 / t+1 of the lane's A rows (window row 32q + r32) outside its
@@ -1935,3 +1939,23 @@ int pd_reflow_denorm(const float* x, const float* spec_min, const float* spec_ma
 }
 
 }  // extern "C"
+
+// Non-default compile-time knobs of this file (pd_build_config): "" for the shipped build.
+namespace pd {
+const char* wavenet_build_flags() {
+  return ""
+#ifdef WN_TRACE
+         " WN_TRACE"
+#endif
+#if WST_WD != 6
+         " WST_WD"
+#endif
+#if WF32_RING != 2
+         " WF32_RING"
+#endif
+#if WF32_NW != 8
+         " WF32_NW"
+#endif
+      ;
+}
+}  // namespace pd

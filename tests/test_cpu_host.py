@@ -28,7 +28,8 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.pd_version() == 1
+    assert lib.pd_version() == 2
+    assert lib.pd_build_config() == b"default"
 
 
 def test_null_arguments_fail_loudly():
@@ -214,8 +215,8 @@ def test_bench_traffic_keyed_by_workload(tmp_path):
     json.dump({"bench_tag": "fd_lvc_block_final", "config": "C3", "batch": 8, "frames": 861,
                "kernels": {sym: {"traffic_bytes_per_launch": 1.0e8, "launches": 4}}}, open(f, "w"))
     assert bench.pmc_traffic("fd_lvc_block_final", "C3", 8, 861, str(f))[0] == 1.0e8
-    assert bench.pmc_traffic("fd_lvc_block_final", "C4", 32, 861, str(f)) == (None, None)
-    assert bench.pmc_traffic("fd_lvc_block_final", "C3", 8, 100, str(f)) == (None, None)
+    assert bench.pmc_traffic("fd_lvc_block_final", "C4", 32, 861, str(f)) == (None, None, None)
+    assert bench.pmc_traffic("fd_lvc_block_final", "C3", 8, 100, str(f)) == (None, None, None)
     # legacy (pre-r03) summaries are C3 8 x 861 unless named *c5*
     assert bench.traffic_workload({}, "profiles/r02_v4_traffic.json") == ("C3", 8, 861)
     assert bench.traffic_workload({}, "profiles/r02_v4c5_traffic.json") == ("C5", 8, 861)
@@ -224,4 +225,30 @@ def test_bench_traffic_keyed_by_workload(tmp_path):
     c4 = bench.pmc_traffic("fd_lvc_block_final", "C4", 32, 861)
     if c4[0] is not None:
         assert "c4" in c4[1] and c4[0] > 3 * c3[0]
-    assert bench.pmc_traffic("fd_lvc_block_final", "C4", 16, 861) == (None, None)
+    assert bench.pmc_traffic("fd_lvc_block_final", "C4", 16, 861) == (None, None, None)
+
+
+def test_bench_tables_cover_every_dominant_tag():
+    """bench.py refuses an untagged slowest kernel: the tags that lead C2 / C3 / C4 /
+    C5 profiles -- the WaveNet stack, the fp32 layer launches, the LVC blocks, the kernel
+    predictor, the NSF pair / upsample / noise convs -- all have FLOP and byte entries."""
+    import bench
+    fl = bench.flops_per_launch(8, 861, "bf16")
+    by = bench.bytes_per_launch(8, 861, "bf16")
+    sf, sb = bench.svs_tables(8, 861, 120, "bf16")
+    fl.update(sf)
+    by.update(sb)
+    for tag in ("wn_stack", "wn_gate", "wn_resskip", "fd_lvc_block_final", "fd_kp_kernel", "fd_kp_hidden",
+                "fd_lvc_block_ups", "fd_lvc_block_sub", "fd_dblock_fused", "nsf_pair", "nsf_res", "nsf_res_small",
+                "nsf_ups", "nsf_noise_conv", "nsf_source", "nsf_post"):
+        assert tag in fl and tag in by and by[tag] > 0, tag
+    # the stack's mean launch: 10 layers of 26.2 MFLOP per frame plus half the in/out projections
+    per_frame = fl["wn_stack"] / (8 * 861)
+    assert 10 * 2 * 2 * 256 * 1280 < per_frame < 10 * 2 * 2 * 256 * 1280 * 1.02
+    # 27 pair launches per C5 forward carry all ResBlock FLOPs of the C = 128 / 64 / 32 stages
+    F = 8 * 861
+    pair_total = sum(2 * 2 * 3 * 21 * F * r * c * c for r, c in bench.nsf_stage_dims() if c in bench.NSF_PAIR_C)
+    assert abs(fl["nsf_pair"] * 27 - pair_total) < 1e-6 * pair_total
+    with pytest.raises(SystemExit):
+        bench.dominant_kernel({"mystery": (1, 5.0), "wn_stack": (2, 1.0)}, fl, by)
+    assert bench.dominant_kernel({"nsf_pair": (27, 5.0), "wn_stack": (2, 1.0)}, fl, by) == "nsf_pair"

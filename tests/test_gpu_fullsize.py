@@ -160,8 +160,10 @@ def test_c3_full_bf16_vs_fp32(B):
     assert_bf16_close(wav16, wav32, f"C3 FastDiff bf16 vs fp32, B={B}x861")
 
 
-def test_c5_full_bf16_vs_fp32():
-    """C5 at full utterance length (2 SVS segments x 861 frames, 120 phonemes each): the bf16
+@pytest.mark.parametrize("B", [2, 8])
+def test_c5_full_bf16_vs_fp32(B):
+    """C5 at full utterance length (B = 2, and the bench's per-GPU batch of 8 SVS segments, x 861
+    frames, 120 phonemes each): the bf16
     pipeline (condition encoder, ProDiff 4-iter M=128, NSF-HiFiGAN on the windowed MFMA convs)
     against the exact fp32 pipeline with the same weights and the same on-device draws
     (Philox, keyed by seed and element index: identical in both dtypes).  The fp32 path is
@@ -171,7 +173,7 @@ def test_c5_full_bf16_vs_fp32():
     from tests.bf16_bar import assert_bf16_close
     dev = torch.device("cuda")
     utts = [{k: torch.from_numpy(v).to(dev) for k, v in synth.synth_svs_utterance(100 + i, 861, 120, SVS_VOCAB).items()}
-            for i in range(2)]
+            for i in range(B)]
     batch = SvsSynthesizer.collate(utts)
     outs = {}
     for dt in ("fp32", "bf16"):
@@ -180,5 +182,5 @@ def test_c5_full_bf16_vs_fp32():
         outs[dt] = (mel.cpu().numpy(), wav.cpu().numpy())
         del syn
     assert np.isfinite(outs["fp32"][1]).all() and np.abs(outs["fp32"][1]).max() <= 1.0
-    assert_bf16_close(outs["bf16"][0], outs["fp32"][0], "C5 mel bf16 vs fp32, 2x861")
-    assert_bf16_close(outs["bf16"][1], outs["fp32"][1], "C5 wav bf16 vs fp32, 2x861")
+    assert_bf16_close(outs["bf16"][0], outs["fp32"][0], f"C5 mel bf16 vs fp32, {B}x861")
+    assert_bf16_close(outs["bf16"][1], outs["fp32"][1], f"C5 wav bf16 vs fp32, {B}x861")

@@ -12,11 +12,11 @@ for spec in "$@"; do
   lib=${spec%%|*}; args=${spec#*|}
   [ "$lib" = "-" ] && lib=$R/prodiff_amd/libprodiff_hip.so
   if [ -n "$AB_TESTS" ]; then
-    PRODIFF_HIP_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_bf16.py -m gpu -x -q --timeout 120 \
+    PRODIFF_ALLOW_VARIANT=1 PRODIFF_HIP_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_bf16.py -m gpu -x -q --timeout 120 \
       --timeout-method thread -k "$AB_TESTS" > $O/tests_$i.log 2>&1
     echo "[$spec] $(tail -1 $O/tests_$i.log)"
   fi
-  PRODIFF_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --cpu-frames 0 $args > $O/bench_$i.json 2> $O/bench_$i.err
+  PRODIFF_ALLOW_VARIANT=1 PRODIFF_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --cpu-frames 0 $args > $O/bench_$i.json 2> $O/bench_$i.err
   python - "$spec" $O/bench_$i.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

@@ -12,9 +12,11 @@ lane) coalesced streaming read, so it is doubled; WRITE_SIZE is exact for 16-B s
 Every kernel here reads and writes 16 B per lane on its streaming paths.
 `traffic_bytes_per_launch` is the mean over all launches of the kernel in the profiled
 run (hop-64 and hop-256 launches of the LVC block alike), the same averaging bench.py
-uses for `achieved`.  bench.py reads the result as `roofline.traffic`.
+uses for `achieved`.  bench.py reads the result as `roofline.traffic`.  `lib_sha16` names the
+library the passes ran (run this where they ran): bench.py flags a summary of another build.
 """
 import csv
+import hashlib
 import json
 import os
 import sys
@@ -44,7 +46,13 @@ def main():
         t = tot[name]
         t[0] += (f + w) * len(fetch[key])
         t[1] += len(fetch[key])
-    res = {"bench_tag": tag, "config": config, "batch": batch, "frames": frames, "units": "bytes per launch (FETCH_SIZE KiB x1024 x2 + WRITE_SIZE KiB x1024)",
+    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "prodiff_amd", "libprodiff_hip.so")
+    lib = os.environ.get("PRODIFF_HIP_LIB", lib)
+    try:
+        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+    except OSError:
+        sha = None
+    res = {"bench_tag": tag, "lib_sha16": sha, "config": config, "batch": batch, "frames": frames, "units": "bytes per launch (FETCH_SIZE KiB x1024 x2 + WRITE_SIZE KiB x1024)",
            "per_grid": per_grid,
            "kernels": {k: {"traffic_bytes_per_launch": v[0] / v[1], "launches": v[1]} for k, v in tot.items()}}
     with open(out, "w") as f:

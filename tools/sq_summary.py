@@ -19,6 +19,7 @@ fractions read low by a few percent.
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 from collections import defaultdict
@@ -95,7 +96,13 @@ def main():
     rows = rows[:a.top]
     for r in rows:
         r.pop("_total_us")
-    out = dict(config=a.config, source=a.dir, definitions=__doc__.split("\n\n")[1].strip(), kernels=rows)
+    lib = os.environ.get("PRODIFF_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                          "prodiff_amd", "libprodiff_hip.so"))
+    try:
+        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+    except OSError:
+        sha = None
+    out = dict(config=a.config, lib_sha16=sha, source=a.dir, definitions=__doc__.split("\n\n")[1].strip(), kernels=rows)
     s = json.dumps(out, indent=1)
     if a.o:
         open(a.o, "w").write(s + "\n")
