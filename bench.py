@@ -495,10 +495,13 @@ def free_port():
     return p
 
 
-def stub_synth(cond, seed, utt_ids=None):
+def stub_synth(cond, seed, utt_ids=None, lens=None):
     """--dry-run stand-in for the Synthesizer (CPU, no compute worth timing)."""
     B, T, _ = cond.shape
     return cond[..., :80].clone(), torch.zeros(B, T * HOP)
+
+
+stub_synth.mel_bins = 80
 
 
 def main():
@@ -510,6 +513,9 @@ def main():
                     help="auto: C3 at N=1, C4 (32 utterances per GPU) at N>1")
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU (global for C4S)")
     ap.add_argument("--frames", type=int, default=None, help="mel frames per utterance")
+    ap.add_argument("--lengths", default="fixed", choices=["fixed", "ds"],
+                    help="ds: the reference song's 30 segment lengths (and phoneme counts) per GPU "
+                         "(tests/golden/ds_lengths.json, from samples/00_*.ds), run as ragged batches")
     ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline_port sample length (0 = skip)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
                     help="compute dtype (default: the config's; fp32 is the exact parity path)")
@@ -560,22 +566,34 @@ def main():
     from prodiff_amd.pipeline import distributed_synthesize, lpt_shards
 
     # utterance list (all ranks know every length; only the own shard is resident)
-    n_total = nb if cfg["strong"] else nb * world
-    lengths = [T] * n_total
+    from prodiff_amd.pipeline import ragged_batches
+    if args.lengths == "ds":   # the song's segments, once per GPU (weak scaling), ragged batches
+        ds = json.load(open(os.path.join(ROOT, "tests", "golden", "ds_lengths.json")))
+        per = len(ds["frames"])
+        n_total = per if cfg["strong"] else per * world
+        lengths = [ds["frames"][i % per] for i in range(n_total)]
+        tokens = [min(ds["phonemes"][i % per], lengths[i]) for i in range(n_total)]
+        nb = per
+    else:
+        n_total = nb if cfg["strong"] else nb * world
+        lengths = [T] * n_total
+        tokens = [cfg.get("tokens", 0)] * n_total
     shards = lpt_shards(lengths, world)
     mine = shards[rank]
     B = len(mine)                                           # utterances this rank runs per step
+    F_rank = sum(lengths[i] for i in mine)
+    n_batches = max(1, len(ragged_batches(lengths, mine)))
     rng = np.random.default_rng(1000 + rank)
-    conds = [(T, None)] * n_total
+    conds = [(L_, None) for L_ in lengths]
     from prodiff_amd import synth as _synth
     for i in mine:
         if svs:      # one SVS segment: phonemes + durations summing to T frames, f0, voicing, breath
             from prodiff_amd.pipeline import SVS_VOCAB
             u = {k: torch.from_numpy(v).to(dev) for k, v in
-                 _synth.synth_svs_utterance(100 + i, T, cfg["tokens"], SVS_VOCAB).items()}
-            conds[i] = (T, (lambda u=u: u))
+                 _synth.synth_svs_utterance(100 + i, lengths[i], tokens[i], SVS_VOCAB).items()}
+            conds[i] = (lengths[i], (lambda u=u: u))
         else:
-            conds[i] = torch.from_numpy(rng.standard_normal((T, 256), dtype=np.float32)).to(dev)
+            conds[i] = torch.from_numpy(rng.standard_normal((lengths[i], 256), dtype=np.float32)).to(dev)
 
     _lib = None
     if dry:
@@ -625,15 +643,21 @@ def main():
                 return graph.replay()
             return gd.sample(cond_b, seed=10_000 * i)
 
+    # per-launch tables: a launch covers one batch; with ragged batches (--lengths ds) the mean
+    # batch, F_rank / n_batches real frames (padding is not algorithmic work)
+    ds_mode = args.lengths == "ds"
+    wl_name = cfg_name + ("DS" if ds_mode else "")        # workload key of the PMC / SQ summaries
+    Bl = B / n_batches if ds_mode else B
+    Tl = F_rank / B if ds_mode else T
     if svs:
-        fl = flops_per_launch(B, T, dtype, M=128)
-        by = bytes_per_launch(B, T, dtype, M=128)
-        sf, sb = svs_tables(B, T, cfg["tokens"], dtype)
+        fl = flops_per_launch(Bl, Tl, dtype, M=128)
+        by = bytes_per_launch(Bl, Tl, dtype, M=128)
+        sf, sb = svs_tables(Bl, Tl, sum(tokens[i] for i in mine) / max(B, 1), dtype)
         fl.update(sf)
         by.update(sb)
     else:
-        fl = flops_per_launch(B, T, dtype)
-        by = bytes_per_launch(B, T, dtype)
+        fl = flops_per_launch(Bl, Tl, dtype)
+        by = bytes_per_launch(Bl, Tl, dtype)
     for i in range(args.warmup):
         step(i)
     if not dry:
@@ -720,7 +744,7 @@ def main():
         else:
             assert torch.isfinite(out).all()
 
-    frames = n_total * T * args.steps
+    frames = sum(lengths) * args.steps
     audio_s = frames * hop / sample_rate
     ms_step = dt / args.steps * 1e3
     peak_tf = BF16_PEAK_TFLOPS if dtype == "bf16" else FP32_PEAK_TFLOPS
@@ -743,7 +767,7 @@ def main():
             ach = fl[dom] * cnt / sec / 1e12
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
                         "frac": round(ach / peak_tf, 4)}
-        traffic, tsrc, tlib = pmc_traffic(dom, cfg_name, B, T, args.traffic)
+        traffic, tsrc, tlib = pmc_traffic(dom, wl_name, B, T, args.traffic)
         roofline.update({"bound_basis": "model estimate: algorithmic intensity vs the ridge; the measured limiter "
                                         "is in `utilisation` (MFMA / VALU busy, wait fractions)",
                          "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
@@ -755,11 +779,12 @@ def main():
                          "timing": ("HIP events around this kernel only, over untimed eager runs of the same "
                                     "sampler (the timed steps replay a hipGraph)") if graph_prof else
                                    "HIP events around this kernel only, over the timed steps"})
-        roofline["denoiser"] = denoiser_roofline(kern_all, nprof, B, T, cfg, dtype, peak_tf, cfg_name)
+        roofline["denoiser"] = denoiser_roofline(kern_all, nprof, 1, F_rank, cfg, dtype, peak_tf, wl_name)
     if svs:
-        step_fl = svs_step_flops(n_total, T, cfg["tokens"])
+        step_fl = svs_step_flops(n_total, sum(lengths) / n_total, sum(tokens) / n_total)
     else:
-        step_fl = 2 * prodiff_step_flops(n_total, T) + (4 * fastdiff_step_flops(n_total, T) if cfg["vocoder"] else 0)
+        Fa = sum(lengths)
+        step_fl = 2 * prodiff_step_flops(1, Fa) + (4 * fastdiff_step_flops(1, Fa) if cfg["vocoder"] else 0)
     out_line = {
         "metric": METRIC,
         "value": round(frames / dt, 1),
@@ -775,16 +800,22 @@ def main():
         "data": ("synthetic SVS segments (phonemes, durations summing to T, f0 with unvoiced gaps, voicing/breath, "
                  "speaker mix)" if svs else "synthetic (cond ~ N(0,1))") +
                 "; random-init weights of the reference architectures; on-device Philox draws",
-        "config": {"workload": cfg["desc"].format(b=nb, t=T, n=cfg.get("tokens")), "name": cfg_name,
+        "config": {"workload": cfg["desc"].format(b=nb, t=T if not ds_mode else f"{min(lengths)}..{max(lengths)}",
+                                                  n=cfg.get("tokens") if not ds_mode else "the .ds file's"),
+                   "name": cfg_name + (" --lengths ds" if ds_mode else ""),
                    "global_batch": n_total,
-                   "per_gpu_batch": B, "seq_len": T,
+                   "per_gpu_batch": B, "seq_len": T if not ds_mode else max(lengths),
+                   "lengths": None if not ds_mode else
+                   f"ragged: the reference song's {nb} segments per GPU ({min(lengths)}..{max(lengths)} frames, "
+                   f"{sum(lengths[i] for i in mine)} per GPU; samples/00_*.ds via tests/golden/ds_lengths.json), "
+                   f"{n_batches} padded batches per GPU (ragged_batches, <= 15% padding)",
                    "parallelism": f"dp{world} (utterance shards, RCCL gather to rank 0)" if cfg["vocoder"]
                    else "single GPU" + ("" if args.no_graph else ", hipGraph replay")},
         "rtf": round(dt / audio_s, 6),
         "x_realtime": round(audio_s / dt, 1),
         "model_tflops": round(step_fl * args.steps / dt / 1e12, 2),
         "roofline": roofline,
-        "utilisation": sq_utilisation(cfg_name) if not dry else None,
+        "utilisation": sq_utilisation(wl_name) if not dry else None,
         "kernels": kernels,
         "phases": phases,
         "kernels_source": (f"untimed {'eager ' if graph_prof else ''}pass of {nprof} steps, every launch bracketed by "

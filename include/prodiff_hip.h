@@ -127,6 +127,15 @@ int pd_wavenet_forward(const pd_wavenet* h, const float* spec, const float* step
                        const float* cond, float* out, int B, int T, void* workspace,
                        size_t ws_bytes, void* stream);
 
+/* Ragged batches (every sampler below, and nsf_forward): `lens` is a device array of B ints, the
+ * length of each row's utterance in mel frames (1 <= lens[b] <= T), or NULL (every row is T frames).
+ * Rows stay laid out at the padded length T; frames t >= lens[b] are padding, and every convolution
+ * of the network reads them as its zero padding -- so row b's first lens[b] frames (and samples)
+ * equal a run of that utterance alone (B = 1, T = lens[b]), the reference's one-segment-at-a-time
+ * inference (handler/infer/handler.py:373-388).  Outputs in the padding are unspecified.  With the
+ * on-device draws below, the draws of an utterance's frames are the same padded or alone.  A few
+ * A/B kernel variants do not take lens (PD_WN_OPT_LAYER 1, FD_OPT_LVC_TS 0, FD_OPT_KP_SIDE, FD_OPT_KP_CHUNK)
+ * and return PD_ERR_UNSUPPORTED. */
 /* Random draws (every sampler below).  When the caller passes no explicit draws they come
  * from an on-device Philox4x32-10 generator keyed by (seed, utterance id, element index
  * within the utterance, stream): `utt_ids` is a device array of B ints (one id per batch
@@ -144,8 +153,8 @@ int pd_wavenet_forward(const pd_wavenet* h, const float* spec, const float* step
  *   mel   [B,T,M] output (the reference's x[:,0].transpose(1,2), prodiff.py:151). */
 int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1,
                       const float* coef2, const float* sigma, int S, const float* x_T,
-                      const float* noise, unsigned long long seed, const int* utt_ids, float* mel,
-                      int B, int T, void* workspace, size_t ws_bytes, void* stream);
+                      const float* noise, unsigned long long seed, const int* utt_ids, const int* lens,
+                      float* mel, int B, int T, void* workspace, size_t ws_bytes, void* stream);
 
 /* ============================================================= rectified flow
  * RectifiedFlow / PitchRectifiedFlow inference (modules/diffusion/reflow.py:5-144) with
@@ -167,8 +176,8 @@ size_t pd_reflow_workspace_size(const pd_wavenet* h, int B, int T, int S, int al
  *   x_T  [B,T,M] time-major draw, or NULL -> Philox N(0,1) from `seed`
  *   x    [B,T,M] output: the reference's x.transpose(2,3).squeeze(1) before denorm_spec. */
 int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, float time_scale,
-                     const float* x_T, unsigned long long seed, const int* utt_ids, float* x, int B,
-                     int T, void* workspace, size_t ws_bytes, void* stream);
+                     const float* x_T, unsigned long long seed, const int* utt_ids, const int* lens, float* x,
+                     int B, int T, void* workspace, size_t ws_bytes, void* stream);
 
 /* denorm_spec (reflow.py:106-107): y = (x+1)/2 * (spec_max - spec_min) + spec_min with
  * spec_min/spec_max device arrays of length nspec (1, broadcast, or M);  x [rows,M].
@@ -255,8 +264,8 @@ int fd_forward(const fd_model* m, const float* audio, const float* cond, const f
  *   or NULL -> Philox;  wav [B,L] output. */
 int fd_sample(const fd_model* m, const float* mel, const float* beta, const float* alpha,
               const float* sigma, const float* steps, int N, const float* x_T,
-              const float* noise, unsigned long long seed, const int* utt_ids, float* wav, int B,
-              int Tc, void* workspace, size_t ws_bytes, void* stream);
+              const float* noise, unsigned long long seed, const int* utt_ids, const int* lens, float* wav,
+              int B, int Tc, void* workspace, size_t ws_bytes, void* stream);
 
 /* The same reverse process with the per-pass update given directly: pass j (j < N, sampling
  * order) evaluates eps at step value steps[j] and sets x = (x - ce[j] eps) / den[j] + sg[j] z.
@@ -266,8 +275,8 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
  * run's draws); the x_T draw is taken only when x_T is NULL. */
 int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce, const float* den,
                     const float* sg, const float* steps, int N, const float* x_T,
-                    const float* noise, unsigned long long seed, const int* utt_ids, int draw0,
-                    float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream);
+                    const float* noise, unsigned long long seed, const int* utt_ids, const int* lens,
+                    int draw0, float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream);
 
 /* The sampler's x_T ~ N(0,1) draw alone (util.py:208): exactly the [B,L] array fd_sample /
  * fd_sample_coefs draw when their x_T is NULL (same seed and utt_ids), written to x_T.  A
@@ -331,8 +340,8 @@ int nsf_set_option(nsf_model* m, int option, int value);
  *   noise [B, T*hop, harmonic_num+1] (randn_like, models.py:182), or NULL -> Philox from seed
  *   wav [B, T*hop] output in [-1, 1]. */
 int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const float* f0, const float* rand_ini,
-                const float* noise, unsigned long long seed, const int* utt_ids, float* wav, int B,
-                int T, void* workspace, size_t ws_bytes, void* stream);
+                const float* noise, unsigned long long seed, const int* utt_ids, const int* lens, float* wav,
+                int B, int T, void* workspace, size_t ws_bytes, void* stream);
 
 /* ============================================================ condition encoder
  * SVS teacher condition -- replaces ProDiffTeacher.forward_condition

@@ -76,11 +76,11 @@ _SIGS = {
     "pd_wavenet_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int]),
     "pd_wavenet_forward": (C.c_int, [_VP, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "pd_prodiff_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),
-                                    C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, _VP,
+                                    C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, _VP, _VP,
                                     C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "pd_reflow_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int, C.c_int, C.c_int]),
-    "pd_reflow_sample": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_float, _VP, C.c_ulonglong, _VP, _VP, C.c_int,
-                                   C.c_int, _VP, C.c_size_t, _VP]),
+    "pd_reflow_sample": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_float, _VP, C.c_ulonglong, _VP, _VP, _VP,
+                                   C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "pd_reflow_denorm": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
                                    _VP, _VP]),
     "fd_create": (C.c_int, [C.POINTER(fd_dims), C.POINTER(_VP), C.c_int, _VP, C.POINTER(_VP)]),
@@ -91,10 +91,10 @@ _SIGS = {
     "fd_fold_weight_norm": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, _VP]),
     "fd_forward": (C.c_int, [_VP, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "fd_sample": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
-                            C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, _VP, C.c_int,
+                            C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, _VP, _VP, C.c_int,
                             C.c_int, _VP, C.c_size_t, _VP]),
     "fd_sample_coefs": (C.c_int, [_VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
-                                  C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, C.c_int, _VP,
+                                  C.POINTER(C.c_float), C.c_int, _VP, _VP, C.c_ulonglong, _VP, _VP, C.c_int, _VP,
                                   C.c_int, C.c_int, _VP, C.c_size_t, _VP]),
     "fd_draw_x_T": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_ulonglong, _VP, _VP]),
     "pd_cond_num_params": (C.c_int, [C.POINTER(pd_cond_dims)]),
@@ -109,9 +109,8 @@ _SIGS = {
     "nsf_hop": (C.c_int, [_VP]),
     "nsf_workspace_size": (C.c_size_t, [_VP, C.c_int, C.c_int]),
     "nsf_set_option": (C.c_int, [_VP, C.c_int, C.c_int]),
-    "nsf_forward": (C.c_int, [_VP, _VP, C.c_float, _VP, _VP, _VP, C.c_ulonglong, _VP, _VP, C.c_int, C.c_int, _VP,
-                              C.c_size_t,
-                              _VP]),
+    "nsf_forward": (C.c_int, [_VP, _VP, C.c_float, _VP, _VP, _VP, C.c_ulonglong, _VP, _VP, _VP, C.c_int, C.c_int,
+                              _VP, C.c_size_t, _VP]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -167,6 +166,55 @@ def lptr(t):
 _UTT_CACHE = {}
 
 
+def _device_rows(vals, B, device, name, lo, hi):
+    """B host ints (checked in [lo, hi]) or a device tensor -> device int32 tensor (cached by value,
+    see utt_ids)."""
+    import torch
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    if torch.is_tensor(vals) and vals.is_cuda:
+        t = vals.reshape(-1)
+        if t.numel() != B:
+            raise HipError(f"{name} holds {t.numel()} values for a batch of {B}")
+        if t.device != dev:
+            t = t.to(dev)
+        return t if t.dtype == torch.int32 and t.is_contiguous() else t.to(torch.int32).contiguous()
+    t = torch.as_tensor(vals).reshape(-1)
+    if t.numel() != B:
+        raise HipError(f"{name} holds {t.numel()} values for a batch of {B}")
+    if t.numel() and (int(t.min()) < lo or int(t.max()) > hi):
+        raise HipError(f"{name} must lie in [{lo}, {hi}]")
+    key = (name, str(dev), tuple(int(v) for v in t.tolist()))
+    d = _UTT_CACHE.get(key)
+    if d is None:
+        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            raise HipError(f"{name}: host values not seen before cannot be copied to the device during a "
+                           "graph capture; pass a device int32 tensor (or call once before capturing)")
+        if len(_UTT_CACHE) >= 256:
+            _UTT_CACHE.pop(next(iter(_UTT_CACHE)))
+        d = t.to(device=dev, dtype=torch.int32).contiguous()
+        _UTT_CACHE[key] = d
+    elif dev.type == "cuda":
+        d.record_stream(torch.cuda.current_stream(dev))
+    return d
+
+
+def lens(vals, B, T, device):
+    """Ragged batch: each row's utterance length in frames (include/prodiff_hip.h), None (every
+    row T frames), B host ints in [1, T], or a device tensor (not range-checked: the kernels clamp
+    to T) -> device int32 tensor or None.  All equal to T -> None (the dense path)."""
+    if vals is None:
+        return None
+    import torch
+    if not (torch.is_tensor(vals) and vals.is_cuda):
+        v = [int(x) for x in (vals.tolist() if torch.is_tensor(vals) else vals)]
+        if len(v) == B and all(x == T for x in v):
+            return None
+        vals = v
+    return _device_rows(vals, B, device, "lens", 1, T)
+
+
 def utt_ids(ids, B, device):
     """Per-row utterance ids for the samplers' Philox draws (include/prodiff_hip.h): None
     (ids 0..B-1) or B ints -> (device int32 tensor or None).  Keep the tensor alive until
@@ -184,35 +232,7 @@ def utt_ids(ids, B, device):
     captured): pass a device tensor or warm the cache before the capture."""
     if ids is None:
         return None
-    import torch
-    dev = torch.device(device)
-    if dev.type == "cuda" and dev.index is None:
-        dev = torch.device("cuda", torch.cuda.current_device())
-    if torch.is_tensor(ids) and ids.is_cuda:
-        t = ids.reshape(-1)
-        if t.numel() != B:
-            raise HipError(f"utt_ids holds {t.numel()} ids for a batch of {B}")
-        if t.device != dev:
-            t = t.to(dev)
-        return t if t.dtype == torch.int32 and t.is_contiguous() else t.to(torch.int32).contiguous()
-    t = torch.as_tensor(ids).reshape(-1)
-    if t.numel() != B:
-        raise HipError(f"utt_ids holds {t.numel()} ids for a batch of {B}")
-    if t.numel() and (int(t.min()) < 0 or int(t.max()) >= 2 ** 31):
-        raise HipError("utt_ids must lie in [0, 2**31)")
-    key = (str(dev), tuple(int(v) for v in t.tolist()))
-    d = _UTT_CACHE.get(key)
-    if d is None:
-        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
-            raise HipError("utt_ids: host ids not seen before cannot be copied to the device during a "
-                           "graph capture; pass a device int32 tensor (or call once before capturing)")
-        if len(_UTT_CACHE) >= 256:
-            _UTT_CACHE.pop(next(iter(_UTT_CACHE)))
-        d = t.to(device=dev, dtype=torch.int32).contiguous()
-        _UTT_CACHE[key] = d
-    elif dev.type == "cuda":
-        d.record_stream(torch.cuda.current_stream(dev))
-    return d
+    return _device_rows(ids, B, device, "utt_ids", 0, 2 ** 31 - 1)
 
 
 def iptr(t):

@@ -106,12 +106,14 @@ namespace {
 __global__ __launch_bounds__(256) void first_conv_kernel(const float* __restrict__ x,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ bias,
-                                                         float* __restrict__ out, int L) {
+                                                         float* __restrict__ out, int L,
+                                                         const int* __restrict__ lens, int hop) {
   __shared__ float xs[32 + 6];
   const int b = blockIdx.y, t0 = blockIdx.x * 32, tid = threadIdx.x;
+  const int Lv = lens ? min(lens[b] * hop, L) : L;   // ragged batch: the utterance's own end
   if (tid < 38) {
     int t = t0 - 3 + tid;
-    xs[tid] = (t >= 0 && t < L) ? x[(long long)b * L + t] : 0.f;
+    xs[tid] = (t >= 0 && t < Lv) ? x[(long long)b * L + t] : 0.f;
   }
   __syncthreads();
   const int s = tid >> 3, q = (tid & 7) * 4, t = t0 + s;
@@ -134,11 +136,12 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
                                                        const float* __restrict__ Wt,
                                                        const float* __restrict__ bias,
                                                        float* __restrict__ out, int Tin, int r,
-                                                       int p) {
+                                                       int p, const int* __restrict__ lens, int rate_in) {
   __shared__ __attribute__((aligned(16))) float w0[CI * CI], w1[CI * CI];
   __shared__ float xw[34][CI];
   const int b = blockIdx.z, phi = blockIdx.y, m0 = blockIdx.x * 32, tid = threadIdx.x;
   const int k0 = (phi + p) % r, d = (phi + p) / r;
+  const int Tv = lens ? min(lens[b] * rate_in, Tin) : Tin;   // input rows past the utterance read zero
   for (int i = tid; i < CI * CI; i += 256) {
     w0[i] = Wt[k0 * CI * CI + i];
     w1[i] = Wt[(k0 + r) * CI * CI + i];
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
   for (int i = tid; i < 34 * CI; i += 256) {
     int jj = i / CI, c = i - jj * CI;
     int j = m0 + d - 1 + jj;
-    float v = (j >= 0 && j < Tin) ? x[((long long)b * Tin + j) * CI + c] : 0.f;
+    float v = (j >= 0 && j < Tv) ? x[((long long)b * Tin + j) * CI + c] : 0.f;
     xw[jj][c] = v >= 0.f ? v : 0.2f * v;
   }
   __syncthreads();
@@ -176,12 +179,13 @@ __global__ __launch_bounds__(256) void lvc_kernel(float* __restrict__ x, const f
                                                   const float* __restrict__ y,
                                                   const KT* __restrict__ Kf, int kf_ld,
                                                   const float* __restrict__ Bf, int bf_ld, int Tc,
-                                                  int hop) {
+                                                  int hop, const int* __restrict__ lens) {
   __shared__ float ks[64 * 97];
   __shared__ float bs[64];
   __shared__ float ys[34 * 33];
   const int g = blockIdx.x, b = g / Tc, l = g - b * Tc, tid = threadIdx.x;
   const long long L = (long long)Tc * hop;
+  const long long Lv = lens ? (long long)min(lens[b], Tc) * hop : L;   // ragged batch: the utterance's end
   const KT* kf = Kf + (long long)g * kf_ld;
   for (int i = tid; i < 64 * 96; i += 256) {
     int oo, q2;
@@ -196,7 +200,7 @@ __global__ __launch_bounds__(256) void lvc_kernel(float* __restrict__ x, const f
     for (int i = tid; i < (chunk + 2) * 32; i += 256) {
       int rr = i >> 5, ci = i & 31;
       long long t = (long long)l * hop + s0 - 1 + rr;
-      ys[rr * 33 + ci] = (t >= 0 && t < L) ? y[((long long)b * L + t) * CI + ci] : 0.f;
+      ys[rr * 33 + ci] = (t >= 0 && t < Lv) ? y[((long long)b * L + t) * CI + ci] : 0.f;
     }
     __syncthreads();
     for (int s = sg; s < chunk; s += 8) {
@@ -365,6 +369,7 @@ struct LvcBlockArgs {
   unsigned stream;
   const int* uid;           // FIN: utterance id per batch row (null -> row index)
   int Tc, hop;
+  const int* lens;          // frames of each row's utterance (null: Tc), already offset by b_off
   int b_off;                // utterance index of blockIdx.y = 0 in the whole batch (Philox draws)
   int prio;                 // FD_OPT_LVC_PRIO: s_setprio(1) for the second half of the waves
 #ifdef LB_TRACE
@@ -494,6 +499,9 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
 #define TILE(j) (TPW == 1 ? wave : PF ? 2 * wave + (j) : wave + ((j) ^ jsw) * NW)
   const int Tc = P.Tc, hop = P.hop;
   const int Lh = Tc * hop;                           // utterance-local times fit in 32 bits
+  // ragged batch: the utterance ends at Le <= Lh (a multiple of hop, so of 32 when hop % 32 == 0):
+  // everything that reads past it -- audio, x_prev, x rows, u, y, the final conv -- reads zero
+  const int Le = P.lens ? min(P.lens[b], Tc) * hop : Lh;
   const int t0 = bx * TS, tg = t0 - 64;              // time of grid row 0
   const long long base = (long long)b * Lh;
   constexpr int RLO = 64 - 44 - EX, RHI = 64 + TS + 44 + EX;   // x rows the valid region reads
@@ -553,7 +561,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
     }
   }
   // UPS: x_prev rows and this wave's first chunk of phase-GEMM weight fragments
-  const int r = UPS ? P.r : 1, pp = UPS ? P.p : 0, Tin = Lh / r;
+  const int r = UPS ? P.r : 1, pp = UPS ? P.p : 0, Tin = Lh / r, Tin_e = Le / r;
   const int ntj = (GR / r + 2 + 31) / 32;
   const int jb = floordiv(tg + pp, r) - 2;           // column j0 = jb + 1 + c, c < 32 ntj
   constexpr int IX = UPS ? ((G::NTJ_MAX * 32 + 1) * 8 + G::NT - 1) / G::NT : 1;
@@ -620,7 +628,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
     for (int it = 0; it < IT; ++it) {
       const int i = tid + it * G::NT;
       const int t = tg - 3 + i;
-      if (i < GR + 6) AS[i] = (t >= 0 && t < Lh) ? av[it] : 0.f;
+      if (i < GR + 6) AS[i] = (t >= 0 && t < Le) ? av[it] : 0.f;
     }
     if (tid < 224) FW[tid] = fwv;
     if (tid < 32) FBL[tid] = fbv;
@@ -663,7 +671,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
       const int i = tid + it * G::NT, rr = i >> 3, q = (i & 7) * 4, j = jb + rr;
       if (i < (ntj * 32 + 1) * 8) {
         // rows outside x_prev are zero (lrelu(0) = 0)
-        const float m = (j >= 0 && j < Tin) ? 1.f : 0.f;
+        const float m = (j >= 0 && j < Tin_e) ? 1.f : 0.f;
         const f32x2 u0 = lrelu2(f32x2{xv4[it].x, xv4[it].y} * m), u1 = lrelu2(f32x2{xv4[it].z, xv4[it].w} * m);
         *reinterpret_cast<bf16x4*>(&XP[rr * LB_LD + q]) = bf16x4{(__bf16)u0.x, (__bf16)u0.y, (__bf16)u1.x, (__bf16)u1.y};
       }
@@ -717,7 +725,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     const int k = TILE(j), row = k * 32 + n, t = tg + row;
-    const bool ok = row >= RLO && row < RHI && t >= 0 && t < Lh;
+    const bool ok = row >= RLO && row < RHI && t >= 0 && t < Le;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
@@ -781,7 +789,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
         }
         if constexpr (PF) {   // a tile outside the utterance is the convs' zero padding (the PF gate
           const int ts = tg + k * 32;   // updates every tile, so its x is not zero there)
-          if (ts < 0 || ts >= Lh) { u0 = bf16x8{}; u1 = bf16x8{}; }
+          if (ts < 0 || ts >= Le) { u0 = bf16x8{}; u1 = bf16x8{}; }
         }
         __bf16* dst = &U[(k * 32 + n + UOFF) * LB_LD + 16 * h];
         *reinterpret_cast<bf16x8*>(dst) = u0;
@@ -825,9 +833,9 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
 #pragma unroll
         for (int p = 0; p < 8; ++p) v[p] = lrelu2(f32x2{acc[2 * p], acc[2 * p + 1]} + bias[p]);
         const int tt = tg + kp * 32 - 1;                  // the tile's first time (wave-uniform)
-        if (tt < 0 || tt + 31 >= Lh) {                    // utterance-edge tile: zero-pad
+        if (tt < 0 || tt + 31 >= Le) {                    // utterance-edge tile: zero-pad
           const int t = tt + n;
-          const bool in = t >= 0 && t < Lh;           // select, not multiply: stale LDS may be NaN
+          const bool in = t >= 0 && t < Le;           // select, not multiply: stale LDS may be NaN
 #pragma unroll
           for (int p = 0; p < 8; ++p) v[p] = in ? v[p] : f32x2{0.f, 0.f};
         }
@@ -912,7 +920,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       const int k = TILE(j), ts = tg + k * 32;
-      if (k >= kf && k <= kl && ts >= 0 && ts < Lh) {
+      if (k >= kf && k <= kl && ts >= 0 && ts < Le) {
         f32x16 g, f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) { g[r] = 0.f; f[r] = 0.f; }
@@ -972,7 +980,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
         }
         // hop < 32: a tile can straddle the utterance end; rows past it stay zero
         // (they are the next layer's conv padding)
-        gate_update(j, g, f, bq, !SUB || ts + n < Lh);
+        gate_update(j, g, f, bq, !SUB || ts + n < Le);
       }
     }
     }
@@ -1007,7 +1015,7 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
         for (int tap = 0; tap < 7; ++tap) st[tap] += __shfl_xor(st[tap], 32);
         if constexpr (PF) {   // x is zero outside the utterance (the final conv's padding)
           const int ts = tg + k * 32;
-          if (ts < 0 || ts >= Lh) {
+          if (ts < 0 || ts >= Le) {
 #pragma unroll
             for (int tap = 0; tap < 7; ++tap) st[tap] = 0.f;
           }
@@ -1078,7 +1086,8 @@ __global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(AF > 4 ? 
                                                           const __bf16* __restrict__ W1, const float* __restrict__ b1,
                                                           const __bf16* __restrict__ W2, const float* __restrict__ b2,
                                                           int Lout, int f, const float* __restrict__ audio,
-                                                          const float* __restrict__ fw, const float* __restrict__ fb) {
+                                                          const float* __restrict__ fw, const float* __restrict__ fb,
+                                                          const int* __restrict__ lens, int rate) {
   // U0 = lrelu(x[f i]) is dead after the first conv, so h2 reuses its rows: 3 x 13 KB of
   // bf16 images
   __shared__ __attribute__((aligned(16))) __bf16 U0[DB_ROWS * DB_LD];   // lrelu(x[f i]), then h2
@@ -1100,6 +1109,10 @@ __global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(AF > 4 ? 
   const int b = blockIdx.y, i0 = blockIdx.x * DB_TS, ib = i0 - 7;
   const long long Lin = (long long)Lout * f;
   const float* src = in + (long long)b * Lin * CI;
+  // ragged batch: the utterance's output rows end at Lv (rate output rows per mel frame), its input
+  // samples at Lv f; both convs' zero padding starts there
+  const int Lv = lens ? min(lens[b] * rate, Lout) : Lout;
+  const long long Linv = (long long)Lv * f;
   // the first stage's weight fragments first: their L2 round trip overlaps the staging's;
   // the later stages' are issued after the staging stores (r04: all 20 fragments live across
   // the staging kept the kernel at 148 VGPRs, 3 waves per SIMD)
@@ -1128,7 +1141,7 @@ __global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(AF > 4 ? 
     for (int it = 0; it < DB_AUI; ++it) {
       const int i = tid + DB_NT * it;
       const long long t = t0 + i;
-      AU[min(i, DB_AUM - 1)] = (i < na && t >= 0 && t < Lin) ? av[it] : 0.f;
+      AU[min(i, DB_AUM - 1)] = (i < na && t >= 0 && t < Linv) ? av[it] : 0.f;
     }
     __syncthreads();
   }
@@ -1152,7 +1165,7 @@ __global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(AF > 4 ? 
   for (int u = 0; u < DB_NI; ++u) {
     const int i = tid + DB_NT * u;
     const int p = i >> 3, q = (i & 7) * 4, ii = ib + p;
-    const bool ok = i < DB_ROWS * 8 && p < DB_TS + 14 && ii >= 0 && ii < Lout;
+    const bool ok = i < DB_ROWS * 8 && p < DB_TS + 14 && ii >= 0 && ii < Lv;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (AUD) {
       if (ok) {
@@ -1204,14 +1217,14 @@ __global__ __launch_bounds__(DB_NT) __attribute__((amdgpu_waves_per_eu(AF > 4 ? 
       }
       // rows outside [0, Lout) (and past DB_ROWS) are zeroed: tile-uniform test first
       const int pt = first + mt * 32, it0 = ib + pt;
-      const bool edge = it0 < 0 || it0 + 31 >= Lout || pt + 31 >= DB_ROWS;
+      const bool edge = it0 < 0 || it0 + 31 >= Lv || pt + 31 >= DB_ROWS;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int p = pt + (reg & 3) + 8 * (reg >> 2) + 4 * h, ii = ib + p;
         float v = acc[reg] + bv;
         v = v >= 0.f ? v : 0.2f * v;                        // the next conv's input activation
         if (edge) {
-          if (ii < 0 || ii >= Lout || p >= DB_ROWS) v = 0.f;
+          if (ii < 0 || ii >= Lv || p >= DB_ROWS) v = 0.f;
           if (p < DB_ROWS) Out[p * DB_LD + r32] = (__bf16)v;
         } else {
           Out[p * DB_LD + r32] = (__bf16)v;
@@ -1272,6 +1285,7 @@ struct KPArgs {
   __bf16* hout;             // [z][B][Tc][64]  h = h0 + R(h0), bf16 (the kernel GEMM's operand)
   float* Bf;                // [z][B][Tc][256] LVC biases
   int Tc;
+  const int* lens;          // frames of each utterance (null: Tc): every conv's zero padding starts there
 };
 
 // Fused KernelPredictor hidden stack (modules.py:320-333 + bias_conv :338-342):
@@ -1286,6 +1300,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   __shared__ __attribute__((aligned(16))) __bf16 Hb[3][98 * LDH];   // H0, R0, R1 (+1 zero row each side)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, f0 = blockIdx.x * 64, Tc = A.Tc;
+  const int Tv = A.lens ? min(A.lens[b], Tc) : Tc;   // ragged batch: the utterance's own end
   const int z = blockIdx.z, step = z / A.nb, nblk = z - step * A.nb;
   const long long rb = (long long)b * Tc;
   const float* nzrow = A.nz + (long long)step * A.nz_step + (long long)b * A.nz_ld + nblk * CC;
@@ -1332,7 +1347,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
     if (i < 100 * 24) {
       const int p = i / 24, g = (i - p * 24) * 4, f = f0 - 18 + p;
       bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-      if (g < CC && f >= 0 && f < Tc) {
+      if (g < CC && f >= 0 && f < Tv) {
         const float4 c = cv[u], n = nv[u];
         v = bf16x4{(__bf16)(c.x + n.x), (__bf16)(c.y + n.y), (__bf16)(c.z + n.z), (__bf16)(c.w + n.w)};
       }
@@ -1374,7 +1389,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
       const int p = mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, f = f0 - 16 + p;
       float v = acc[reg] + bias;
       v = v >= 0.f ? v : 0.1f * v;
-      if (f < 0 || f >= Tc) v = 0.f;
+      if (f < 0 || f >= Tv) v = 0.f;
       keep[q][reg] = v;
       Hb[0][(p + 1) * LDH + n] = (__bf16)v;
     }
@@ -1417,7 +1432,7 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
         float v = acc[reg] + bias;
         v = v >= 0.f ? v : 0.1f * v;
         if (j == 5) v += keep[q][reg];           // h = h0 + R(h0)
-        if (f < 0 || f >= Tc) v = 0.f;
+        if (f < 0 || f >= Tv) v = 0.f;
         Out[(p + 1) * LDH + n] = (__bf16)v;
         if (j == 5 && p >= 16 && p < 80 && f < Tc) hout[(rb + f) * HK + n] = (__bf16)v;
       }
@@ -1492,7 +1507,7 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
                                                                        const __bf16* __restrict__ W,
                                                                        const float* __restrict__ bias,
                                                                        __bf16* __restrict__ Kf, int Tc, int rows,
-                                                                       int nfg) {
+                                                                       int nfg, const int* __restrict__ lens) {
   __shared__ __attribute__((aligned(16))) __bf16 Hs[2][KP_F * KP_LDH];
   __shared__ __attribute__((aligned(16))) __bf16 Ot[8][32 * KP_LDO];
   __shared__ __attribute__((aligned(16))) float Bq[8][64];   // wave-private: its rows' biases
@@ -1529,8 +1544,9 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
       }
       const int ff = f + tap - 1;
       const int ffc = ff < 0 ? 0 : ff >= Tc ? Tc - 1 : ff;     // clamped: unconditional load
+      const int Tv = lens ? lens[b] : Tc;                        // ragged batch: the utterance's own end
       hv[i] = *reinterpret_cast<const uint4*>(hin + ((long long)b * Tc + ffc) * HK + ch);
-      hz |= (R >= rows || ff < 0 || ff >= Tc) ? 1u << i : 0u;
+      hz |= (R >= rows || ff < 0 || ff >= Tc || ff >= Tv) ? 1u << i : 0u;
     }
   };
   auto h_store = [&](int buf) {
@@ -1652,7 +1668,7 @@ __global__ void kp_prescale_kernel(const float* __restrict__ w, const float* __r
 }
 
 int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B, int Tc, hipStream_t st,
-                   bool prescale = false) {
+                   bool prescale = false, const int* lens = nullptr) {
   const int rows = B * Tc;
   const int nfg = cdiv(rows, KP_F);
   // buffer-store offsets are 32-bit bytes, up to the last (partial) item's rows
@@ -1661,7 +1677,7 @@ int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B
   const int grid = items < 256 ? items : 256;   // persistent: one block per CU
   ProfScope ps("fd_kp_kernel", st);
   hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(grid), dim3(KP_THREADS), 0, st, hk,
-                     prescale ? K.kks_w : lookup_bf16(K.kk_w), prescale ? K.kks_b : K.kk_b, Kb, Tc, rows, nfg);
+                     prescale ? K.kks_w : lookup_bf16(K.kk_w), prescale ? K.kks_b : K.kk_b, Kb, Tc, rows, nfg, lens);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -1674,18 +1690,19 @@ __global__ __launch_bounds__(256) void final_conv_kernel(const float* __restrict
                                                          float* eps_out, float* xa, float ce, float den,
                                                          float sig, const float* noise,
                                                          unsigned long long seed, unsigned stream,
-                                                         const int* uid, long long L) {
+                                                         const int* uid, long long L, const int* lens, int hop) {
   // rows of 36 floats (144 B): 16-B reads, slot 9*row mod 16 -> conflict-free across lanes
   __shared__ __attribute__((aligned(16))) float xs[262 * 36];
   __shared__ __attribute__((aligned(16))) float wsh[7 * 32];
   const int b = blockIdx.y, tid = threadIdx.x;
   const long long t0 = (long long)blockIdx.x * 256;
+  const long long Lv = lens ? (long long)lens[b] * hop : L;   // ragged batch: x reads zero past the utterance
   if (tid < 224) wsh[tid] = w[tid];
   for (int i = tid; i < 262 * 8; i += 256) {
     const int rr = i >> 3, q = (i & 7) * 4;
     const long long t = t0 - 3 + rr;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (t >= 0 && t < L) v = *reinterpret_cast<const float4*>(x + ((long long)b * L + t) * CI + q);
+    if (t >= 0 && t < L && t < Lv) v = *reinterpret_cast<const float4*>(x + ((long long)b * L + t) * CI + q);
     *reinterpret_cast<float4*>(&xs[rr * 36 + q]) = v;
   }
   __syncthreads();
@@ -1821,22 +1838,25 @@ int fd_step_mlp(const fd_model* m, float* ws, const FdWs& W, int nv, hipStream_t
 }
 
 // DiffusionDBlock (modules.py:131-138): out = conv_d4(lr(conv_d2(lr(conv_d1(lr(x[f i])))))) + Wr x[f i]
+// lens / rate: ragged batch (utterance b's output rows end at lens[b] * rate), or null
 int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, float* t1, int B, int Tout,
-           int f, hipStream_t st, const fd_model* m = nullptr, const float* audio = nullptr) {
+           int f, hipStream_t st, const fd_model* m = nullptr, const float* audio = nullptr,
+           const int* lens = nullptr, int rate = 1) {
   const long long bsi = (long long)Tout * f * CI, bso = (long long)Tout * CI;
   if (const __bf16* w0 = lookup_bf16(D.c0_w)) {   // bf16: one fused launch, intermediates in LDS
     ProfScope ps("fd_dblock_fused", st);
     if (audio && f <= 4)
       hipLaunchKernelGGL(dblock_bf16_kernel<4>, dim3(cdiv(Tout, DB_TS), B), dim3(DB_NT), 0, st, in, out, w0, D.c0_b,
                          lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, audio, m->first_w,
-                         m->first_b);
+                         m->first_b, lens, rate);
     else if (audio)
       hipLaunchKernelGGL(dblock_bf16_kernel<16>, dim3(cdiv(Tout, DB_TS), B), dim3(DB_NT), 0, st, in, out, w0, D.c0_b,
                          lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, audio, m->first_w,
-                         m->first_b);
+                         m->first_b, lens, rate);
     else
       hipLaunchKernelGGL(dblock_bf16_kernel<0>, dim3(cdiv(Tout, DB_TS), B), dim3(DB_NT), 0, st, in, out, w0, D.c0_b,
-                         lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, nullptr, nullptr, nullptr);
+                         lookup_bf16(D.c1_w), D.c1_b, lookup_bf16(D.c2_w), D.c2_b, Tout, f, nullptr, nullptr, nullptr,
+                         lens, rate);
     PD_LAUNCH_CHECK();
     return PD_OK;
   }
@@ -1847,6 +1867,7 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
       s.act = ACT_LRELU; s.alpha = 0.2f;
       add_seg(a, s);
     }
+    a.lens = lens; a.lens_mul = rate;
     PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_DBLOCK>(a, st, "fd_dblock")));
   }
   {
@@ -1856,6 +1877,7 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
       s.act = ACT_LRELU; s.alpha = 0.2f;
       add_seg(a, s);
     }
+    a.lens = lens; a.lens_mul = rate;
     PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_DBLOCK>(a, st, "fd_dblock")));
   }
   {
@@ -1866,6 +1888,7 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
       add_seg(a, s);
     }
     add_seg(a, make_seg(in, bsi, CI, CI, 0, f));   // residual_dense on x[f i]
+    a.lens = lens; a.lens_mul = rate;
     PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_DBLOCK>(a, st, "fd_dblock")));
   }
   return PD_OK;
@@ -1874,7 +1897,7 @@ int dblock(const fd_model::Down& D, const float* in, float* out, float* t0, floa
 // Kernel-predictor hidden stacks (bf16) for `nsteps` steps x every block in one launch.
 // nz: [nsteps*B][nb*80] (the step-MLP output); results in ws.hall / ws.bfall, z = s*nb + n.
 int fd_kp_hidden_all(const fd_model* m, float* ws, const FdWs& W, const float* condT, const float* nz,
-                     int nsteps, int B, int Tc, hipStream_t st) {
+                     int nsteps, int B, int Tc, hipStream_t st, const int* lens = nullptr) {
   const int nb = m->nblocks;
   KPArgs ka{};
   ka.condT = condT; ka.nz = nz; ka.nz_step = B * nb * CC; ka.nz_ld = nb * CC; ka.nb = nb; ka.B = B;
@@ -1884,7 +1907,7 @@ int fd_kp_hidden_all(const fd_model* m, float* ws, const FdWs& W, const float* c
     for (int j = 0; j < 6; ++j) { ka.Wr[n][j] = lookup_bf16(K.kres_w[j]); ka.br[n][j] = K.kres_b[j]; }
     ka.Wb[n] = lookup_bf16(K.kb_w); ka.bb[n] = K.kb_b;
   }
-  ka.hout = reinterpret_cast<__bf16*>(ws + W.hall); ka.Bf = ws + W.bfall; ka.Tc = Tc;
+  ka.hout = reinterpret_cast<__bf16*>(ws + W.hall); ka.Bf = ws + W.bfall; ka.Tc = Tc; ka.lens = lens;
   ProfScope ps("fd_kp_hidden", st);
   hipLaunchKernelGGL(kp_hidden_bf16_kernel, dim3(cdiv(Tc, 64), B, nsteps * nb), dim3(256), 0, st, ka);
   PD_LAUNCH_CHECK();
@@ -1953,10 +1976,16 @@ int launch_lvc_block_ts(const LvcBlockArgs& la, bool ups, bool aud, bool fin, bo
 // nz: this step's per-block fc_t(emb) rows ([B][nblocks*80]).  Leaves the LVC output in
 // *xout, or -- when `fin` is given and the last block is the fused LVC kernel -- applies
 // the sampler update itself and sets *xout = nullptr.
+// lens (device, B ints, or null): ragged batch -- utterance b is lens[b] mel frames of the padded Tc;
+// every conv of the network reads zero past it ("Ragged batches").
 int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const float* condT,
            const float* nz, int step, int B, int Tc, float** xout, hipStream_t st,
-           const FdFinal* fin = nullptr, bool side = false) {
+           const FdFinal* fin = nullptr, bool side = false, const int* lens = nullptr) {
   const int nb = m->nblocks;
+  if (lens && m->pool_bf && m->lvc_ts == 0) {
+    set_error("FD_OPT_LVC_TS 0 (per-layer LVC launches) does not take ragged batches (lens)");
+    return PD_ERR_UNSUPPORTED;
+  }
   const long long L = (long long)Tc * m->hops[nb - 1];
   const bool bf = m->pool_bf != nullptr;
   // whole-block LVC kernel with its prologue/epilogue fusions (bf16)
@@ -1968,7 +1997,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
   if (!aud) {
     ProfScope ps("fd_first_conv", st);
     hipLaunchKernelGGL(first_conv_kernel, dim3(cdiv(L, 32), B), dim3(256), 0, st, xa, m->first_w,
-                       m->first_b, a0, (int)L);
+                       m->first_b, a0, (int)L, lens, m->hops[nb - 1]);
     PD_LAUNCH_CHECK();
   }
   // downsample chain: a0 -> d[0] -> ... -> d[nb-1]   (FastDiff_model.py:89-93)
@@ -1980,7 +2009,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
     const int f = m->ratios[nb - 1 - n];
     Lc /= f;
     PD_TRY(dblock(m->dn[n], cur, ws + W.d[n], ws + W.dtmp0, ws + W.dtmp1, B, (int)Lc, f, st, m,
-                  n == 0 && aud ? xa : nullptr));
+                  n == 0 && aud ? xa : nullptr, lens, (int)(Lc / Tc)));
     cur = ws + W.d[n];
   }
   // LVC blocks (FastDiff_model.py:95-97)
@@ -2013,6 +2042,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         add_seg(a, s);
       }
       a.act = ACT_LRELU; a.alpha = 0.1f;
+      a.lens = lens; a.lens_mul = 1;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_IN>(a, st, "fd_kp_in")));
     }
     const float* src = ws + W.h0;
@@ -2023,6 +2053,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(src, bsH, HK, HK, tap - 1));
       a.act = ACT_LRELU; a.alpha = 0.1f;
       if (j == 5) { a.res = ws + W.h0; a.res_bs = bsH; a.res_ld = HK; }   // h + R(h)
+      a.lens = lens; a.lens_mul = 1;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_RES>(a, st, "fd_kp_res")));
       src = dst;
     }
@@ -2031,6 +2062,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       GemmArgs a = make_gemm(B, Tc, 2 * CI * NLY, K.kb_w, 3 * HK, K.kb_b, ws + W.Bf,
                              (long long)Tc * 2 * CI * NLY, 2 * CI * NLY);
       for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
+      a.lens = lens; a.lens_mul = 1;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_BIAS>(a, st, "fd_kp_bias")));
     }
     }
@@ -2041,7 +2073,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       if (!ups) {   // separate upsample (modules.py:205-206)
         ProfScope ps("fd_upsample", st);
         hipLaunchKernelGGL(upsample_kernel, dim3(cdiv(Tin, 32), r, B), dim3(256), 0, st, x, K.up_w, K.up_b,
-                           xn, (int)Tin, r, r / 2 + r % 2);
+                           xn, (int)Tin, r, r / 2 + r % 2, lens, (int)(Tin / Tc));
         PD_LAUNCH_CHECK();
       }
       __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf);
@@ -2056,7 +2088,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         Kc += (size_t)n * rows * NLY * KPERLAYER;
         PD_HIP(hipStreamWaitEvent(st, m->ev_kp[n], 0));
       } else {
-        PD_TRY(kp_kernels_all(K, hkb + (size_t)b0 * Tc * HK, Kc, nbk, Tc, st, true));
+        PD_TRY(kp_kernels_all(K, hkb + (size_t)b0 * Tc * HK, Kc, nbk, Tc, st, true, lens ? lens + b0 : nullptr));
       }
       LvcBlockArgs la{};
       for (int i = 0; i < NLY; ++i) {
@@ -2070,6 +2102,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       la.xout = (ups ? xn : ws + W.y) + (size_t)b0 * Tout * CI;
       la.a = (last && aud) ? nullptr : ad + (size_t)b0 * Tout * CI;
       la.Bf = Bfp + (size_t)b0 * Tc * 2 * CI * NLY; la.Tc = Tc; la.hop = hop; la.b_off = b0;
+      la.lens = lens ? lens + b0 : nullptr;
       la.prio = m->lvc_prio;
       la.Wup = lookup_bf16(K.upf_w); la.bup = K.up_b; la.r = r; la.p = r / 2 + r % 2;
       la.audio = xa + (size_t)b0 * L; la.fw = m->first_w; la.fb = m->first_b;
@@ -2103,11 +2136,11 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       const int p = r / 2 + r % 2;
       ProfScope ps("fd_upsample", st);
       hipLaunchKernelGGL(upsample_kernel, dim3(cdiv(Tin, 32), r, B), dim3(256), 0, st, x, K.up_w, K.up_b,
-                         xn, (int)Tin, r, p);
+                         xn, (int)Tin, r, p, lens, (int)(Tin / Tc));
       PD_LAUNCH_CHECK();
     }
     // --- 4 LVC layers (modules.py:208-217)
-    if (bf) PD_TRY(kp_kernels_all(K, hkb, reinterpret_cast<__bf16*>(ws + W.Kf), B, Tc, st));   // all 4 layers
+    if (bf) PD_TRY(kp_kernels_all(K, hkb, reinterpret_cast<__bf16*>(ws + W.Kf), B, Tc, st, false, lens));   // all 4 layers
     for (int i = 0; i < NLY; ++i) {
       const __bf16* Kbl = reinterpret_cast<const __bf16*>(ws + W.Kf) + (size_t)i * B * Tc * KPERLAYER;
       if (!bf) {
@@ -2115,6 +2148,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
                                K.kk_b + (size_t)i * KPERLAYER, ws + W.Kf, (long long)Tc * KPERLAYER,
                                KPERLAYER);
         for (int tap = 0; tap < 3; ++tap) add_seg(a, make_seg(hk, bsH, HK, HK, tap - 1));
+        a.lens = lens; a.lens_mul = 1;
         PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_FD_KP_KERNEL>(a, st, "fd_kp_kernel")));
       }
       const int dil = (int)std::pow(3, i);
@@ -2139,16 +2173,17 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
             add_seg(a, sg);
           }
           a.act = ACT_LRELU; a.alpha = 0.2f;
+          a.lens = lens; a.lens_mul = hop;
           PD_TRY((launch_gemm<1, 1, 4, 1, EPI_STORE, U_FD_LVC_PRECONV>(a, st, "fd_lvc_preconv")));
         }
         ProfScope ps("fd_lvc", st);
         if (bf)
           hipLaunchKernelGGL(lvc_kernel<__bf16>, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y,
                              Kbl, KPERLAYER, Bfp + i * 2 * CI,
-                             2 * CI * NLY, Tc, hop);
+                             2 * CI * NLY, Tc, hop, lens);
         else
           hipLaunchKernelGGL(lvc_kernel<float>, dim3(B * Tc), dim3(256), 0, st, xn, ad, ws + W.y, ws + W.Kf,
-                             KPERLAYER, Bfp + i * 2 * CI, 2 * CI * NLY, Tc, hop);
+                             KPERLAYER, Bfp + i * 2 * CI, 2 * CI * NLY, Tc, hop, lens);
       }
       PD_LAUNCH_CHECK();
     }
@@ -2399,15 +2434,16 @@ int fd_forward(const fd_model* m, const float* audio, const float* cond, const f
   if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, ws + W.condT, ws + W.nz, 1, B, Tc, st));
   PD_TRY(fd_net(m, ws, W, audio, ws + W.condT, ws + W.nz, 0, B, Tc, &x, st));
   hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w, m->final_b,
-                     eps, (float*)nullptr, 0.f, 0.f, 0.f, (const float*)nullptr, 0ull, 0u, (const int*)nullptr, L);
+                     eps, (float*)nullptr, 0.f, 0.f, 0.f, (const float*)nullptr, 0ull, 0u, (const int*)nullptr, L,
+                     (const int*)nullptr, 1);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
 
 int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce_, const float* den_, const float* sg_,
                     const float* steps_, int N, const float* x_T, const float* noise, unsigned long long seed,
-                    const int* utt_ids, int draw0, float* wav, int B, int Tc, void* workspace, size_t ws_bytes,
-                    void* stream) {
+                    const int* utt_ids, const int* lens, int draw0, float* wav, int B, int Tc, void* workspace,
+                    size_t ws_bytes, void* stream) {
   PD_CHECK_ARG(m && mel && ce_ && den_ && sg_ && steps_ && wav && workspace, "null pointer");
   PD_CHECK_ARG(B > 0 && Tc > 0 && N >= 1 && draw0 >= 0, "bad B/T'/N/draw0");
   // Long schedules (the 200- and 1000-step ones, fastdiff.py:58-61) run in chunks of
@@ -2450,7 +2486,7 @@ int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce_, const
     for (int j = 0; j < nc; ++j) sv[j] = steps_[j0 + j];
     PD_TRY(fill_steps(ws + W.steps, sv.data(), nc, B, st));
     PD_TRY(fd_step_mlp(m, ws, W, nc * B, st));
-    if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, mel, ws + W.nz, nc, B, Tc, st));
+    if (m->pool_bf) PD_TRY(fd_kp_hidden_all(m, ws, W, mel, ws + W.nz, nc, B, Tc, st, lens));
     if (side) {
       PD_HIP(hipEventRecord(m->ev_hidden, st));
       PD_HIP(hipStreamWaitEvent(m->side, m->ev_hidden, 0));
@@ -2463,7 +2499,7 @@ int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce_, const
           if (j > 0) PD_HIP(hipStreamWaitEvent(m->side, m->ev_lvc[b], 0));
           const __bf16* hkb = reinterpret_cast<const __bf16*>(ws + W.hall) + ((size_t)jl * nb + b) * rows * HK;
           __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf) + (size_t)b * rows * NLY * KPERLAYER;
-          PD_TRY(kp_kernels_all(m->blk[b], hkb, Kb, B, Tc, m->side, true));
+          PD_TRY(kp_kernels_all(m->blk[b], hkb, Kb, B, Tc, m->side, true, lens));
           PD_HIP(hipEventRecord(m->ev_kp[b], m->side));
         }
       }
@@ -2473,7 +2509,7 @@ int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce_, const
       const FdFinal fin{other, noise ? noise + (size_t)j * B * L : (const float*)nullptr, ce, den, sg, seed,
                         0x10000u + draw0 + j, utt_ids};
       PD_TRY(fd_net(m, ws, W, cur, mel, ws + W.nz + (size_t)jl * B * nb * CC, jl, B, Tc, &x, st,
-                    fused ? &fin : nullptr, side));
+                    fused ? &fin : nullptr, side, lens));
       if (x == nullptr) {   // updated inside the last LVC block
         std::swap(cur, other);
         continue;
@@ -2481,7 +2517,8 @@ int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce_, const
       {
         ProfScope ps("fd_final_update", st);
         hipLaunchKernelGGL(final_conv_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, st, x, m->final_w,
-                           m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + draw0 + j, utt_ids, L);
+                           m->final_b, (float*)nullptr, cur, ce, den, sg, fin.noise, seed, 0x10000u + draw0 + j, utt_ids, L,
+                           lens, m->hops[nb - 1]);
       }
       PD_LAUNCH_CHECK();
     }
@@ -2492,7 +2529,8 @@ int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce_, const
 
 int fd_sample(const fd_model* m, const float* mel, const float* beta, const float* alpha, const float* sigma,
               const float* steps, int N, const float* x_T, const float* noise, unsigned long long seed,
-              const int* utt_ids, float* wav, int B, int Tc, void* workspace, size_t ws_bytes, void* stream) {
+              const int* utt_ids, const int* lens, float* wav, int B, int Tc, void* workspace, size_t ws_bytes,
+              void* stream) {
   PD_CHECK_ARG(m && mel && beta && alpha && sigma && steps && wav && workspace, "null pointer");
   PD_CHECK_ARG(N >= 1, "bad N");
   // pass j runs schedule index n = N-1-j:
@@ -2505,8 +2543,8 @@ int fd_sample(const fd_model* m, const float* mel, const float* beta, const floa
     sg[j] = n > 0 ? sigma[n] : 0.f;
     st[j] = steps[n];
   }
-  return fd_sample_coefs(m, mel, ce.data(), den.data(), sg.data(), st.data(), N, x_T, noise, seed, utt_ids, 0, wav,
-                         B, Tc, workspace, ws_bytes, stream);
+  return fd_sample_coefs(m, mel, ce.data(), den.data(), sg.data(), st.data(), N, x_T, noise, seed, utt_ids, lens, 0,
+                         wav, B, Tc, workspace, ws_bytes, stream);
 }
 
 }  // extern "C"

@@ -79,6 +79,8 @@ struct GemmArgs {
   const int* uid;           // POSTERIOR: utterance id per batch row (null -> row index)
   int ksplit;               // STORE, > 1: split-K -- blockIdx.z sums one K range into `part`,
   float* part;              //   [ksplit][B*T][N] fp32, and gemm_splitk_reduce applies the epilogue
+  const int* lens;          // ragged batch: utterance b's segments read zero from row lens[b] * lens_mul
+  int lens_mul;             //   on (null: from row T), the rows being in units of 1 / lens_mul frame
 };
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
   const int nb = PAIRED ? blockIdx.y * (BN / 2) : blockIdx.y * BN;
   const int q4 = (tid & 7) * 4;
 
-  int a_b[A_IT], a_t[A_IT];
+  int a_b[A_IT], a_t[A_IT], a_len[A_IT];
   bool a_ok[A_IT];
 #pragma unroll
   for (int i = 0; i < A_IT; ++i) {
@@ -122,6 +124,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
     int b = a_ok[i] ? R / a.T : 0;
     a_b[i] = b;
     a_t[i] = R - b * a.T;
+    a_len[i] = a.lens ? min(a.lens[b] * a.lens_mul, a.T) : a.T;   // the conv's zero padding starts here
   }
   const TW* w_ptr[B_IT];
   bool w_ok[B_IT];
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs a) {
     for (int i = 0; i < A_IT; ++i) {
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       int vv = a_t[i] + sg.row_off;
-      if (a_ok[i] && c < sg.cs && vv >= 0 && vv < a.T) {
+      if (a_ok[i] && c < sg.cs && vv >= 0 && vv < a_len[i]) {
         long long off = (long long)a_b[i] * sg.bstride + (long long)vv * sg.row_mul * sg.ld + c;
         v = *reinterpret_cast<const float4*>(sg.src + off);
         if (sg.add_ten) {

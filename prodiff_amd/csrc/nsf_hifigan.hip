@@ -71,6 +71,16 @@ constexpr float NSF_SINE_AMP = 0.1f;     // SineGen defaults (models.py:118-119)
 constexpr float NSF_NOISE_STD = 0.003f;
 constexpr unsigned NSF_STREAM_INI = 0x4e534600u, NSF_STREAM_NOISE = 0x4e534601u;
 
+// Ragged batch (nsf_forward's lens): utterance b's rows at a stage of `rate` rows per mel frame end
+// at lens[b] * rate <= Tl; every conv reads zero past that end.  lens == null: every row is Tl.
+struct NsfRag {
+  const int* lens = nullptr;
+  int rate = 1;
+};
+__device__ __forceinline__ int nsf_tv(const NsfRag& rg, int b, int Tl) {
+  return rg.lens ? min(rg.lens[b] * rg.rate, Tl) : Tl;
+}
+
 // rad_values of SineGen._f02sine (models.py:137-141), bit-for-bit in fp32:
 // fn = f0 * (h+1); rad = fmod(fn / sr, 1); frame 0 adds rand_ini[h] (rand_ini[0] = 0).
 __device__ __forceinline__ float nsf_rad(float f0, int h, int f, float sr, const float* rand_ini,
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(256) void nsf_noise_conv_kernel(const float* __rest
                                                              const float* __restrict__ wt,
                                                              const float* __restrict__ bias, int C, int K,
                                                              int stride, int pad, long long Tout,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out, NsfRag rag_) {
   extern __shared__ float s_har[];
   const int CT = C < 256 ? C : 256, G = 256 / CT;
   const int tid = threadIdx.x;
@@ -171,9 +181,10 @@ __global__ __launch_bounds__(256) void nsf_noise_conv_kernel(const float* __rest
   const int win = (G * NC_ROWS - 1) * stride + K;
   const float* hb = har + (long long)b * L;
   const long long s0 = row0 * stride - pad;
+  const long long Lv = rag_.lens ? min((long long)rag_.lens[b] * rag_.rate, L) : L;   // the utterance's own end
   for (int i = tid; i < win; i += 256) {
     long long sidx = s0 + i;
-    s_har[i] = (sidx >= 0 && sidx < L) ? hb[sidx] : 0.f;
+    s_har[i] = (sidx >= 0 && sidx < Lv) ? hb[sidx] : 0.f;
   }
   __syncthreads();
   float acc[NC_ROWS];
@@ -210,7 +221,8 @@ template <int C>
 __global__ __launch_bounds__(256) void nsf_conv_small_kernel(const float* __restrict__ in, const float* __restrict__ wp,
                                                              int ldw, int kpad, const float* __restrict__ bias,
                                                              int taps, int dil, float alpha, float scale, int Tl,
-                                                             const float* __restrict__ res, float* __restrict__ out) {
+                                                             const float* __restrict__ res, float* __restrict__ out,
+                                                             NsfRag rag_) {
   constexpr int OC = C < 8 ? C : 8, NG = C / OC, NRG = 256 / NG, RR = 4, TR = NRG * RR, P = C + 1;
   extern __shared__ float lds[];
   const int pad = (taps - 1) * dil / 2;
@@ -218,7 +230,7 @@ __global__ __launch_bounds__(256) void nsf_conv_small_kernel(const float* __rest
   float* s_w = lds;                          // [tap][ci][co]
   float* s_x = lds + taps * C * C;           // [win][P]
   const int tid = threadIdx.x, b = blockIdx.y;
-  const int t0 = blockIdx.x * TR;
+  const int t0 = blockIdx.x * TR, Tv = nsf_tv(rag_, b, Tl);
   const float* ib = in + (long long)b * Tl * C;
   for (int i = tid; i < taps * C * C; i += 256) {
     int co = i % C, r = i / C, ci = r % C, k = r / C;
@@ -228,7 +240,7 @@ __global__ __launch_bounds__(256) void nsf_conv_small_kernel(const float* __rest
     int row = i / C, c = i - row * C;
     int t = t0 - pad + row;
     float v = 0.f;
-    if (t >= 0 && t < Tl) {
+    if (t >= 0 && t < Tv) {
       v = ib[(long long)t * C + c];
       v = (v >= 0.f ? v : alpha * v) * scale;
     }
@@ -269,7 +281,7 @@ __global__ __launch_bounds__(256) void nsf_conv_small_kernel(const float* __rest
 
 template <int C>
 int launch_conv_small(const NsfConv& c, const float* in, float alpha, float scale, int B, int Tl, float* out,
-                      const float* res, hipStream_t st) {
+                      const float* res, hipStream_t st, NsfRag rag_) {
   constexpr int OC = C < 8 ? C : 8, NG = C / OC, TR = 256 / NG * 4;
   const size_t lds = ((size_t)c.taps * C * C + (size_t)(TR + (c.taps - 1) * c.dil) * (C + 1)) * sizeof(float);
   if (lds > 160 * 1024) { set_error("nsf conv: LDS window too large"); return PD_ERR_UNSUPPORTED; }
@@ -278,7 +290,7 @@ int launch_conv_small(const NsfConv& c, const float* in, float alpha, float scal
   if (attr != hipSuccess) { set_error("nsf conv: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
   ProfScope ps("nsf_res_small", st);
   hipLaunchKernelGGL(nsf_conv_small_kernel<C>, dim3(cdiv(Tl, TR), B), dim3(256), lds, st, in, c.w, c.taps * c.kpad,
-                     c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out);
+                     c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out, rag_);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -323,13 +335,13 @@ __device__ __forceinline__ void nsf_store_utt(__amdgpu_buffer_rsrc_t r, int elem
 }
 
 // Stages window rows r0 .. r0 + W - 1 of `in` (lrelu(alpha) * scale, bf16) into win; rows outside
-// [0, Tl) are zero.  r04: loads unconditional (clamped row), zero rows by a multiply, and every LDS
+// [0, Tv) are zero (Tv <= Tl: the utterance's own end in a ragged batch; rows are laid out at Tl).  r04: loads unconditional (clamped row), zero rows by a multiply, and every LDS
 // store unconditional -- items past the window go to row W, one spare row the callers allocate
 // (or that the next stage overwrites): with `if (ok)` loads / `if (i < nitems)` stores hipcc sank
 // the loads into the branches and waited for each one, a round trip per item instead of per batch.
 template <int C, bool IN_BF>
-__device__ __forceinline__ void stage_window(const void* __restrict__ in, int b, int Tl, int r0, int W, float alpha,
-                                             float scale, __bf16* __restrict__ win, int lda, int tid) {
+__device__ __forceinline__ void stage_window(const void* __restrict__ in, int b, int Tl, int Tv, int r0, int W,
+                                             float alpha, float scale, __bf16* __restrict__ win, int lda, int tid) {
   constexpr int C8 = C / 8;
   const int nitems = W * C8;
   for (int base = tid; base < nitems; base += 256 * NSF_WB) {
@@ -339,7 +351,7 @@ __device__ __forceinline__ void stage_window(const void* __restrict__ in, int b,
       const int i = base + 256 * u;
       const int row = i / C8, c8 = i - row * C8;
       const int t = r0 + row;
-      const bool ok = i < nitems && t >= 0 && t < Tl;
+      const bool ok = i < nitems && t >= 0 && t < Tv;
       const float m = ok ? 1.f : 0.f;
       const long long e = ((long long)b * Tl + (ok ? t : 0)) * C + 8 * c8;
       if constexpr (IN_BF) {
@@ -382,7 +394,7 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
                                                         int ldw, int kpad, const float* __restrict__ bias, int taps,
                                                         int dil, float alpha, float scale, int Tl,
                                                         const float* __restrict__ res, void* __restrict__ out,
-                                                        int accum) {
+                                                        int accum, NsfRag rag_) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN, LDA = C + 8, KS = C / 16;
   static_assert(C % TN == 0, "channel tiling");
@@ -394,7 +406,7 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
   const int W = TM + (taps - 1) * dil;
   // 1. the input window, 8 channels (16 B of bf16) per item, NSF_WB items per thread in flight
   //    together (a load-convert-store loop waits one HBM round trip per item)
-  stage_window<C, IN_BF>(in, b, Tl, t0 - pad, W, alpha, scale, nsf_win, LDA, tid);
+  stage_window<C, IN_BF>(in, b, Tl, nsf_tv(rag_, b, Tl), t0 - pad, W, alpha, scale, nsf_win, LDA, tid);
   __syncthreads();
   // 2. taps x 16-deep k-steps; B fragments prefetched one step ahead
   const int r32 = lane & 31, h = lane >> 5;
@@ -505,7 +517,8 @@ template <int C, int FMO>
 __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restrict__ x, const __bf16* __restrict__ w1,
                                                       const __bf16* __restrict__ w2, int ldw, int kpad,
                                                       const float* __restrict__ b1, const float* __restrict__ b2,
-                                                      int taps, int dil, int Tl, float* __restrict__ out, int accum) {
+                                                      int taps, int dil, int Tl, float* __restrict__ out, int accum,
+                                                      NsfRag rag_) {
   constexpr int NCT = C / 32, RG = 4 / NCT, LDA = C + 8, KS = C / 16;
   constexpr int TM = 32 * FMO, RT1 = FMO + 1;            // output rows; c1 row tiles
   constexpr int MF1 = (RT1 + RG - 1) / RG, MF2 = (FMO + RG - 1) / RG;   // row tiles per wave
@@ -521,7 +534,8 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
   // wave's c1 is done (a barrier between c1's MFMAs and its epilogue): one window per block, so 2
   // blocks share a CU at C = 128 (r04: x and xt side by side, 88-101 KB, left room for one)
   __bf16* xtw = nsf_win;
-  stage_window<C, false>(x, b, Tl, t0 - p2 - p1, WX, NSF_LRELU, 1.f, xwin, LDA, tid);
+  const int Tv = nsf_tv(rag_, b, Tl);
+  stage_window<C, false>(x, b, Tl, Tv, t0 - p2 - p1, WX, NSF_LRELU, 1.f, xwin, LDA, tid);
   __syncthreads();
   const int S = taps * KS;
   constexpr int PF = KS >= NSF_PF ? NSF_PF : KS;
@@ -570,7 +584,7 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
         for (int reg = 0; reg < 16; ++reg) {
           const int i = rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, t = t0 - p2 + i;
           const float v = (float)(__bf16)(acc[m][reg] + bn);
-          const float u = (t >= 0 && t < Tl) ? (v >= 0.f ? v : NSF_LRELU * v) : 0.f;
+          const float u = (t >= 0 && t < Tv) ? (v >= 0.f ? v : NSF_LRELU * v) : 0.f;
           xtw[i * LDA + n] = (__bf16)u;
         }
       }
@@ -639,7 +653,7 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
 #endif
 template <int C>
 int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
-                  hipStream_t st) {
+                  hipStream_t st, NsfRag rag_) {
   constexpr int FMO = C == 32 ? NSF_PAIR_FMO32 : C == 64 ? NSF_PAIR_FMO64 : 4, TM = 32 * FMO;
   // x / xt window + stage_window's spare row
   const size_t lds = (size_t)(32 * (FMO + 1) + (c1.taps - 1) * c1.dil + 1) * (C + 8) * sizeof(__bf16);
@@ -648,7 +662,7 @@ int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, i
   if (attr != hipSuccess) { set_error("nsf pair: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
   ProfScope ps("nsf_pair", st);
   hipLaunchKernelGGL((nsf_pair_kernel<C, FMO>), dim3(cdiv(Tl, TM), 1, B), dim3(256), lds, st, x, lookup_bf16(c1.w),
-                     lookup_bf16(c2.w), c1.taps * c1.kpad, c1.kpad, c1.b, c2.b, c1.taps, c1.dil, Tl, out, accum);
+                     lookup_bf16(c2.w), c1.taps * c1.kpad, c1.kpad, c1.b, c2.b, c1.taps, c1.dil, Tl, out, accum, rag_);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -663,14 +677,14 @@ bool pair_ok(const nsf_model* m, const NsfConv& c1, const NsfConv& c2) {
 }
 
 int launch_pair(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
-                hipStream_t st) {
+                hipStream_t st, NsfRag rag_) {
   if ((long long)B * Tl * c1.cout >= (1ll << 31)) {
     set_error("nsf pair: B * T * C >= 2^31 elements (32-bit epilogue offsets)");
     return PD_ERR_UNSUPPORTED;
   }
-  if (c1.cout == 128) return launch_pair_c<128>(c1, c2, x, B, Tl, out, accum, st);
-  if (c1.cout == 32) return launch_pair_c<32>(c1, c2, x, B, Tl, out, accum, st);
-  return launch_pair_c<64>(c1, c2, x, B, Tl, out, accum, st);
+  if (c1.cout == 128) return launch_pair_c<128>(c1, c2, x, B, Tl, out, accum, st, rag_);
+  if (c1.cout == 32) return launch_pair_c<32>(c1, c2, x, B, Tl, out, accum, st, rag_);
+  return launch_pair_c<64>(c1, c2, x, B, Tl, out, accum, st, rag_);
 }
 
 // 16-channel variant (the last upsample stage, 512 samples per frame) on
@@ -685,7 +699,7 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
                                                           int kpad, const float* __restrict__ bias, int taps, int dil,
                                                           float alpha, float scale, int Tl,
                                                           const float* __restrict__ res, void* __restrict__ out,
-                                                          int accum) {
+                                                          int accum, NsfRag rag_) {
   constexpr int C = 16, TM = 256, LDA = 24, MAXP = 6;
   extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win16[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -694,7 +708,7 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
   const int W = TM + (taps - 1) * dil;
   // the window (W rows x 2 items) in batches of NSF_WB items per thread, every load of a batch
   // issued before any is converted (one round trip per batch, not one per item)
-  stage_window<C, IN_BF>(in, b, Tl, t0 - pad, W, alpha, scale, nsf_win16, LDA, tid);
+  stage_window<C, IN_BF>(in, b, Tl, nsf_tv(rag_, b, Tl), t0 - pad, W, alpha, scale, nsf_win16, LDA, tid);
   const int r16 = lane & 15, g = lane >> 4, kg = g & 1, tg = g >> 1;
   const int npair = (taps + 1) >> 1;
   // every pair's fragment loaded unconditionally (clamped tap) and zeroed by a bit mask: a load
@@ -759,14 +773,14 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
 }
 
 int launch_wconv16(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
-                   int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum) {
+                   int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum, NsfRag rag_) {
   if (c.taps > 12) { set_error("nsf wconv16: at most 12 taps"); return PD_ERR_UNSUPPORTED; }
   const size_t lds = (size_t)(256 + (c.taps - 1) * c.dil + 1) * 24 * sizeof(__bf16);   // + stage_window's spare row
   dim3 grid(cdiv(Tl, 256), B);
   ProfScope ps("nsf_res_small", st);
 #define PD_WCONV16(IB, OB)                                                                                      \
   hipLaunchKernelGGL((nsf_wconv16_kernel<IB, OB>), grid, dim3(256), lds, st, in, wb, c.kpad, c.b, c.taps, c.dil, \
-                     alpha, scale, Tl, res, out, accum)
+                     alpha, scale, Tl, res, out, accum, rag_)
   if (in_bf && out_bf) PD_WCONV16(true, true);
   else if (in_bf) PD_WCONV16(true, false);
   else if (out_bf) PD_WCONV16(false, true);
@@ -783,18 +797,18 @@ int launch_wconv16(const NsfConv& c, const __bf16* wb, const void* in, bool in_b
 template <int C>
 __global__ __launch_bounds__(256) void nsf_post_kernel(const float* __restrict__ in, const float* __restrict__ wp,
                                                        int kpad, const float* __restrict__ bias, float alpha,
-                                                       float scale, int Tl, float* __restrict__ out) {
+                                                       float scale, int Tl, float* __restrict__ out, NsfRag rag_) {
   constexpr int TR = 256, K = 7, P = C + 1;
   __shared__ float s_x[(TR + K - 1) * P];
   __shared__ float s_w[K * C];
-  const int tid = threadIdx.x, b = blockIdx.y, t0 = blockIdx.x * TR;
+  const int tid = threadIdx.x, b = blockIdx.y, t0 = blockIdx.x * TR, Tv = nsf_tv(rag_, b, Tl);
   for (int i = tid; i < K * C; i += 256) s_w[i] = wp[(i / C) * kpad + i % C];
   const float* ib = in + (long long)b * Tl * C;
   for (int i = tid; i < (TR + K - 1) * C; i += 256) {
     const int row = i / C, c = i - row * C;
     const int t = t0 - (K - 1) / 2 + row;
     float v = 0.f;
-    if (t >= 0 && t < Tl) {
+    if (t >= 0 && t < Tv) {
       v = ib[(long long)t * C + c];
       v = (v >= 0.f ? v : alpha * v) * scale;
     }
@@ -824,7 +838,7 @@ __global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict
                                                       long long wstride, int kpad, int ntap, int u, int p, int dlo,
                                                       int cout, const float* __restrict__ bias, float alpha,
                                                       float scale, int Tin, const float* __restrict__ res,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, NsfRag rag_) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN, LDA = CIN + 8, KS = CIN / 16;
   constexpr int PF = KS >= NSF_PF ? NSF_PF : KS;
@@ -833,7 +847,7 @@ __global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict
   const int wm = wave % WM, wn = wave / WM;
   const int b = blockIdx.z, i0 = blockIdx.x * TQ, n0 = blockIdx.y * TN;
   const int W = TQ + ntap;                 // rows i0 + dlo ... (dlo = 1 - ntap, top offset q0 <= 1)
-  stage_window<CIN, false>(in, b, Tin, i0 + dlo, W, alpha, scale, nsf_uwin, LDA, tid);
+  stage_window<CIN, false>(in, b, Tin, nsf_tv(rag_, b, Tin), i0 + dlo, W, alpha, scale, nsf_uwin, LDA, tid);
   __syncthreads();
   const int r32 = lane & 31, h = lane >> 5;
   const int ldw = ntap * kpad;
@@ -917,7 +931,7 @@ __global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict
 
 template <int CIN, int FM, int FN, int WM, int WN, bool NPAD>
 int launch_ups_c(const NsfUps& U, const __bf16* wb, const float* in, float scale, int B, int Tin, const float* res,
-                 float* out, hipStream_t st) {
+                 float* out, hipStream_t st, NsfRag rag_) {
   constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN;
   const int p = (U.k - U.u) / 2;
   const size_t lds = (size_t)(TQ + U.ntap + 1) * (CIN + 8) * sizeof(__bf16);   // + stage_window's spare row
@@ -929,7 +943,7 @@ int launch_ups_c(const NsfUps& U, const __bf16* wb, const float* in, float scale
   ProfScope ps("nsf_ups", st);
   hipLaunchKernelGGL((nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD>), grid, dim3(256), lds, st, in, wb,
                      (long long)(U.w[1] - U.w[0]), U.kpad, U.ntap, U.u, p, 1 - U.ntap, U.cout, U.b, NSF_LRELU,
-                     scale, Tin, res, out);
+                     scale, Tin, res, out, rag_);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -953,19 +967,19 @@ bool ups_window_ok(const NsfUps& U, bool wconv) {
 }
 
 int launch_ups_window(const NsfUps& U, const float* in, float scale, int B, int Tin, const float* res, float* out,
-                      hipStream_t st) {
+                      hipStream_t st, NsfRag rag_) {
   const __bf16* wb = lookup_bf16(U.w[0]);
   // (r02: one row-wave per column tile, <512,2,1,1,4> / <256,4,1,1,4>, measured slower: 188 vs 178 us avg)
-  if (U.cin == 512) return launch_ups_c<512, 1, 2, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);
-  if (U.cin == 256) return launch_ups_c<256, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);
-  if (U.cin == 128) return launch_ups_c<128, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st);
-  if (U.cin == 64) return launch_ups_c<64, 1, 1, 4, 1, false>(U, wb, in, scale, B, Tin, res, out, st);
-  return launch_ups_c<32, 1, 1, 4, 1, true>(U, wb, in, scale, B, Tin, res, out, st);
+  if (U.cin == 512) return launch_ups_c<512, 1, 2, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_);
+  if (U.cin == 256) return launch_ups_c<256, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_);
+  if (U.cin == 128) return launch_ups_c<128, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_);
+  if (U.cin == 64) return launch_ups_c<64, 1, 1, 4, 1, false>(U, wb, in, scale, B, Tin, res, out, st, rag_);
+  return launch_ups_c<32, 1, 1, 4, 1, true>(U, wb, in, scale, B, Tin, res, out, st, rag_);
 }
 
 template <int C, int FM, int FN, int WM, int WN>
 int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
-                   int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum) {
+                   int Tl, void* out, bool out_bf, const float* res, hipStream_t st, int accum, NsfRag rag_) {
   constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN;
   const size_t lds = (size_t)(TM + (c.taps - 1) * c.dil + 1) * (C + 8) * sizeof(__bf16);   // + stage_window's spare row
   if (lds > 160 * 1024) { set_error("nsf conv: LDS window too large"); return PD_ERR_UNSUPPORTED; }
@@ -978,7 +992,7 @@ int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_b
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                                                  \
     if (attr != hipSuccess) { set_error("nsf conv: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }    \
     hipLaunchKernelGGL((nsf_wconv_kernel<C, FM, FN, WM, WN, IB, OB>), grid, dim3(256), lds, st, in, wb, ldw,      \
-                       c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out, accum);                            \
+                       c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out, accum, rag_);                        \
   } while (0)
   ProfScope ps("nsf_res", st);
   if (in_bf && out_bf) PD_WCONV(true, true);
@@ -1000,7 +1014,7 @@ bool wconv_ok(const NsfConv& c) {
 // accum = 1: out (fp32) += conv + res -- the ResBlock sum xs += resblock_j(x) (models.py:275-279)
 // fused into the block's last conv instead of a separate pass.
 int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, float scale, int B, int Tl, void* out,
-                 bool out_bf, const float* res, hipStream_t st, int accum = 0) {
+                 bool out_bf, const float* res, hipStream_t st, int accum, NsfRag rag_) {
   const __bf16* wb = lookup_bf16(c.w);
   // 32-bit element offsets, and one utterance's bytes inside the unsigned buffer-resource range
   if ((long long)B * Tl * c.cout >= (1ll << 31) || (long long)Tl * c.cout * 4 >= (1ll << 32)) {
@@ -1017,11 +1031,11 @@ int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, floa
     // 2 x 2 wave grids at C = 128/256 read every fragment twice; C5 21.07 -> 19.19 ms/step,
     // ResBlock convs 187 -> 159 us avg).  C = 32: 128, 256 or 512 rows per block measured
     // equal or slower than 128 rows with four row-waves.
-    case 256: return launch_wconv_c<256, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
-    case 128: return launch_wconv_c<128, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
-    case 64: return launch_wconv_c<64, 4, 1, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
-    case 32: return launch_wconv_c<32, 1, 1, 4, 1>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
-    case 16: return launch_wconv16(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum);
+    case 256: return launch_wconv_c<256, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
+    case 128: return launch_wconv_c<128, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
+    case 64: return launch_wconv_c<64, 4, 1, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
+    case 32: return launch_wconv_c<32, 1, 1, 4, 1>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
+    case 16: return launch_wconv16(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
     default: set_error("nsf wconv: unsupported channel count"); return PD_ERR_UNSUPPORTED;
   }
 }
@@ -1081,13 +1095,13 @@ NsfWs nsf_layout(const nsf_model* m, int B, int T) {
 // conv over time-major `in` [B][Tl][cin] (taps with dilation, zero padding (taps-1)*dil/2),
 // pre-activation leaky_relu(alpha) * in_scale on load; out = act(conv + b) (+ res).
 int nsf_conv(const NsfConv& c, const float* in, float in_alpha, float in_scale, int B, int Tl, float* out,
-             const float* res, int act, hipStream_t st, int use) {
+             const float* res, int act, hipStream_t st, int use, NsfRag rag_) {
   if (use == U_NSF_RES && c.cin == c.cout && c.cout <= c.small_max && in_alpha >= 0.f) {
     switch (c.cout) {
-      case 4: return launch_conv_small<4>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
-      case 8: return launch_conv_small<8>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
-      case 16: return launch_conv_small<16>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
-      case 32: return launch_conv_small<32>(c, in, in_alpha, in_scale, B, Tl, out, res, st);
+      case 4: return launch_conv_small<4>(c, in, in_alpha, in_scale, B, Tl, out, res, st, rag_);
+      case 8: return launch_conv_small<8>(c, in, in_alpha, in_scale, B, Tl, out, res, st, rag_);
+      case 16: return launch_conv_small<16>(c, in, in_alpha, in_scale, B, Tl, out, res, st, rag_);
+      case 32: return launch_conv_small<32>(c, in, in_alpha, in_scale, B, Tl, out, res, st, rag_);
       default: break;
     }
   }
@@ -1101,6 +1115,7 @@ int nsf_conv(const NsfConv& c, const float* in, float in_alpha, float in_scale, 
     add_seg(a, s);
   }
   a.act = act;
+  a.lens = rag_.lens; a.lens_mul = rag_.rate;
   if (res) { a.res = res; a.res_bs = (long long)Tl * c.cout; a.res_ld = c.cout; }
   if (use == U_NSF_POST) return launch_gemm<1, 1, 4, 1, EPI_STORE, U_NSF_POST>(a, st, "nsf_post");
   if (use == U_NSF_CONV_PRE) return launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_CONV_PRE>(a, st, "nsf_conv_pre");
@@ -1323,8 +1338,8 @@ size_t nsf_workspace_size(const nsf_model* m, int B, int T) {
 }
 
 int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const float* f0, const float* rand_ini, const float* noise,
-                unsigned long long seed, const int* utt_ids, float* wav, int B, int T, void* workspace, size_t ws_bytes,
-                void* stream) {
+                unsigned long long seed, const int* utt_ids, const int* lens, float* wav, int B, int T, void* workspace,
+                size_t ws_bytes, void* stream) {
   PD_CHECK_ARG(m && mel && f0 && wav && B >= 0 && T >= 0, "null argument");
   if (B == 0 || T == 0) return PD_OK;
   const NsfWs W = nsf_layout(m, B, T);
@@ -1348,6 +1363,10 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
                        dim, sr, rand_ini, noise, seed, utt_ids, m->lin_w, m->lin_b, har);
   }
   PD_LAUNCH_CHECK();
+  // ragged batch: stage s of `rate` samples per frame reads zero past lens[b] * rate (the phase
+  // prefix and the source are causal per utterance, so frames past an utterance's end change nothing
+  // before it)
+  auto rag = [&](int rate) { NsfRag g; g.lens = lens; g.rate = rate; return g; };
   // conv_pre(mel_scale * mel^T) (nsf_hifigan.py:53, models.py:267)
   {
     const NsfConv& c = m->pre;
@@ -1358,6 +1377,7 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
       s.scale = mel_scale;
       add_seg(a, s);
     }
+    a.lens = lens; a.lens_mul = 1;
     PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_CONV_PRE>(a, st, "nsf_conv_pre")));
   }
   int Tin = T;
@@ -1371,14 +1391,14 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
       const size_t lds = (size_t)((G * NC_ROWS - 1) * U.nc_stride + U.nc_k) * sizeof(float);
       ProfScope ps("nsf_noise_conv", st);
       hipLaunchKernelGGL(nsf_noise_conv_kernel, dim3(cdiv(Lc, G * NC_ROWS), U.cout / CT, B), dim3(256), lds, st, har,
-                         L, U.nc_w, U.nc_b, U.cout, U.nc_k, U.nc_stride, U.nc_pad, (long long)Lc, XSRC);
+                         L, U.nc_w, U.nc_b, U.cout, U.nc_k, U.nc_stride, U.nc_pad, (long long)Lc, XSRC, rag(m->upp));
       PD_LAUNCH_CHECK();
     }
     // x = ups(leaky_relu(x, 0.1)) + noise_conv(har)  (models.py:270-274): the windowed bf16
     // kernel, or one GEMM per phase
     const int p = (U.k - U.u) / 2;
     const bool upsw = ups_window_ok(U, m->ups_window);
-    if (upsw) PD_TRY(launch_ups_window(U, XS, in_scale, B, Tin, XSRC, X, st));
+    if (upsw) PD_TRY(launch_ups_window(U, XS, in_scale, B, Tin, XSRC, X, st, rag(Tin / T)));
     for (int phi = 0; phi < (upsw ? 0 : U.u); ++phi) {
       const int q0 = U.qmin[phi];
       const int o = q0 * U.u + phi - p;        // first output row of this phase, in [0, u)
@@ -1395,11 +1415,13 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
       a.res = XSRC + (long long)o * U.cout;
       a.res_bs = (long long)Lc * U.cout;
       a.res_ld = U.u * U.cout;
+      a.lens = lens; a.lens_mul = Tin / T;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_STORE, U_NSF_UPS>(a, st, "nsf_ups")));
     }
     // xs = sum_j resblock_j(x); x = xs / num_kernels (models.py:275-281); the division is
     // folded into the next consumer's load scale.
     const long long n4 = (long long)B * Lc * U.cout / 4;
+    const NsfRag rag_ = rag(Lc / T);
     for (int j = 0; j < nk; ++j) {
       float* target = j == 0 ? XS : R;
       const float* cur = X;
@@ -1415,7 +1437,7 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
             // landing in target -- or accumulating into XS for resblock j >= 1
             const bool last_acc = j > 0 && q == D - 1;
             float* dst = q == D - 1 ? (last_acc ? XS : target) : ((D - 2 - q) % 2 == 0 ? T1 : target);
-            PD_TRY(launch_pair(c1, c2, cur, B, Lc, dst, last_acc ? 1 : 0, st));
+            PD_TRY(launch_pair(c1, c2, cur, B, Lc, dst, last_acc ? 1 : 0, st, rag_));
             if (last_acc) { summed = true; continue; }
             cur = dst;
             continue;
@@ -1424,22 +1446,22 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
             // windowed bf16 convs; the inner activation xt = c1(lrelu(x)) travels as bf16; the
             // last pair of resblock j >= 1 accumulates straight into XS
             const bool last_acc = j > 0 && q == d.num_dilations - 1;
-            PD_TRY(launch_wconv(c1, cur, false, NSF_LRELU, 1.f, B, Lc, T1, true, nullptr, st));
+            PD_TRY(launch_wconv(c1, cur, false, NSF_LRELU, 1.f, B, Lc, T1, true, nullptr, st, 0, rag_));
             PD_TRY(launch_wconv(c2, T1, true, NSF_LRELU, 1.f, B, Lc, last_acc ? XS : target, false, cur, st,
-                                last_acc ? 1 : 0));
+                                last_acc ? 1 : 0, rag_));
             if (last_acc) { summed = true; continue; }
           } else {
-            PD_TRY(nsf_conv(c1, cur, NSF_LRELU, 1.f, B, Lc, T1, nullptr, ACT_NONE, st, U_NSF_RES));
-            PD_TRY(nsf_conv(c2, T1, NSF_LRELU, 1.f, B, Lc, target, cur, ACT_NONE, st, U_NSF_RES));
+            PD_TRY(nsf_conv(c1, cur, NSF_LRELU, 1.f, B, Lc, T1, nullptr, ACT_NONE, st, U_NSF_RES, rag_));
+            PD_TRY(nsf_conv(c2, T1, NSF_LRELU, 1.f, B, Lc, target, cur, ACT_NONE, st, U_NSF_RES, rag_));
           }
           cur = target;
         } else {
           // out must not alias the taps being read: ping-pong target <-> T1
           float* dst = (cur == target) ? T1 : target;
           if (wconv_ok(m->res[r + q]))
-            PD_TRY(launch_wconv(m->res[r + q], cur, false, NSF_LRELU, 1.f, B, Lc, dst, false, cur, st));
+            PD_TRY(launch_wconv(m->res[r + q], cur, false, NSF_LRELU, 1.f, B, Lc, dst, false, cur, st, 0, rag_));
           else
-            PD_TRY(nsf_conv(m->res[r + q], cur, NSF_LRELU, 1.f, B, Lc, dst, cur, ACT_NONE, st, U_NSF_RES));
+            PD_TRY(nsf_conv(m->res[r + q], cur, NSF_LRELU, 1.f, B, Lc, dst, cur, ACT_NONE, st, U_NSF_RES, rag_));
           cur = dst;
         }
       }
@@ -1459,13 +1481,13 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
     ProfScope ps("nsf_post", st);
     if (m->post.cin == 16)
       hipLaunchKernelGGL(nsf_post_kernel<16>, dim3(cdiv(Tin, 256), B), dim3(256), 0, st, XS, m->post.w, m->post.kpad,
-                         m->post.b, 0.01f, in_scale, Tin, wav);
+                         m->post.b, 0.01f, in_scale, Tin, wav, rag(Tin / T));
     else
       hipLaunchKernelGGL(nsf_post_kernel<32>, dim3(cdiv(Tin, 256), B), dim3(256), 0, st, XS, m->post.w, m->post.kpad,
-                         m->post.b, 0.01f, in_scale, Tin, wav);
+                         m->post.b, 0.01f, in_scale, Tin, wav, rag(Tin / T));
     PD_LAUNCH_CHECK();
   } else {
-    PD_TRY(nsf_conv(m->post, XS, 0.01f, in_scale, B, Tin, wav, nullptr, ACT_TANH, st, U_NSF_POST));
+    PD_TRY(nsf_conv(m->post, XS, 0.01f, in_scale, B, Tin, wav, nullptr, ACT_TANH, st, U_NSF_POST, rag(Tin / T)));
   }
   return PD_OK;
 }

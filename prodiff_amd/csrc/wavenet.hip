@@ -80,6 +80,7 @@ struct WnLayerArgs {
   const __bf16* W2f;      // [2C/32][C/16][64][8]
   const float* b2;        // [2C]
   int B, T, H, dil, first;
+  const int* lens;        // frames of each row's utterance (null: T); taps past it read zero
   const __bf16* pfw[2];   // the next layer's W1 and W2 fragments (never null), pulled into each
   int pf_lines[2];        //   XCD's L2 line by line: pf_lines 128-B lines each
 #ifdef WN_TRACE
@@ -183,7 +184,8 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
         while (tq >= P.T) { tq -= P.T; ++bq; }
       }
       const int b = bq, t = tq, tt = isx ? t + sh : t;
-      const bool v = R < rows && tt >= 0 && tt < P.T;
+      const int lb = P.lens ? P.lens[b] : P.T;    // ragged batch: the utterance's own end
+      const bool v = R < rows && tt >= 0 && tt < P.T && tt < lb;
       const int ttc = tt < 0 ? 0 : tt >= P.T ? P.T - 1 : tt;
       ok[it] = v ? 1.f : 0.f;
       bi[it] = b;
@@ -334,6 +336,7 @@ struct WnStackArgs {
   const __bf16* W2f;      // [L][2C/32][C/16][64][8]
   const float* b2;        // [L][2C]
   int rows, T, l0, nl, first, L;
+  const int* lens;        // frames of each row's utterance (null: T): the conv's zero padding starts there
   int ro;                 // output rows per block (<= 32): window rows [16, 16 + ro)
   // PD_WN_OPT_STACK_FUSE, first launch: x = relu(W_in spec + b_in) of the window rows computed
   // here (spec [rows][M] fp32, Winb [C][ldw_in] bf16, M <= ldw_in <= 128) instead of read
@@ -490,9 +493,10 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   bool mlo[2], mhi[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int R = W0 + 32 * q + r32, Rc = min(max(R, 0), rows - 1), t = Rc - (Rc / T) * T;
+    const int R = W0 + 32 * q + r32, Rc = min(max(R, 0), rows - 1), bq = Rc / T, t = Rc - bq * T;
+    const int lb = P.lens ? min(P.lens[bq], T) : T;   // ragged batch: the utterance's own end
     mlo[q] = R >= 0 && R < rows && t >= 1;
-    mhi[q] = R >= 0 && R < rows && t <= T - 2;
+    mhi[q] = R >= 0 && R < rows && t <= lb - 2;
   }
   __syncthreads();
   const bf16x8 z8 = {};
@@ -699,6 +703,7 @@ struct WnF32Args {
   float* skip;              // RESSKIP: skip sum
   int first;                // RESSKIP: first layer (skip = value)
   int rows, T, C, H, dil;
+  const int* lens;          // GATE: frames of each row's utterance (null: T)
 };
 
 // ADD: A = row + aadd (the taps' x + dp).  A compile-time choice: a runtime `if (aadd)` around
@@ -770,7 +775,8 @@ __global__ __launch_bounds__(NW * 64) void wn_f32_layer_kernel(const WnF32Args P
     if constexpr (GATE) {
       const int sg = wave / (NW / 4), k0 = (wave % (NW / 4)) * (C / (NW / 4));   // segment, offset in it
       if (sg < 3) {   // tap segment: x(t + (sg - 1) d) + dp, zero outside the utterance
-        const int tt = t + (sg - 1) * P.dil, ok = R < P.rows && tt >= 0 && tt < P.T;
+        const int lb = P.lens ? P.lens[b] : P.T;   // ragged batch: the utterance's own end
+        const int tt = t + (sg - 1) * P.dil, ok = R < P.rows && tt >= 0 && tt < P.T && tt < lb;
         const float* arow = P.a + ((long long)b * P.T + min(max(tt, 0), P.T - 1)) * C + k0;
         wf32_seg<NCH, true>(arow, P.dp + (long long)b * P.dp_ld + k0, ok, w0 + sg * C + k0, w1 + sg * C + k0, h, acc0,
                             acc1);
@@ -1346,9 +1352,12 @@ struct StackTail {
 // cond: time-major [B][T][H]; dproj: [B][L][C].  Leaves relu(skip head) in ws.hs -- or, when
 // `tail` is given and the stack kernel fuses it (PD_WN_OPT_STACK_FUSE), applies the whole output
 // stage itself and sets *tail_done.
+// lens (device, B ints, or null): each row's utterance length in frames -- a ragged batch whose rows
+// are padded to T; every dilated conv reads zero past the row's own end, so each utterance's
+// frames equal a run of that utterance alone (B = 1, T = lens[b]).
 int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float* xin,
                  const float* cond, const float* dproj, int B, int T, hipStream_t st,
-                 const StackTail* tail = nullptr, bool* tail_done = nullptr) {
+                 const StackTail* tail = nullptr, bool* tail_done = nullptr, const int* lens = nullptr) {
   const int M = h->M, H = h->H, C = h->C, Ly = h->L;
   const long long BTs = (long long)T;
   float* x = ws + Lw.x;
@@ -1374,6 +1383,10 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
   // bf16 layer implementation (PD_WN_OPT_LAYER 1): GATE + RESSKIP launches.  Not the default: at
   // B*T = 1722 .. 27552 frames it measured equal to or slower than the fused kernel.
   const bool two = h->W1p && dil_max <= 16 && h->layer_mode == 1;
+  if (two && lens) {
+    set_error("PD_WN_OPT_LAYER 1 (two-kernel layers) does not take ragged batches (lens)");
+    return PD_ERR_UNSUPPORTED;
+  }
   if (two) {
     // bf16: GATE + RESSKIP launches per residual layer (wn_gate_bf16_kernel, wn_resskip_bf16_kernel)
     __bf16* xa = reinterpret_cast<__bf16*>(ws + Lw.xa);
@@ -1431,6 +1444,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       P.dp = dproj; P.dp_ld = Ly * C;
       P.W1f = h->W1f; P.b1 = h->bl1; P.W2f = h->W2f; P.b2 = h->bl2;
       P.rows = rows; P.T = T; P.l0 = l0; P.nl = std::min(h->stack_nl, Ly - l0); P.first = l0 == 0; P.L = Ly;
+      P.lens = lens;
       // output rows per block (PD_WN_OPT_STACK_RO, default 32).  r04: spreading C3's 6888 rows over
       // all 256 CUs (27 rows per block) measured slower than 216 blocks of 32 (214 vs 202-205 us per
       // 10 layers, profiles/r04_ab/): every block streams each layer's 1.3 MB of weights from its
@@ -1462,7 +1476,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       P.dp = dproj + (size_t)l * C; P.dp_ld = Ly * C;
       P.W1f = h->W1f + (size_t)l * 2 * C * (3 * C + H); P.b1 = h->bl1 + (size_t)l * 2 * C;
       P.W2f = h->W2f + (size_t)l * 2 * C * C; P.b2 = h->bl2 + (size_t)l * 2 * C;
-      P.B = B; P.T = T; P.H = H; P.dil = 1 << (l % h->cyc); P.first = (l == 0);
+      P.B = B; P.T = T; P.H = H; P.dil = 1 << (l % h->cyc); P.first = (l == 0); P.lens = lens;
       // the next layer's weights (the last layer, or prefetch off: this layer's, already on-die)
       const int lp = l + 1 < Ly && h->l2_prefetch ? l + 1 : l;
       P.pfw[0] = h->W1f + (size_t)lp * 2 * C * (3 * C + H);
@@ -1490,7 +1504,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
     if (f32k) {
       const dim3 grid((unsigned)cdiv(rows, 32), C / 32);
       WnF32Args F{};
-      F.rows = rows; F.T = T; F.C = C; F.H = H; F.dil = dil;
+      F.rows = rows; F.T = T; F.C = C; F.H = H; F.dil = dil; F.lens = lens;
       F.a = x; F.cond = cond; F.dp = dproj + (size_t)l * C; F.dp_ld = Ly * C;
       F.W = h->Wl1 + (size_t)l * 2 * C * h->ldw1; F.ldw = h->ldw1; F.bias = h->bl1 + (size_t)l * 2 * C; F.g = g;
       {
@@ -1522,6 +1536,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       a.half = C;
       a.ksplit = wn_ksplit((long long)B * T, C, h->ldw1, h->ksplit_blocks);
       a.part = ws + Lw.part;
+      a.lens = lens; a.lens_mul = 1;
       PD_TRY((launch_gemm<1, 2, 4, 1, EPI_GATE, U_WN_GATE>(a, st, "wn_gate")));
     }
     {  // o = W_out g + b ; x = (x + o[:C]) / sqrt2 ; skip += o[C:]   (wavenet.py:69-72)
@@ -1762,8 +1777,8 @@ int pd_wavenet_forward(const pd_wavenet* h, const float* spec, const float* step
 
 int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1, const float* coef2,
                       const float* sigma, int S, const float* x_T, const float* noise,
-                      unsigned long long seed, const int* utt_ids, float* mel, int B, int T, void* workspace,
-                      size_t ws_bytes, void* stream) {
+                      unsigned long long seed, const int* utt_ids, const int* lens, float* mel, int B, int T,
+                      void* workspace, size_t ws_bytes, void* stream) {
   PD_CHECK_ARG(h && cond && coef1 && coef2 && sigma && mel && workspace, "null pointer");
   PD_CHECK_ARG(B > 0 && T > 0 && S >= 1 && S <= 64, "bad B/T/S");
   WsLayout Lw = ws_layout(h, B, T, S);
@@ -1790,7 +1805,7 @@ int pd_prodiff_sample(const pd_wavenet* h, const float* cond, const float* coef1
     tl.noise = noise ? noise + (size_t)j * BTM : nullptr; tl.noise_bs = BTs * M; tl.noise_ld = M;
     tl.seed = seed; tl.stream_id = (unsigned)j; tl.uid = utt_ids;
     bool done = false;
-    PD_TRY(wavenet_core(h, ws, Lw, mel, cond, ws + Lw.dproj + (size_t)j * B * Ly * C, B, T, st, &tl, &done));
+    PD_TRY(wavenet_core(h, ws, Lw, mel, cond, ws + Lw.dproj + (size_t)j * B * Ly * C, B, T, st, &tl, &done, lens));
     if (done) continue;
     GemmArgs a = make_gemm(B, T, M, h->Wo, C, h->bo, mel, BTs * M, M);
     add_seg(a, make_seg(ws + Lw.hs, BTs * C, C, C, 0));
@@ -1856,9 +1871,8 @@ size_t pd_reflow_workspace_size(const pd_wavenet* h, int B, int T, int S, int al
 }
 
 int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, float time_scale,
-                     const float* x_T, unsigned long long seed, const int* utt_ids, float* x, int B, int T,
-                     void* workspace,
-                     size_t ws_bytes, void* stream) {
+                     const float* x_T, unsigned long long seed, const int* utt_ids, const int* lens, float* x,
+                     int B, int T, void* workspace, size_t ws_bytes, void* stream) {
   PD_CHECK_ARG(h && cond && x && workspace, "null pointer");
   RkTableau tb;
   PD_CHECK_ARG(reflow_tableau(algo, tb), "algorithm must be PD_REFLOW_EULER/RK2/RK4/RK5");
@@ -1905,7 +1919,8 @@ int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, fl
         xin = xs;
       }
       const int e = i * tb.s + j;
-      PD_TRY(wavenet_core(h, ws, Lw, xin, cond, ws + Lw.dproj + (size_t)e * B * Ly * C, B, T, st));
+      PD_TRY(wavenet_core(h, ws, Lw, xin, cond, ws + Lw.dproj + (size_t)e * B * Ly * C, B, T, st, nullptr, nullptr,
+                          lens));
       GemmArgs a = make_gemm(B, T, M, h->Wo, C, h->bo, tb.s == 1 ? x : kb + (size_t)j * kstride, BTs * M, M);
       add_seg(a, make_seg(ws + Lw.hs, BTs * C, C, C, 0));
       if (tb.s == 1) {   // Euler: x += v dt fused into the output projection (reflow.py:50)

@@ -271,9 +271,11 @@ class FastDiff(nn.Module):
         return x
 
     @torch.no_grad()
-    def sample_coefs(self, mel, ce, den, sg, steps, x_T=None, noise=None, seed=None, utt_ids=None, draw0=0):
+    def sample_coefs(self, mel, ce, den, sg, steps, x_T=None, noise=None, seed=None, utt_ids=None, draw0=0,
+                     lens=None):
         """The reverse loop with explicit per-pass coefficients (fd_sample_coefs): pass j
-        evaluates eps at steps[j] and sets x = (x - ce[j] eps) / den[j] + sg[j] z."""
+        evaluates eps at steps[j] and sets x = (x - ce[j] eps) / den[j] + sg[j] z.  ``lens``: ragged
+        batch, each row's utterance length in mel frames (``sample``)."""
         h = self.handle()
         B, Tc, _ = mel.shape
         N = len(steps)
@@ -286,19 +288,23 @@ class FastDiff(nn.Module):
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         wav = torch.empty(B, 1, L, device=dev, dtype=torch.float32)
         uid = _lib.utt_ids(utt_ids, B, dev)
+        ln = _lib.lens(lens, B, Tc, dev)
         lib = _lib.lib()
         ws, wsb = self._ws.get(lib.fd_workspace_size(h, B, Tc, N), dev)
         _lib.check(lib.fd_sample_coefs(h, _lib.fptr(mel), _lib.farr(ce), _lib.farr(den), _lib.farr(sg),
                                        _lib.farr(steps), N, _lib.fptr(xT), _lib.fptr(nz), seed, _lib.iptr(uid),
-                                       int(draw0), _lib.fptr(wav), B, Tc, ws, wsb, _lib.stream_ptr(dev)))
+                                       _lib.iptr(ln), int(draw0), _lib.fptr(wav), B, Tc, ws, wsb,
+                                       _lib.stream_ptr(dev)))
         return wav
 
     @torch.no_grad()
-    def sample(self, mel, beta, alpha, sigma, steps, x_T=None, noise=None, seed=None, utt_ids=None):
+    def sample(self, mel, beta, alpha, sigma, steps, x_T=None, noise=None, seed=None, utt_ids=None, lens=None):
         """Fused reverse process.  mel [B,T',80] TIME-major (the ProDiff output);
         beta/alpha/sigma/steps: float32 arrays of the reverse schedule;
         x_T [B,1,L] / noise [N-1,B,1,L] optional explicit draws -> wav [B,1,L].
-        Missing draws: on-device Philox keyed by ``seed`` and each row's ``utt_ids``."""
+        Missing draws: on-device Philox keyed by ``seed`` and each row's ``utt_ids``.
+        lens: ragged batch -- each row's utterance length in mel frames (<= T'); row b's first
+        lens[b] * hop samples equal a run of that utterance alone (include/prodiff_hip.h)."""
         h = self.handle()
         B, Tc, _ = mel.shape
         N = len(steps)
@@ -313,11 +319,12 @@ class FastDiff(nn.Module):
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         wav = torch.empty(B, 1, L, device=dev, dtype=torch.float32)
         uid = _lib.utt_ids(utt_ids, B, dev)
+        ln = _lib.lens(lens, B, Tc, dev)
         lib = _lib.lib()
         ws, wsb = self._ws.get(lib.fd_workspace_size(h, B, Tc, N), dev)
         _lib.check(lib.fd_sample(h, _lib.fptr(mel), _lib.farr(beta), _lib.farr(alpha), _lib.farr(sigma),
-                                 _lib.farr(steps), N, _lib.fptr(xT), _lib.fptr(nz), seed, _lib.iptr(uid), _lib.fptr(wav),
-                                 B, Tc, ws, wsb, _lib.stream_ptr(dev)))
+                                 _lib.farr(steps), N, _lib.fptr(xT), _lib.fptr(nz), seed, _lib.iptr(uid),
+                                 _lib.iptr(ln), _lib.fptr(wav), B, Tc, ws, wsb, _lib.stream_ptr(dev)))
         return wav
 
 

@@ -200,11 +200,12 @@ class Generator(nn.Module):
 
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
-    def synthesize(self, mel, f0, mel_scale=1.0, rand_ini=None, noise=None, seed=None, utt_ids=None):
+    def synthesize(self, mel, f0, mel_scale=1.0, rand_ini=None, noise=None, seed=None, utt_ids=None, lens=None):
         """mel [B,T,M] time-major, f0 [B,T] -> wav [B, T*hop].  rand_ini [dim] / noise
         [B, T*hop, dim] replay the reference's torch.rand / randn_like draws
         (models.py:139,182); None draws them on the device (Philox, `seed` and each row's
-        ``utt_ids``)."""
+        ``utt_ids``).  ``lens``: ragged batch, each row's length in frames (samples past
+        lens[b] * hop are unspecified; the rest equal the utterance run alone)."""
         h = self.handle()
         dev = mel.device
         mel = mel.float().contiguous()
@@ -218,10 +219,12 @@ class Generator(nn.Module):
         nz = None if noise is None else noise.to(dev).float().contiguous()
         wav = torch.empty(B, T * self.upp, device=dev, dtype=torch.float32)
         uid = _lib.utt_ids(utt_ids, B, dev)
+        ln = _lib.lens(lens, B, T, dev)
         L = _lib.lib()
         ws, wsb = self._ws.get(L.nsf_workspace_size(h, B, T), dev)
         _lib.check(L.nsf_forward(h, _lib.fptr(mel), float(mel_scale), _lib.fptr(f0), _lib.fptr(ri), _lib.fptr(nz),
-                                 int(seed), _lib.iptr(uid), _lib.fptr(wav), B, T, ws, wsb, _lib.stream_ptr(dev)))
+                                 int(seed), _lib.iptr(uid), _lib.iptr(ln), _lib.fptr(wav), B, T, ws, wsb,
+                                 _lib.stream_ptr(dev)))
         return wav
 
     def forward(self, x, f0, **kw):

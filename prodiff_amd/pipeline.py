@@ -37,6 +37,14 @@ class Synthesizer:
     def __init__(self, diffusion: GaussianDiffusion, vocoder: FastDiffVocoder):
         self.diffusion = diffusion
         self.vocoder = vocoder
+        self.mel_bins = diffusion.mel_bins
+
+    @staticmethod
+    def collate(conds):
+        """[T_i,H] conditions -> one [B, max T_i, H] batch, zero-padded (a ragged batch: the
+        samplers take each row's length as ``lens``)."""
+        T = max(int(c.shape[0]) for c in conds)
+        return torch.stack([torch.nn.functional.pad(c, (0, 0, 0, T - int(c.shape[0]))) for c in conds])
 
     @classmethod
     def synthetic(cls, device, seed=0, dtype="fp32", **over):
@@ -59,12 +67,14 @@ class Synthesizer:
         return cls(gd, voc)
 
     @torch.no_grad()
-    def __call__(self, cond, seed=None, utt_ids=None):
+    def __call__(self, cond, seed=None, utt_ids=None, lens=None):
         """Random draws are keyed by (seed, utterance id): row i of the batch is utterance
-        ``utt_ids[i]`` (default i), and its output does not depend on the other rows."""
+        ``utt_ids[i]`` (default i), and its output does not depend on the other rows.  ``lens``:
+        a ragged batch (each row's frames, default all T): row i's first lens[i] frames (and
+        lens[i] * hop samples) equal the utterance synthesized alone."""
         g = None if seed is None else 2 * seed
-        mel = self.diffusion.sample(cond, seed=g, utt_ids=utt_ids)
-        wav = self.vocoder.spec2wav_batch(mel, seed=None if seed is None else g + 1, utt_ids=utt_ids)
+        mel = self.diffusion.sample(cond, seed=g, utt_ids=utt_ids, lens=lens)
+        wav = self.vocoder.spec2wav_batch(mel, seed=None if seed is None else g + 1, utt_ids=utt_ids, lens=lens)
         return mel, wav
 
 
@@ -80,6 +90,7 @@ SVS_SAMPLE_RATE = 44100
 SVS_VOCAB = 64
 
 TOKEN_KEYS = ("txt_tokens", "lang_seq")
+FRAME_KEYS = ("mel2ph", "f0", "voicing", "breath")
 
 
 class SvsSynthesizer:
@@ -90,6 +101,7 @@ class SvsSynthesizer:
     def __init__(self, teacher: ProDiffTeacher, generator: NsfGenerator, infer_step=4):
         self.teacher, self.generator, self.infer_step = teacher, generator, infer_step
         self.diffusion = teacher.diffusion
+        self.mel_bins = self.diffusion.mel_bins
 
     @classmethod
     def synthetic(cls, device, seed=0, dtype="fp32", **over):
@@ -113,13 +125,15 @@ class SvsSynthesizer:
 
     @staticmethod
     def collate(items):
-        """Per-utterance dicts -> one batch: token fields padded with 0 (PAD) to the longest,
-        the frame fields (equal length within a batch) stacked; ``ntok`` keeps each
-        utterance's token count."""
-        out = {"ntok": [int(it["txt_tokens"].shape[0]) for it in items]}
+        """Per-utterance dicts -> one batch: token fields padded with 0 (PAD) to the longest, the
+        frame fields (mel2ph, f0, voicing, breath) padded with 0 to the longest segment (mel2ph 0 =
+        a padding frame, prodiff_teacher.py:118-146: a ragged batch, see ``lens``); ``ntok`` keeps
+        each utterance's token count, ``nframes`` its frame count."""
+        out = {"ntok": [int(it["txt_tokens"].shape[0]) for it in items],
+               "nframes": [int(it["mel2ph"].shape[0]) for it in items]}
         for k in items[0]:
             vs = [it[k] for it in items]
-            if k in TOKEN_KEYS:
+            if k in TOKEN_KEYS or k in FRAME_KEYS:
                 n = max(v.shape[0] for v in vs)
                 vs = [torch.nn.functional.pad(v, (0, n - v.shape[0])) for v in vs]
             out[k] = torch.stack(vs)
@@ -132,7 +146,7 @@ class SvsSynthesizer:
         """cond [B,T,H].  Utterances are encoded in groups of equal token count: token padding
         is not neutral in the FFT encoder (the FFN conv reads LayerNorm(0) = beta on padded rows,
         common_layers.py:668-669), and the reference encodes every segment alone (B=1)."""
-        b = {k: v for k, v in batch.items() if k != "ntok"}
+        b = {k: v for k, v in batch.items() if k not in ("ntok", "nframes")}
         ntok = batch.get("ntok") or [int(b["txt_tokens"].shape[1])] * int(b["txt_tokens"].shape[0])
         groups = {}
         for i, n in enumerate(ntok):
@@ -154,12 +168,15 @@ class SvsSynthesizer:
         return cond
 
     @torch.no_grad()
-    def __call__(self, batch, seed=None, utt_ids=None):
+    def __call__(self, batch, seed=None, utt_ids=None, lens=None):
+        """``lens`` (default: the batch's ``nframes``): each segment's frames in a ragged batch."""
         g = None if seed is None else 3 * seed
+        if lens is None:
+            lens = batch.get("nframes")
         cond = self.condition(batch)
-        mel = self.diffusion.sample(cond, infer_step=self.infer_step, seed=g, utt_ids=utt_ids)
+        mel = self.diffusion.sample(cond, infer_step=self.infer_step, seed=g, utt_ids=utt_ids, lens=lens)
         wav = self.generator.synthesize(mel, batch["f0"], LOG10_TO_LN, seed=None if seed is None else g + 1,
-                                        utt_ids=utt_ids)
+                                        utt_ids=utt_ids, lens=lens)
         return mel, wav
 
 
@@ -224,66 +241,104 @@ def gather_to_root(t, root=0, shapes=None, force=False):
     return None
 
 
+def ragged_batches(lengths, idx, max_waste=0.15, max_frames=None):
+    """Batches of utterances `idx` for one rank, as [(T_pad, [indices])] longest first.
+
+    The samplers take ragged batches (``lens``: every conv reads zero past each row's own end, so
+    a padded batch reproduces the reference's one-segment-at-a-time results,
+    handler/infer/handler.py:373-388); padding only costs compute.  Utterances are sorted by
+    length and a batch grows while its padded frames stay within (1 + max_waste) of its real
+    frames (and, if given, its padded frames within max_frames).  Equal lengths give one batch."""
+    order = sorted((int(i) for i in idx), key=lambda i: (-int(lengths[i]), i))
+    out = []
+    for i in order:
+        L = int(lengths[i])
+        if out:
+            T, ids, tot = out[-1]
+            n = len(ids) + 1
+            if T * n <= (1.0 + max_waste) * (tot + L) and (max_frames is None or T * n <= max_frames):
+                ids.append(i)
+                out[-1] = (T, ids, tot + L)
+                continue
+        out.append((L, [i], L))
+    return [(T, ids) for T, ids, _ in out]
+
+
 def length_groups(lengths, idx):
-    """Utterances `idx` grouped by exact length (a batch must share T: the
-    denoiser has no frame mask, so padding would change results near utterance
-    ends).  Returns [(T, [indices])] in descending T."""
+    """Utterances `idx` grouped by exact length, longest first (the dense batches of rounds 1-4;
+    kept for callers that want them -- distributed_synthesize uses ``ragged_batches``)."""
     groups = {}
     for i in idx:
         groups.setdefault(int(lengths[i]), []).append(int(i))
     return sorted(groups.items(), key=lambda kv: -kv[0])
 
 
+def _default_collate(items):
+    T = max(int(c.shape[0]) for c in items)
+    return torch.stack([torch.nn.functional.pad(c, (0, 0, 0, T - int(c.shape[0]))) for c in items])
+
+
 def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None,
-                           collectives=False):
+                           collectives=False, max_waste=0.15):
     """Synthesize utterances sharded over the ranks of the default process group
     (SURVEY §8(e)); the reference runs them one by one, B=1 per segment
     (handler/infer/handler.py:373-388).
 
-    synth_fn(cond [B,T,H], seed, utt_ids) -> (mel [B,T,M], wav [B,T*hop]): one rank's
-      batched synthesis (a ``Synthesizer``; an ``SvsSynthesizer`` takes per-utterance
-      input dicts, batched by its ``collate``).  Every batch gets the same ``seed`` and
-      the global indices of its utterances as ``utt_ids``, and the samplers key their
-      random draws by (seed, utterance id): an utterance's mel and waveform are the same
-      at any world size and in any batch position.
+    synth_fn(cond [B,T,H], seed, utt_ids, lens) -> (mel [B,T,M], wav [B,T*hop]): one rank's
+      batched synthesis (a ``Synthesizer``; an ``SvsSynthesizer`` takes per-utterance input
+      dicts).  Its ``collate`` pads a batch's inputs to the longest (default: zero-pad [T_i,H]
+      conditions), ``lens`` gives each row's frames (a ragged batch), ``mel_bins`` the mel
+      channels.  Every batch gets the same ``seed`` and the global indices of its utterances as
+      ``utt_ids``, and the samplers key their random draws by (seed, utterance id): an
+      utterance's mel and waveform are the same at any world size, in any batch position, and
+      padded or alone.
     conds: list over ALL utterances (same order on every rank) of [T_i,H] tensors
       on this rank's device, or (T_i, callable returning one) pairs, so that only
       this rank's shard is materialized.
-    Utterances are LPT-partitioned by length (``lpt_shards``); each rank runs its
-    shard in equal-length batches, flattens its outputs, and one ragged gather
-    per output kind brings them to the root, which un-permutes them.  The plan is
-    deterministic, so no shape exchange is needed.  Returns on the root the lists
-    [mel_i [T_i,M]], [wav_i [T_i*hop]] in input order; (None, None) elsewhere.
+    Utterances are LPT-partitioned by length (``lpt_shards``); each rank runs its shard in
+    ragged batches of similar lengths (``ragged_batches``, padding <= max_waste), trims each
+    utterance's outputs to its length, and one ragged gather per output kind brings them to the
+    root, which un-permutes them.  The plan is deterministic and the mel channels known
+    (``synth_fn.mel_bins``), so nothing but the outputs crosses ranks.  Returns on the root the
+    lists [mel_i [T_i,M]], [wav_i [T_i*hop]] in input order; (None, None) elsewhere.
     ``stats`` (a dict, optional) receives this rank's ``compute_ms`` (its shard's
     synthesis, device-synchronized) and ``gather_ms`` (the collectives after it).
-    ``collectives=True`` runs the all_reduce and the ragged gathers even at world size 1
-    (otherwise short-circuited), so the N > 1 code path can be exercised on one GPU."""
+    ``collectives=True`` runs the ragged gathers even at world size 1 (otherwise
+    short-circuited), so the N > 1 code path can be exercised on one GPU."""
     import time
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     lengths = [int(c.shape[0]) if torch.is_tensor(c) else int(c[0]) for c in conds]
     shards = lpt_shards(lengths, world)
-    mel_parts, wav_parts, order = [], [], []
-    M = None
-    collate = getattr(synth_fn, "collate", torch.stack)
+    mel_parts, wav_parts = [], []
+    M = getattr(synth_fn, "mel_bins", None)
+    collate = getattr(synth_fn, "collate", _default_collate)
+    plans = [ragged_batches(lengths, s, max_waste) for s in shards]
 
     def sync():
         if stats is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
             torch.cuda.synchronize()
 
     t0 = time.perf_counter()
-    for T, idx in length_groups(lengths, shards[rank]):
+    for T, idx in plans[rank]:
+        lens = [lengths[i] for i in idx]
         cb = collate([conds[i] if torch.is_tensor(conds[i]) else conds[i][1]() for i in idx])
-        mel, wav = synth_fn(cb, seed, utt_ids=idx)
+        if all(n == T for n in lens):
+            mel, wav = synth_fn(cb, seed, utt_ids=idx)
+        else:
+            mel, wav = synth_fn(cb, seed, utt_ids=idx, lens=lens)
         M = mel.shape[-1]
-        mel_parts.append(mel.reshape(-1))
-        wav_parts.append(wav.reshape(-1))
-        order += idx
+        if all(n == T for n in lens):
+            mel_parts.append(mel.reshape(-1))
+            wav_parts.append(wav.reshape(-1))
+        else:
+            for r, n in enumerate(lens):       # trim each row to its utterance
+                mel_parts.append(mel[r, :n].reshape(-1))
+                wav_parts.append(wav[r, :n * hop])
     dev = device
     if dev is None:
         dev = next((c.device for c in conds if torch.is_tensor(c)), torch.device("cpu"))
-    if M is None:     # an empty shard still takes part in the collectives
-        M = 0
+    if not mel_parts:     # an empty shard still takes part in the collectives
         mel_flat = torch.zeros(0, device=dev)
         wav_flat = torch.zeros(0, device=dev)
     else:
@@ -293,10 +348,12 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     if world == 1 and not (collectives and dist.is_initialized()):
         mels_all, wavs_all = [mel_flat], [wav_flat]
     else:
-        # mel bins: known to every rank with a non-empty shard
-        mt = torch.tensor([M], device=mel_flat.device)
-        dist.all_reduce(mt, op=dist.ReduceOp.MAX)
-        M = int(mt.item())
+        if getattr(synth_fn, "mel_bins", None) is None:   # (the same answer on every rank)
+            # a synth_fn without `mel_bins`: every rank with a non-empty shard knows it (one small
+            # all_reduce; the library's synthesizers declare it, so the bench never pays this)
+            mt = torch.tensor([0 if not mel_parts else M], device=mel_flat.device)
+            dist.all_reduce(mt, op=dist.ReduceOp.MAX)
+            M = int(mt.item())
         mel_shapes = [(sum(lengths[i] for i in s) * M,) for s in shards]
         wav_shapes = [(sum(lengths[i] for i in s) * hop,) for s in shards]
         mels_all = gather_to_root(mel_flat, root, mel_shapes, force=collectives)
@@ -308,12 +365,13 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     if rank != root:
         return None, None
     mels, wavs = [None] * len(lengths), [None] * len(lengths)
-    for r, s in enumerate(shards):
+    for r in range(world):
         mo, wo = 0, 0
-        for T, idx in length_groups(lengths, s):
+        for T, idx in plans[r]:
             for i in idx:
-                mels[i] = mels_all[r][mo:mo + T * M].reshape(T, M)
-                wavs[i] = wavs_all[r][wo:wo + T * hop]
-                mo += T * M
-                wo += T * hop
+                n = lengths[i]
+                mels[i] = mels_all[r][mo:mo + n * M].reshape(n, M)
+                wavs[i] = wavs_all[r][wo:wo + n * hop]
+                mo += n * M
+                wo += n * hop
     return mels, wavs

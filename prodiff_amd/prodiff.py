@@ -229,8 +229,13 @@ class GaussianDiffusion(nn.Module):
         return self._coef_cache[1:]
 
     @torch.no_grad()
-    def sample(self, cond, infer_step=4, x_T=None, noise=None, seed=None, workspace=None, utt_ids=None):
+    def sample(self, cond, infer_step=4, x_T=None, noise=None, seed=None, workspace=None, utt_ids=None,
+               lens=None):
         """cond [B,T,H] -> mel [B,T,M].
+
+        lens: ragged batch -- each row's utterance length in frames (B ints <= T, or a device
+        int32 tensor); row b's first lens[b] frames equal a run of that utterance alone (B = 1,
+        T = lens[b]), the frames after it are unspecified (include/prodiff_hip.h).
 
         x_T: [B,1,M,T] draw (reference layout, prodiff.py:147) or None;
         noise: [S,B,1,M,T] per-step draws in sampling order, or None.
@@ -256,12 +261,13 @@ class GaussianDiffusion(nn.Module):
         c1, c2, sg = self._step_scalars()
         mel = torch.empty(B, T, M, device=dev, dtype=torch.float32)
         uid = _lib.utt_ids(utt_ids, B, dev)
+        ln = _lib.lens(lens, B, T, dev)
         L = _lib.lib()
         nbytes = L.pd_wavenet_workspace_size(h, B, T, S)
         ws, wsb = (workspace or self._ws).get(nbytes, dev)
         _lib.check(L.pd_prodiff_sample(h, _lib.fptr(cond), _lib.farr(c1), _lib.farr(c2), _lib.farr(sg), S,
-                                       _lib.fptr(xT), _lib.fptr(nz), seed, _lib.iptr(uid), _lib.fptr(mel), B, T, ws, wsb,
-                                       _lib.stream_ptr(dev)))
+                                       _lib.fptr(xT), _lib.fptr(nz), seed, _lib.iptr(uid), _lib.iptr(ln), _lib.fptr(mel),
+                                       B, T, ws, wsb, _lib.stream_ptr(dev)))
         return mel
 
     @torch.no_grad()

@@ -43,12 +43,12 @@ class RectifiedFlow(nn.Module):
         return _lib.PD_REFLOW.get(self.sampling_algorithm, _lib.PD_REFLOW["euler"])
 
     @torch.no_grad()
-    def sample(self, cond, infer_step=20, x_T=None, seed=None, utt_ids=None):
+    def sample(self, cond, infer_step=20, x_T=None, seed=None, utt_ids=None, lens=None):
         """cond [B,T,H] (time-major, as the teacher hands it) -> x [B,T,M] before denorm_spec.
 
         x_T: [B,1,M,T] draw (reference layout, reflow.py:88) or None -> on-device Philox
         N(0,1) keyed by ``seed`` (default: drawn from torch's CPU generator) and each row's
-        utterance id (``utt_ids``, default 0..B-1)."""
+        utterance id (``utt_ids``, default 0..B-1).  ``lens``: ragged batch (GaussianDiffusion.sample)."""
         if not isinstance(self.velocity_fn, WaveNet):
             raise TypeError("RectifiedFlow needs a prodiff_amd.WaveNet velocity_fn")
         if self.num_features != 1:
@@ -70,8 +70,10 @@ class RectifiedFlow(nn.Module):
         ws, wsb = self._ws.get(nbytes, dev)
         x = torch.empty(B, T, M, device=dev, dtype=torch.float32)
         uid = _lib.utt_ids(utt_ids, B, dev)
+        ln = _lib.lens(lens, B, T, dev)
         _lib.check(L.pd_reflow_sample(h, _lib.fptr(cond), S, algo, float(self.time_scale), _lib.fptr(xT), seed,
-                                      _lib.iptr(uid), _lib.fptr(x), B, T, ws, wsb, _lib.stream_ptr(dev)))
+                                      _lib.iptr(uid), _lib.iptr(ln), _lib.fptr(x), B, T, ws, wsb,
+                                      _lib.stream_ptr(dev)))
         return x
 
     def inference(self, cond, b=1, infer_step=20, device=None):

@@ -111,11 +111,12 @@ class FastDiff(BaseVocoder):
         return self
 
     @torch.no_grad()
-    def spec2wav_batch(self, mel, x_T=None, noise=None, seed=None, utt_ids=None):
-        """mel [B,T,80] on the device -> wav [B, T*hop], one row per utterance."""
+    def spec2wav_batch(self, mel, x_T=None, noise=None, seed=None, utt_ids=None, lens=None):
+        """mel [B,T,80] on the device -> wav [B, T*hop], one row per utterance (``lens``: ragged
+        batch, each row's length in frames; samples past lens[b] * hop are unspecified)."""
         b, a, s, st = self.sched
         return self.model.sample(mel.to(self.device), b, a, s, st, x_T=x_T, noise=noise, seed=seed,
-                                 utt_ids=utt_ids)[:, 0]
+                                 utt_ids=utt_ids, lens=lens)[:, 0]
 
     @torch.no_grad()
     def spec2wav_torch(self, mel, f0=None, x_T=None, noise=None, seed=None, **kwargs):

@@ -36,7 +36,7 @@ def test_null_arguments_fail_loudly():
     lib = _lib.lib()
     rc = lib.pd_wavenet_forward(None, None, None, None, None, 1, 1, None, 0, None)
     assert rc == 1 and b"null" in lib.pd_last_error()
-    assert lib.fd_sample(None, None, None, None, None, None, 4, None, None, 0, None, None, 1, 1, None, 0, None) == 1
+    assert lib.fd_sample(None, None, None, None, None, None, 4, None, None, 0, None, None, None, 1, 1, None, 0, None) == 1
 
 
 def test_wavenet_state_dict_matches_reference_names():

@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from prodiff_amd.pipeline import distributed_synthesize, gather_to_root, length_groups, lpt_shards
+from prodiff_amd.pipeline import distributed_synthesize, gather_to_root, length_groups, lpt_shards, ragged_batches
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HOP = 4          # stub vocoder hop (keeps the test tensors small)
@@ -42,11 +42,27 @@ def test_length_groups_exact():
     assert g == [(7, [3, 4]), (5, [0]), (2, [5])]
 
 
-def stub_synth(cond, seed, utt_ids=None):
+def test_ragged_batches_plan():
+    """Longest first, padding within max_waste of the real frames, every utterance once."""
+    lengths = [504, 522, 539, 720, 1197, 550, 550, 515, 1917, 286, 460, 579]
+    plan = ragged_batches(lengths, range(len(lengths)), max_waste=0.15)
+    assert sorted(i for _, ids in plan for i in ids) == list(range(len(lengths)))
+    for T, ids in plan:
+        assert T == max(lengths[i] for i in ids)
+        assert T * len(ids) <= 1.15 * sum(lengths[i] for i in ids)
+    assert plan[0] == (1917, [8]) and plan[1] == (1197, [4])
+    assert [T for T, _ in plan] == sorted((T for T, _ in plan), reverse=True)
+    # equal lengths: one dense batch; a frame cap splits it
+    assert ragged_batches([861] * 8, range(8)) == [(861, list(range(8)))]
+    assert [len(ids) for _, ids in ragged_batches([861] * 8, range(8), max_frames=861 * 3)] == [3, 3, 2]
+
+
+def stub_synth(cond, seed, utt_ids=None, lens=None):
     """A deterministic stand-in for Synthesizer: per-utterance (independent of the batch
     it runs in), mel [B,T,M], wav [B,T*HOP].  Like the real samplers' draws it depends on
     (seed, utterance id), so the test sees that every batch gets the job's seed and the
-    utterances' GLOBAL indices."""
+    utterances' GLOBAL indices.  A ragged batch's zero padding is neutral (the real samplers
+    read zero past each row's ``lens``)."""
     ids = torch.as_tensor(list(range(cond.shape[0])) if utt_ids is None else utt_ids, dtype=torch.float32)
     mel = cond[..., :M] * 2.0 + 1.0 + 1000.0 * ids[:, None, None] + seed
     wav = torch.repeat_interleave(cond[..., 0], HOP, dim=1) - cond[..., 1].sum(1, keepdim=True)
@@ -87,7 +103,8 @@ def _worker(rank, world, port, q, lengths):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,lengths", [(2, [5, 9, 3, 7, 7, 2]), (3, [4, 11, 6, 6]), (2, [6])])
+@pytest.mark.parametrize("world,lengths", [(2, [5, 9, 3, 7, 7, 2]), (3, [4, 11, 6, 6]), (2, [6]),
+                                          (2, [40, 41, 43, 44, 39, 12, 90])])
 def test_distributed_synthesize_ragged(world, lengths):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -134,7 +151,7 @@ class StubSvs:
     from prodiff_amd.pipeline import SvsSynthesizer as _S
     collate = staticmethod(_S.collate)
 
-    def __call__(self, batch, seed, utt_ids=None):
+    def __call__(self, batch, seed, utt_ids=None, lens=None):
         n = torch.tensor(batch["ntok"], dtype=torch.float32)[:, None]
         tok_sum = batch["txt_tokens"].float().sum(1, keepdim=True)        # pads are 0: neutral
         mel = batch["f0"][..., None].repeat(1, 1, M) + tok_sum[..., None] + n[..., None]
