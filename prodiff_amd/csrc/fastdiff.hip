@@ -1493,8 +1493,19 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 // A lane of C holds 4 consecutive kernel values of one frame; a per-wave LDS transpose turns
 // them into 128-B row segments (8 frames per 1-KiB store: 6.0 TB/s in tools/store_probe.hip).
 constexpr int KP_F = 128, KP_NG = 512, KP_LDH = 200;   // 400-B LDS rows: conflict-free b128 reads
-constexpr int KP_LDO = 72;                             // output transpose rows: 64 + 8 pad (144 B: rows stay
-                                                       // 16-B aligned for the b128 reads; 68 measured 15% slower)
+// Output transpose tile.  KP_SWZ 0 (default): 32 frames x (64 + 8 pad) bf16 rows (144 B: 16-B aligned
+// for the b128 reads; 68 measured 15% slower).  KP_SWZ 1 (r05 A/B): unpadded 128-B rows with an XOR
+// swizzle -- at 256 VGPRs the per-slot addresses spill (51 registers) unless KP_STAGGER is off: 8-B slot s
+// of frame row r lives at slot s ^ kp_swz(r), kp_swz(r) = 2 (r & 7) + ((r >> 3) & 1).  The epilogue's
+// ds_write_b64 (16 lanes = 16 frame rows at one slot) then hits 16 distinct slots -- the 144-B padded
+// rows of r02-r04 put rows r and r + 8 on one bank pair (2-way, the SQ pass's 1.62 conflict cycles per
+// LDS instruction) -- and the store side's ds_read_b128 (16-B chunk c of row r at chunk c ^ (r & 7),
+// halves swapped when (r >> 3) & 1) covers all 64 banks in every lane group.
+#ifndef KP_SWZ
+#define KP_SWZ 0
+#endif
+constexpr int KP_LDO = KP_SWZ ? 64 : 72;
+__device__ __forceinline__ int kp_swz(int r) { return KP_SWZ ? 2 * (r & 7) + ((r >> 3) & 1) : 0; }
 constexpr int KP_NGROUPS = NLY * KPERLAYER / KP_NG;    // 48
 constexpr int KP_THREADS = 512;
 #ifndef KP_STAGGER
@@ -1509,7 +1520,7 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
                                                                        __bf16* __restrict__ Kf, int Tc, int rows,
                                                                        int nfg, const int* __restrict__ lens) {
   __shared__ __attribute__((aligned(16))) __bf16 Hs[2][KP_F * KP_LDH];
-  __shared__ __attribute__((aligned(16))) __bf16 Ot[8][32 * KP_LDO];
+  __shared__ __attribute__((aligned(16))) __bf16 Ot[8][32 * KP_LDO];   // swizzled (kp_swz)
   __shared__ __attribute__((aligned(16))) float Bq[8][64];   // wave-private: its rows' biases
   const int tid = threadIdx.x, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
   // wave-uniform, and provably so: the K-store descriptor is built from it (a descriptor hipcc
@@ -1529,22 +1540,25 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
     hz = 0;
     // the item's first frame split once (wave-uniform); piece frames step forward from it
     const int R0 = fg * KP_F, b0 = R0 / Tc, f00 = R0 - b0 * Tc;
+    // ragged batch: the item's (at most two, when Tc >= KP_F) utterances' own ends -- uniform loads
+    const int tvA = lens ? lens[b0] : Tc, tvB = lens ? lens[min(b0 + 1, rows / Tc - 1)] : Tc;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const int c = tid + KP_THREADS * i, fl = c / 24, v = (c - fl * 24) * 8, tap = v >> 6, ch = v & 63;
       const int R = R0 + fl, Rc = R < rows ? R : rows - 1;
-      int b = b0, f = f00 + (Rc - R0);
+      int b = b0, f = f00 + (Rc - R0), Tv = tvA;
       if (Tc >= KP_F) {                   // (uniform) the item crosses at most one utterance end
         const bool nx = f >= Tc;
         f -= nx ? Tc : 0;
         b += nx ? 1 : 0;
+        Tv = nx ? tvB : tvA;
       } else {
         b = Rc / Tc;
         f = Rc - b * Tc;
+        Tv = lens ? lens[b] : Tc;
       }
       const int ff = f + tap - 1;
       const int ffc = ff < 0 ? 0 : ff >= Tc ? Tc - 1 : ff;     // clamped: unconditional load
-      const int Tv = lens ? lens[b] : Tc;                        // ragged batch: the utterance's own end
       hv[i] = *reinterpret_cast<const uint4*>(hin + ((long long)b * Tc + ffc) * HK + ch);
       hz |= (R >= rows || ff < 0 || ff >= Tc || ff >= Tv) ? 1u << i : 0u;
     }
@@ -1602,12 +1616,13 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
         acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[12 + kk], hb, acc[1], 0, 0, 0);
       }
     };
+    const int swz = kp_swz(r32);
     auto epi = [&](int ft, const f32x16 (&acc)[2]) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + j * 32 + 8 * g + 4 * h]) =
+        for (int g = 0; g < 4; ++g)   // 8-B slot 8j + 2g + h of frame row r32 (swizzled: KP_SWZ)
+          *reinterpret_cast<bf16x4*>(&ot[r32 * KP_LDO + 4 * (KP_SWZ ? (8 * j + 2 * g + h) ^ swz : 8 * j + 2 * g + h)]) =
               bf16x4{(__bf16)acc[j][4 * g], (__bf16)acc[j][4 * g + 1], (__bf16)acc[j][4 * g + 2], (__bf16)acc[j][4 * g + 3]};
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed (wave-private tile)
       __builtin_amdgcn_wave_barrier();
@@ -1615,7 +1630,10 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int fl = i * 8 + (lane >> 3), ch = (lane & 7) * 8;
-        const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + ch]);
+        // chunk (lane & 7) of row fl sits at chunk (lane & 7) ^ (fl & 7), its halves swapped when
+        // (fl >> 3) & 1 = i & 1 (compile-time here)
+        uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * KP_LDO + 8 * (KP_SWZ ? (lane & 7) ^ (lane >> 3) : lane & 7)]);
+        if (KP_SWZ && (i & 1)) v = make_uint4(v.z, v.w, v.x, v.y);
         // 340 MB per launch, read back by the next launch
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_{v.x, v.y, v.z, v.w}, kout,
                                                ((f0 + fl) * KPERLAYER + n0 + ch) * 2, 0, KP_AUX);
@@ -2570,6 +2588,9 @@ const char* fastdiff_build_flags() {
 #endif
 #if KP_AUX != 0
          " KP_AUX"
+#endif
+#if KP_SWZ != 0
+         " KP_SWZ"
 #endif
       ;
 }

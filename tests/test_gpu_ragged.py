@@ -80,7 +80,7 @@ def test_reflow_pitch_ragged_equals_alone(dtype):
     net = WaveNet(M, 256, 20, 256, 5)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in
                          synth.synth_params(synth.wavenet_param_shapes(M, 256, 20, 256), 3).items()})
-    rf = RectifiedFlow(M, net, time_scale=1000).to(DEV)
+    rf = RectifiedFlow(M, net, time_scale=1000, spec_min=[-12], spec_max=[0]).to(DEV)
     net.set_compute_dtype(dtype)
     g = torch.Generator(device=DEV).manual_seed(3)
     conds = [torch.randn(T, 256, device=DEV, generator=g) for T in lengths]
