@@ -104,7 +104,9 @@ void pd_wavenet_destroy(pd_wavenet* h);
  * resident for the n layers; bit-identical to the one-layer kernel), default 10; 0 = one launch
  * per layer. */
 #define PD_WN_OPT_STACK 3
-/* PD_WN_OPT_STACK_RO: output frames per wn_stack_bf16_kernel block, 16..32; 0 (default) = 32. */
+/* PD_WN_OPT_STACK_RO: output frames per wn_stack_bf16_kernel block, 16..48, capped at 64 - 2 max(nl, 8)
+ * (the 64-frame window less a halo of one frame per layer each side); 0 (default) = that cap (44 at
+ * the default 10 layers per launch). */
 #define PD_WN_OPT_STACK_RO 4
 /* 5: reserved (r04's in-kernel split-K reduction by arrival counters, removed: measured slower) */
 /* PD_WN_OPT_STACK_FUSE (bf16 stack path): 1 (default) the input projection runs inside the first
@@ -406,6 +408,12 @@ typedef struct {
   int gender_mix_frames;
   const float* voicing;
   const float* breath;
+  /* Ragged token batch (device, B ints, or NULL = every row T_txt tokens): row b's phonemes are its
+   * first txt_lens[b] tokens.  The FFN conv (k = 9 over tokens) then reads zero past each row's own
+   * end -- the zero padding of the row encoded alone (B = 1, T_txt = txt_lens[b]), the reference's
+   * one-segment-at-a-time inference -- where it would otherwise read the padded rows' LayerNorm(0) =
+   * beta (common_layers.py:668-669).  Attention and LayerNorm already mask padding tokens. */
+  const int* txt_lens;
 } pd_cond_inputs;
 
 /* cond [B,T_mel,H] time-major (what pd_prodiff_sample / pd_reflow_sample take), and optionally

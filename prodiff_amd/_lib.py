@@ -59,7 +59,7 @@ class pd_cond_inputs(C.Structure):
     _fields_ = [("txt_tokens", C.c_void_p), ("mel2ph", C.c_void_p), ("f0", C.c_void_p), ("lang_seq", C.c_void_p),
                 ("spk_embed_id", C.c_void_p), ("spk_mix_embed", C.c_void_p), ("spk_mix_frames", C.c_int),
                 ("gender_embed_id", C.c_void_p), ("gender_mix_embed", C.c_void_p), ("gender_mix_frames", C.c_int),
-                ("voicing", C.c_void_p), ("breath", C.c_void_p)]
+                ("voicing", C.c_void_p), ("breath", C.c_void_p), ("txt_lens", C.c_void_p)]
 
 
 _VP = C.c_void_p
@@ -186,17 +186,27 @@ def _device_rows(vals, B, device, name, lo, hi):
     if t.numel() and (int(t.min()) < lo or int(t.max()) > hi):
         raise HipError(f"{name} must lie in [{lo}, {hi}]")
     key = (name, str(dev), tuple(int(v) for v in t.tolist()))
-    d = _UTT_CACHE.get(key)
+    d = _UTT_CACHE.get(key)   # (device tensor, pinned host source)
     if d is None:
         if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
             raise HipError(f"{name}: host values not seen before cannot be copied to the device during a "
                            "graph capture; pass a device int32 tensor (or call once before capturing)")
         if len(_UTT_CACHE) >= 256:
             _UTT_CACHE.pop(next(iter(_UTT_CACHE)))
-        d = t.to(device=dev, dtype=torch.int32).contiguous()
-        _UTT_CACHE[key] = d
-    elif dev.type == "cuda":
-        d.record_stream(torch.cuda.current_stream(dev))
+        h = t.to(torch.int32).contiguous()
+        if dev.type == "cuda":
+            # pinned source + non_blocking: a pageable copy would block the host until the stream
+            # drains (no queuing ahead, no overlap of batches on other streams); the pinned host
+            # buffer lives in the cache entry, so it outlives the copy
+            h = h.pin_memory()
+            d = h.to(device=dev, non_blocking=True)
+        else:
+            d = h
+        _UTT_CACHE[key] = (d, h)
+    else:
+        d = d[0]
+        if dev.type == "cuda":
+            d.record_stream(torch.cuda.current_stream(dev))
     return d
 
 
@@ -277,13 +287,21 @@ def profile_summary():
 
 
 class Workspace:
-    """Grow-only device scratch buffer (torch caching allocator)."""
+    """Grow-only device scratch buffers (torch caching allocator), one per (device, stream): the
+    library's calls are stream-ordered, so calls on different streams -- distributed_synthesize
+    runs ragged batches side by side -- must not share scratch (include/prodiff_hip.h: "concurrent
+    calls on different streams need separate workspaces")."""
 
     def __init__(self):
-        self.buf = None
+        self.bufs = {}
 
     def get(self, nbytes, device):
         import torch
-        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
-            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
-        return C.c_void_p(self.buf.data_ptr()), self.buf.numel()
+        device = torch.device(device)
+        sid = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
+        key = (str(device), sid)
+        buf = self.bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self.bufs[key] = buf
+        return C.c_void_p(buf.data_ptr()), buf.numel()

@@ -606,6 +606,7 @@ int pd_cond_forward(const pd_cond* h, const pd_cond_inputs* in, float* cond, flo
     {   // f = gelu(k^-0.5 (conv_k(hn) + b1))   (TransformerFFNLayer, common_layers.py:570-576)
       GemmArgs a = make_gemm(B, T_txt, F, h->W1[l], K * H, h->b1[l], ff, bs * F, F);
       for (int tap = 0; tap < K; ++tap) add_seg(a, make_seg(hn, bs * H, H, H, tap - K / 2));
+      a.lens = in->txt_lens; a.lens_mul = 1;   // ragged token batch: zero past each row's own tokens
       a.act = ACT_GELU;
       a.alpha = (float)std::pow((double)K, -0.5);
       PD_TRY((enc_gemm<EPI_STORE, U_ENC_FFN1>(a, part, st, "enc_ffn1")));

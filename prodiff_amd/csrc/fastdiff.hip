@@ -470,7 +470,10 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
   // SUB (hop 8) stages the pre-conv weights too (WW): a global load per layer made every layer
   // start with an L2 round trip; its LVC biases stay per-frame global reads.
   constexpr bool WL = PF, WW = PF || SUB;
-  constexpr int BFR = WL ? GR / 32 + 2 : 1;          // frames a block touches at hop >= 32
+  // frames a block touches: its GR rows span at most GR / hop + 2 frames, and PF (= WL) launches
+  // have hop % 64 == 0 (r05: sized for hop >= 32 before, 18 frames -- 8 more than any PF launch reads,
+  // 8 KB of LDS and two float4 loads per thread in every block's prologue)
+  constexpr int BFR = WL ? GR / 64 + 2 : 1;
   __shared__ __attribute__((aligned(16))) bf16x8 WCL[WW ? NLY * 6 * 64 : 1];
   __shared__ __attribute__((aligned(16))) float BCL[WW ? NLY * CI : 4];
   __shared__ __attribute__((aligned(16))) float BFL[WL ? BFR * 2 * CI * NLY : 4];
@@ -1509,7 +1512,7 @@ __device__ __forceinline__ int kp_swz(int r) { return KP_SWZ ? 2 * (r & 7) + ((r
 constexpr int KP_NGROUPS = NLY * KPERLAYER / KP_NG;    // 48
 constexpr int KP_THREADS = 512;
 #ifndef KP_STAGGER
-#define KP_STAGGER 1
+#define KP_STAGGER 0   // r05 same-box ABAB: off 5.68 vs on 5.72-5.76 ms/step, kp 103 vs 107 us (profiles/r05_ab/kp_stagger_swz_ab.txt)
 #endif
 #ifndef KP_AUX
 #define KP_AUX 0   // plain K stores: the lines stay on-die for the LVC block that reads them next (r03 A/B: non-temporal (2) made kp ~4% and the next LVC launch ~4% slower)
@@ -2583,7 +2586,7 @@ const char* fastdiff_build_flags() {
 #if DB_WPE != 5
          " DB_WPE"
 #endif
-#if KP_STAGGER != 1
+#if KP_STAGGER != 0
          " KP_STAGGER"
 #endif
 #if KP_AUX != 0

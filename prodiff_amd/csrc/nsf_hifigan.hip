@@ -513,12 +513,19 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
 // Waves: column tile ct = wave % NCT (NCT = C / 32) of both convs; with NCT = 2 the row tiles are
 // split between two wave pairs by parity, with NCT = 1 (C = 32, r04) between all four waves (FMO = 15:
 // 16 c1 row tiles and 15 c2 row tiles over 4 waves).
-template <int C, int FMO>
+// TAPS / DIL > 0 (r05): the ResBlock's kernel size and c1's dilation as compile-time constants --
+// every LDS / weight address of the fully unrolled tap loops folds into an immediate offset (the
+// runtime-taps build spent ~60 VALU instructions per MFMA at C = 32, mostly address arithmetic,
+// and ran VALU-bound: 0.90 VALU busy, profiles/r04_final/c5_sq.json).  0 = runtime (other shapes).
+template <int C, int FMO, int TAPS = 0, int DIL = 0>
 __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restrict__ x, const __bf16* __restrict__ w1,
-                                                      const __bf16* __restrict__ w2, int ldw, int kpad,
+                                                      const __bf16* __restrict__ w2, int ldw_, int kpad_,
                                                       const float* __restrict__ b1, const float* __restrict__ b2,
-                                                      int taps, int dil, int Tl, float* __restrict__ out, int accum,
+                                                      int taps_, int dil_, int Tl, float* __restrict__ out, int accum,
                                                       NsfRag rag_) {
+  // (compile-time shapes: the packed weights' K chunk is C, the host checks kpad == C)
+  const int taps = TAPS ? TAPS : taps_, dil = DIL ? DIL : dil_;
+  const int kpad = TAPS ? C : kpad_, ldw = TAPS ? TAPS * C : ldw_;
   constexpr int NCT = C / 32, RG = 4 / NCT, LDA = C + 8, KS = C / 16;
   constexpr int TM = 32 * FMO, RT1 = FMO + 1;            // output rows; c1 row tiles
   constexpr int MF1 = (RT1 + RG - 1) / RG, MF2 = (FMO + RG - 1) / RG;   // row tiles per wave
@@ -556,6 +563,7 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
     };
 #pragma unroll
     for (int q = 0; q < PF - 1; ++q) bq[q] = bload(q);
+#pragma unroll
     for (int s0 = 0; s0 < S; s0 += PF) {
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
@@ -606,6 +614,7 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
     };
 #pragma unroll
     for (int q = 0; q < PF - 1; ++q) bq[q] = bload(q);
+#pragma unroll
     for (int s0 = 0; s0 < S; s0 += PF) {
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
@@ -651,20 +660,36 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
 #ifndef NSF_PAIR_FMO64
 #define NSF_PAIR_FMO64 8   // C = 64 output row tiles per block (r04: 4 -> 8, C5 -4%)
 #endif
-template <int C>
-int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
-                  hipStream_t st, NsfRag rag_) {
+template <int C, int TAPS, int DIL>
+int launch_pair_ct(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
+                   hipStream_t st, NsfRag rag_) {
   constexpr int FMO = C == 32 ? NSF_PAIR_FMO32 : C == 64 ? NSF_PAIR_FMO64 : 4, TM = 32 * FMO;
   // x / xt window + stage_window's spare row
   const size_t lds = (size_t)(32 * (FMO + 1) + (c1.taps - 1) * c1.dil + 1) * (C + 8) * sizeof(__bf16);
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&nsf_pair_kernel<C, FMO>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&nsf_pair_kernel<C, FMO, TAPS, DIL>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      160 * 1024);
   if (attr != hipSuccess) { set_error("nsf pair: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
   ProfScope ps("nsf_pair", st);
-  hipLaunchKernelGGL((nsf_pair_kernel<C, FMO>), dim3(cdiv(Tl, TM), 1, B), dim3(256), lds, st, x, lookup_bf16(c1.w),
-                     lookup_bf16(c2.w), c1.taps * c1.kpad, c1.kpad, c1.b, c2.b, c1.taps, c1.dil, Tl, out, accum, rag_);
+  hipLaunchKernelGGL((nsf_pair_kernel<C, FMO, TAPS, DIL>), dim3(cdiv(Tl, TM), 1, B), dim3(256), lds, st, x,
+                     lookup_bf16(c1.w), lookup_bf16(c2.w), c1.taps * c1.kpad, c1.kpad, c1.b, c2.b, c1.taps, c1.dil, Tl,
+                     out, accum, rag_);
   PD_LAUNCH_CHECK();
   return PD_OK;
+}
+
+// compile-time (taps, dilation) for the shipped ResBlock1 shapes (kernel sizes 3, 7, 11 x dilations
+// 1, 3, 5; handler/base_config.yaml), the runtime kernel otherwise
+template <int C>
+int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
+                  hipStream_t st, NsfRag rag_) {
+#define PD_PAIR_CASE(K, D) \
+  if (c1.taps == K && c1.dil == D && c1.kpad == C) return launch_pair_ct<C, K, D>(c1, c2, x, B, Tl, out, accum, st, rag_)
+  PD_PAIR_CASE(3, 1); PD_PAIR_CASE(3, 3); PD_PAIR_CASE(3, 5);
+  PD_PAIR_CASE(7, 1); PD_PAIR_CASE(7, 3); PD_PAIR_CASE(7, 5);
+  PD_PAIR_CASE(11, 1); PD_PAIR_CASE(11, 3); PD_PAIR_CASE(11, 5);
+#undef PD_PAIR_CASE
+  return launch_pair_ct<C, 0, 0>(c1, c2, x, B, Tl, out, accum, st, rag_);
 }
 
 bool wconv_ok(const NsfConv& c);
@@ -694,13 +719,15 @@ int launch_pair(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int
 // fragments), loaded once.  Block = 4 waves x 64 rows (4 M fragments of 16) = 256 rows.
 // MFMA 16x16x32 layouts: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15],
 // D[row 4(l>>4)+r][col l&15].
-template <bool IN_BF, bool OUT_BF>
+// TAPS / DIL > 0 (r05): compile-time kernel size and dilation (see nsf_pair_kernel); kpad is then 32.
+template <bool IN_BF, bool OUT_BF, int TAPS = 0, int DIL = 0>
 __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
-                                                          int kpad, const float* __restrict__ bias, int taps, int dil,
-                                                          float alpha, float scale, int Tl,
+                                                          int kpad_, const float* __restrict__ bias, int taps_,
+                                                          int dil_, float alpha, float scale, int Tl,
                                                           const float* __restrict__ res, void* __restrict__ out,
                                                           int accum, NsfRag rag_) {
   constexpr int C = 16, TM = 256, LDA = 24, MAXP = 6;
+  const int taps = TAPS ? TAPS : taps_, dil = DIL ? DIL : dil_, kpad = TAPS ? 32 : kpad_;
   extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win16[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.y, t0 = blockIdx.x * TM;
@@ -778,14 +805,30 @@ int launch_wconv16(const NsfConv& c, const __bf16* wb, const void* in, bool in_b
   const size_t lds = (size_t)(256 + (c.taps - 1) * c.dil + 1) * 24 * sizeof(__bf16);   // + stage_window's spare row
   dim3 grid(cdiv(Tl, 256), B);
   ProfScope ps("nsf_res_small", st);
-#define PD_WCONV16(IB, OB)                                                                                      \
-  hipLaunchKernelGGL((nsf_wconv16_kernel<IB, OB>), grid, dim3(256), lds, st, in, wb, c.kpad, c.b, c.taps, c.dil, \
-                     alpha, scale, Tl, res, out, accum, rag_)
+#define PD_WCONV16T(IB, OB, K, D)                                                                                 \
+  hipLaunchKernelGGL((nsf_wconv16_kernel<IB, OB, K, D>), grid, dim3(256), lds, st, in, wb, c.kpad, c.b, c.taps,   \
+                     c.dil, alpha, scale, Tl, res, out, accum, rag_)
+  // compile-time (taps, dilation) for the shipped ResBlock shapes, the runtime kernel otherwise
+#define PD_WCONV16(IB, OB)                                                                                        \
+  do {                                                                                                            \
+    const int K_ = c.kpad == 32 ? c.taps : 0, D_ = c.dil;                                                         \
+    if (K_ == 3 && D_ == 1) PD_WCONV16T(IB, OB, 3, 1);                                                            \
+    else if (K_ == 3 && D_ == 3) PD_WCONV16T(IB, OB, 3, 3);                                                       \
+    else if (K_ == 3 && D_ == 5) PD_WCONV16T(IB, OB, 3, 5);                                                       \
+    else if (K_ == 7 && D_ == 1) PD_WCONV16T(IB, OB, 7, 1);                                                       \
+    else if (K_ == 7 && D_ == 3) PD_WCONV16T(IB, OB, 7, 3);                                                       \
+    else if (K_ == 7 && D_ == 5) PD_WCONV16T(IB, OB, 7, 5);                                                       \
+    else if (K_ == 11 && D_ == 1) PD_WCONV16T(IB, OB, 11, 1);                                                     \
+    else if (K_ == 11 && D_ == 3) PD_WCONV16T(IB, OB, 11, 3);                                                     \
+    else if (K_ == 11 && D_ == 5) PD_WCONV16T(IB, OB, 11, 5);                                                     \
+    else PD_WCONV16T(IB, OB, 0, 0);                                                                               \
+  } while (0)
   if (in_bf && out_bf) PD_WCONV16(true, true);
   else if (in_bf) PD_WCONV16(true, false);
   else if (out_bf) PD_WCONV16(false, true);
   else PD_WCONV16(false, false);
 #undef PD_WCONV16
+#undef PD_WCONV16T
   PD_LAUNCH_CHECK();
   return PD_OK;
 }

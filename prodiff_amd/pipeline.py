@@ -13,6 +13,8 @@ rank (``gather_to_root``, RCCL over xGMI under the ``nccl`` backend).
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -38,6 +40,12 @@ class Synthesizer:
         self.diffusion = diffusion
         self.vocoder = vocoder
         self.mel_bins = diffusion.mel_bins
+
+    def prepare(self):
+        """Pack every handle now (stream-ordered packing must finish before batches run on other
+        streams: distributed_synthesize calls this, then synchronizes)."""
+        self.diffusion.denoise_fn.handle()
+        self.vocoder.model.handle()
 
     @staticmethod
     def collate(conds):
@@ -103,6 +111,12 @@ class SvsSynthesizer:
         self.diffusion = teacher.diffusion
         self.mel_bins = self.diffusion.mel_bins
 
+    def prepare(self):
+        """Pack every handle now (see Synthesizer.prepare)."""
+        self.teacher.cond_handle()
+        self.diffusion.denoise_fn.handle()
+        self.generator.handle()
+
     @classmethod
     def synthetic(cls, device, seed=0, dtype="fp32", **over):
         hp = dict(SVS_TEACHER, **over)
@@ -143,29 +157,21 @@ class SvsSynthesizer:
 
     @torch.no_grad()
     def condition(self, batch):
-        """cond [B,T,H].  Utterances are encoded in groups of equal token count: token padding
-        is not neutral in the FFT encoder (the FFN conv reads LayerNorm(0) = beta on padded rows,
-        common_layers.py:668-669), and the reference encodes every segment alone (B=1)."""
+        """cond [B,T,H] in one encoder pass over the token-padded batch.  Token padding is not
+        neutral in the reference's batched FFT encoder (its FFN conv reads LayerNorm(0) = beta on
+        padded rows, common_layers.py:668-669) and the reference encodes every segment alone
+        (B=1), so each row's phoneme count goes to the encoder as ``txt_lens``: the FFN conv reads
+        zero past it and every row equals its segment encoded alone (r05; rounds 2-4 ran one
+        encoder pass per distinct phoneme count)."""
         b = {k: v for k, v in batch.items() if k not in ("ntok", "nframes")}
-        ntok = batch.get("ntok") or [int(b["txt_tokens"].shape[1])] * int(b["txt_tokens"].shape[0])
-        groups = {}
-        for i, n in enumerate(ntok):
-            groups.setdefault(n, []).append(i)
-        if len(groups) == 1:
-            return self.teacher.forward_condition(b.pop("txt_tokens")[:, :ntok[0]], b.pop("mel2ph"), b.pop("f0"),
-                                                  lang_seq=None if "lang_seq" not in b else b.pop("lang_seq")[:, :ntok[0]],
-                                                  **b)
-        cond = None
-        for n, idx in groups.items():
-            ix = torch.tensor(idx, device=b["txt_tokens"].device)
-            sub = {k: v.index_select(0, ix) for k, v in b.items()}
-            if "lang_seq" in sub:
-                sub["lang_seq"] = sub["lang_seq"][:, :n]
-            c = self.teacher.forward_condition(sub.pop("txt_tokens")[:, :n], sub.pop("mel2ph"), sub.pop("f0"), **sub)
-            if cond is None:
-                cond = c.new_empty((b["txt_tokens"].shape[0],) + tuple(c.shape[1:]))
-            cond.index_copy_(0, ix, c)
-        return cond
+        B, Tt = int(b["txt_tokens"].shape[0]), int(b["txt_tokens"].shape[1])
+        ntok = batch.get("ntok") or [Tt] * B
+        n = max(ntok)
+        tok = b.pop("txt_tokens")[:, :n]
+        if "lang_seq" in b:
+            b["lang_seq"] = b["lang_seq"][:, :n]
+        return self.teacher.forward_condition(tok, b.pop("mel2ph"), b.pop("f0"),
+                                              txt_lens=None if all(k == n for k in ntok) else ntok, **b)
 
     @torch.no_grad()
     def __call__(self, batch, seed=None, utt_ids=None, lens=None):
@@ -279,7 +285,7 @@ def _default_collate(items):
 
 
 def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None,
-                           collectives=False, max_waste=0.15):
+                           collectives=False, max_waste=0.15, streams=4):
     """Synthesize utterances sharded over the ranks of the default process group
     (SURVEY §8(e)); the reference runs them one by one, B=1 per segment
     (handler/infer/handler.py:373-388).
@@ -304,7 +310,11 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     ``stats`` (a dict, optional) receives this rank's ``compute_ms`` (its shard's
     synthesis, device-synchronized) and ``gather_ms`` (the collectives after it).
     ``collectives=True`` runs the ragged gathers even at world size 1 (otherwise
-    short-circuited), so the N > 1 code path can be exercised on one GPU."""
+    short-circuited), so the N > 1 code path can be exercised on one GPU.
+    ``streams``: a shard of several ragged batches runs them side by side on up to this many HIP
+    streams (each with its own workspaces, ``_lib.Workspace``): a long utterance alone in its batch
+    fills a fraction of the GPU (the WaveNet stack puts 32 frames on a CU), so it overlaps the
+    others instead of running after them.  1 = one after the other on the current stream."""
     import time
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -319,14 +329,39 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         if stats is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
             torch.cuda.synchronize()
 
+    dev = device
+    if dev is None:
+        dev = next((c.device for c in conds if torch.is_tensor(c)), torch.device("cpu"))
+    dev = torch.device(dev)
+    plan = plans[rank]
+    side = None
+    if streams > 1 and len(plan) > 1 and dev.type == "cuda":
+        if getattr(synth_fn, "prepare", None):
+            synth_fn.prepare()
+        cur = torch.cuda.current_stream(dev)
+        side = [torch.cuda.Stream(dev) for _ in range(min(streams, len(plan)))]
+        for s in side:
+            s.wait_stream(cur)          # the inputs and the packed handles are ready
+
     t0 = time.perf_counter()
-    for T, idx in plans[rank]:
+    outs = []
+    for k, (T, idx) in enumerate(plan):
         lens = [lengths[i] for i in idx]
-        cb = collate([conds[i] if torch.is_tensor(conds[i]) else conds[i][1]() for i in idx])
-        if all(n == T for n in lens):
-            mel, wav = synth_fn(cb, seed, utt_ids=idx)
-        else:
-            mel, wav = synth_fn(cb, seed, utt_ids=idx, lens=lens)
+        ctx = torch.cuda.stream(side[k % len(side)]) if side else contextlib.nullcontext()
+        with ctx:
+            cb = collate([conds[i] if torch.is_tensor(conds[i]) else conds[i][1]() for i in idx])
+            if all(n == T for n in lens):
+                mel, wav = synth_fn(cb, seed, utt_ids=idx)
+            else:
+                mel, wav = synth_fn(cb, seed, utt_ids=idx, lens=lens)
+        outs.append((mel, wav, lens, T))
+    if side:
+        for s in side:
+            cur.wait_stream(s)
+        for mel, wav, _, _ in outs:     # made on a side stream, read (and freed) on the current one
+            mel.record_stream(cur)
+            wav.record_stream(cur)
+    for mel, wav, lens, T in outs:
         M = mel.shape[-1]
         if all(n == T for n in lens):
             mel_parts.append(mel.reshape(-1))
@@ -335,9 +370,6 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
             for r, n in enumerate(lens):       # trim each row to its utterance
                 mel_parts.append(mel[r, :n].reshape(-1))
                 wav_parts.append(wav[r, :n * hop])
-    dev = device
-    if dev is None:
-        dev = next((c.device for c in conds if torch.is_tensor(c)), torch.device("cpu"))
     if not mel_parts:     # an empty shard still takes part in the collectives
         mel_flat = torch.zeros(0, device=dev)
         wav_flat = torch.zeros(0, device=dev)

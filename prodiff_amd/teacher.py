@@ -245,9 +245,11 @@ class ProDiffTeacher(nn.Module):
     @torch.no_grad()
     def forward_condition(self, txt_tokens, mel2ph, f0, lang_seq=None, spk_embed_id=None, spk_mix_embed=None,
                           gender_embed_id=None, gender_mix_embed=None, voicing=None, breath=None,
-                          return_encoder=False):
+                          return_encoder=False, txt_lens=None):
         """prodiff_teacher.py:103-146 -> condition [B, T_mel, H].  ``return_encoder`` (not in the
-        reference) also returns the FastspeechEncoder output [B, T_txt, H]."""
+        reference) also returns the FastspeechEncoder output [B, T_txt, H].  ``txt_lens`` (not in the
+        reference): each row's phoneme count in a token-padded batch -- every row then equals the
+        segment encoded alone (pd_cond_inputs.txt_lens)."""
         if self.with_lang_embed and lang_seq is None:
             raise AssertionError("use_lang_embed is True, lang_seq is required")
         if self.with_spk_embed and spk_embed_id is None and spk_mix_embed is None:
@@ -269,11 +271,12 @@ class ProDiffTeacher(nn.Module):
         smix = None if spk_mix_embed is None else flt(spk_mix_embed.reshape(B, -1, H))
         gmix = None if gender_mix_embed is None else flt(gender_mix_embed.reshape(B, -1, H))
         f0_, vo, br = flt(f0), flt(voicing), flt(breath)
-        keep = (tok, m2p, lang, spk_id, gen_id, smix, gmix, f0_, vo, br)
+        tl = _lib.lens(txt_lens, B, Tt, dev)
+        keep = (tok, m2p, lang, spk_id, gen_id, smix, gmix, f0_, vo, br, tl)
         vp = lambda t: None if t is None else t.data_ptr()
         ins = _lib.pd_cond_inputs(vp(tok), vp(m2p), vp(f0_), vp(lang), vp(spk_id), vp(smix),
                                   0 if smix is None else smix.shape[1], vp(gen_id), vp(gmix),
-                                  0 if gmix is None else gmix.shape[1], vp(vo), vp(br))
+                                  0 if gmix is None else gmix.shape[1], vp(vo), vp(br), vp(tl))
         cond = torch.empty(B, Tm, H, device=dev, dtype=torch.float32)
         enc = torch.empty(B, Tt, H, device=dev, dtype=torch.float32) if return_encoder else None
         L = _lib.lib()

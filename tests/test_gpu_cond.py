@@ -108,9 +108,11 @@ def test_teacher_forward_infer_end_to_end():
 
 
 def test_svs_synthesizer_ragged_tokens_and_pipeline():
-    """SvsSynthesizer (bench C5): a batch with different phoneme counts encodes each group
-    exactly as alone (B=1, the reference handler's way); the whole path returns finite
-    mel [B,T,128] and wav [B,T*512]; distributed_synthesize un-permutes it."""
+    """SvsSynthesizer (bench C5): a batch with different phoneme counts, encoded in ONE padded
+    pass with each row's phoneme count as txt_lens, equals every segment encoded alone (B=1, the
+    reference handler's way) within 1e-5 * max (the split-K choice of the small GEMMs depends on
+    the row count); the whole path returns finite mel [B,T,128] and wav [B,T*512];
+    distributed_synthesize un-permutes it."""
     from prodiff_amd import synth
     from prodiff_amd.pipeline import SVS_VOCAB, SvsSynthesizer, distributed_synthesize
     syn = SvsSynthesizer.synthetic(torch.device("cuda"), seed=0, dtype="fp32", residual_layers=2)
@@ -121,7 +123,8 @@ def test_svs_synthesizer_ragged_tokens_and_pipeline():
     cond = syn.condition(batch)
     for i, u in enumerate(utts):
         alone = syn.condition(SvsSynthesizer.collate([u]))
-        assert torch.equal(cond[i], alone[0]), i
+        err = float((cond[i] - alone[0]).abs().max())
+        assert err <= 1e-5 * float(alone[0].abs().max()), (i, err)
     mel, wav = syn(batch, seed=5)
     assert mel.shape == (3, T, 128) and wav.shape == (3, T * 512)
     assert torch.isfinite(mel).all() and torch.isfinite(wav).all() and wav.abs().max() <= 1.0

@@ -33,8 +33,8 @@ for part in "$@"; do
   key=${part%%=*}; val=${part#*=}; [ "$val" = "$part" ] && val=""
   case $key in
     tests)
-      K=""; [ -n "$val" ] && K="-k $val"
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K \
+      K=(); [ -n "$val" ] && K=(-k "$val")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
         > $O/gpu_tests.log 2>&1
       tail -2 $O/gpu_tests.log ;;
     bench)
