@@ -40,7 +40,7 @@ struct pd_wavenet {
   // 0 = off.  r04 (C3, same box): 10 layers per launch 20.7-21.0 us per layer vs 25.7-26.6 for the
   // one-layer kernel; 7 layers 20.3 us (profiles/r04_ab/wn_stack_ab.txt)
   int stack_nl = 10;
-  int stack_ro = 0;          // PD_WN_OPT_STACK_RO: output rows per stack block (0 = auto, else 16..32)
+  int stack_ro = 0;          // PD_WN_OPT_STACK_RO: output rows per stack block (0 = auto: 64 - 2 max(nl, 8); else 16..48, capped there)
   int stack_fuse = 1;        // PD_WN_OPT_STACK_FUSE: input projection / sampler output stage inside the stack launches
   int f32_layer = 1;         // PD_WN_OPT_F32_LAYER: fp32 layers on wn_f32_layer_kernel (0 off, 1 where K would split, 2 always)
 };
@@ -316,10 +316,12 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
 
 // ------------------------------------------------------------------ residual stack, several layers per launch (bf16)
 // Consecutive residual layers [l0, l0 + nl) of wavenet.py:115-119 in ONE launch, for dilation 1
-// (dilation_cycle_length = 1, handler/base_config.yaml).  Block = 32 output rows of the flattened
-// [B*T] batch, holding a 64-row window [R0 - 16, R0 + 48) for all nl layers: x (fp32) in registers
-// in the GEMM2 C layout, bf16(x + dp_l) and bf16(cond) in LDS.  A layer's conv reads rows t +- 1,
-// so the window's outer rows go stale one row per layer; with nl <= 16 the output rows stay exact.
+// (dilation_cycle_length = 1, handler/base_config.yaml).  Block = ro output rows of the flattened
+// [B*T] batch, holding a 64-row window [R0 - hl, R0 - hl + 64) for all nl layers: x (fp32) in
+// registers in the GEMM2 C layout, bf16(x + dp_l) and bf16(cond) in LDS.  A layer's conv reads rows
+// t +- 1, so the window's outer rows go stale one row per layer: after nl layers window rows
+// [nl, 64 - nl) are exact, so the host sets hl = max(nl, 8) and ro <= 64 - 2 hl (44 at nl = 10;
+// r04 wrote 32 rows per window at any nl, i.e. 27% more blocks streaming the same weights).
 // Every layer streams its 1.3 MB of fragment-ordered weights through the same register rings as
 // wn_layer_bf16_kernel (the L2 -> CU weight stream, ~12 us per layer and block, is this design's
 // floor), but the staging, the x / skip HBM round trip and the launch happen once per nl layers.
@@ -337,7 +339,7 @@ struct WnStackArgs {
   const float* b2;        // [L][2C]
   int rows, T, l0, nl, first, L;
   const int* lens;        // frames of each row's utterance (null: T): the conv's zero padding starts there
-  int ro;                 // output rows per block (<= 32): window rows [16, 16 + ro)
+  int ro, hl;             // output rows per block: window rows [hl, hl + ro) (8 <= hl, hl + ro <= 56)
   // PD_WN_OPT_STACK_FUSE, first launch: x = relu(W_in spec + b_in) of the window rows computed
   // here (spec [rows][M] fp32, Winb [C][ldw_in] bf16, M <= ldw_in <= 128) instead of read
   const float* spec;
@@ -375,10 +377,10 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   __shared__ __attribute__((aligned(16))) __bf16 XW[WR * WST_LD];   // bf16(x + dp_l)
   __shared__ __attribute__((aligned(16))) __bf16 CW[WR * WST_LD];   // bf16(cond)
   __shared__ __attribute__((aligned(16))) __bf16 Gs[WR * WST_LD];   // gated g
-  __shared__ float SK[32 * WNF_C];                                   // skip sum of the output rows (lane-private entries)
+  __shared__ float SK[48 * WNF_C];                                   // skip sums of window rows [8, 56) (lane-private entries)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int rows = P.rows, T = P.T;
-  const int R0 = blockIdx.x * P.ro, W0 = R0 - 16;    // window row 0
+  const int R0 = blockIdx.x * P.ro, HL = P.hl, W0 = R0 - HL;   // window row 0
   const int n = wave * 32 + r32;                     // this lane's residual / skip column
   // T >= 64 (the host's condition) puts at most two utterances, bA and bB, in the window
   const int bA = min(max(W0, 0), rows - 1) / T, RB = (bA + 1) * T;   // rows >= RB: utterance bB
@@ -421,9 +423,9 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
     *reinterpret_cast<uint4*>(&CW[wr * WST_LD + c]) = make_uint4(v.x & mk, v.y & mk, v.z & mk, v.w & mk);
   }
   // x (fp32) of the lane's 32 window rows, column n, in registers (the GEMM2 C layout: tile q,
-  // register reg -> window row 32 q + (reg & 3) + 8 (reg >> 2) + 4 h); the skip sum of its 16
-  // output rows (tile 0 regs 8..15 = window rows 16..31, tile 1 regs 0..7 = window rows 32..47)
-  // in LDS, entries only this lane touches
+  // register reg -> window row 32 q + (reg & 3) + 8 (reg >> 2) + 4 h); the skip sums of its 24
+  // rows in [8, 56) (tile 0 regs 4..15 = window rows 8..31, tile 1 regs 0..11 = window rows 32..55),
+  // a superset of the output rows, in LDS, entries only this lane touches
   float xr[2][16];
   if constexpr (IN) {
     // x = relu(W_in . bf16(spec) + b_in): the GEMM engine's k order (ldw_in / 16 k-steps)
@@ -461,10 +463,10 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
       }
     }
   }
-  auto sko = [&](int i) {   // SK index of output value i
-    const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
-    return (32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h - 16) * C + n;
-  };
+  auto skq = [](int i) { return i < 12 ? 0 : 1; };          // SK value i: tile, register
+  auto skr = [](int i) { return i < 12 ? 4 + i : i - 12; };
+  auto skw = [&](int i) { const int reg = skr(i); return 32 * skq(i) + (reg & 3) + 8 * (reg >> 2) + 4 * h; };
+  auto sko = [&](int i) { return (skw(i) - 8) * C + n; };
   if constexpr (!IN) {
 #pragma unroll
     for (int q = 0; q < 2; ++q)
@@ -475,22 +477,33 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
       }
   }
   {   // (unconditional loads, the first launch's zero by a bit mask: see the cond staging above).
-      // Only this block's output rows [R0, R0 + ro) are read: with ro < 32 the window's rows past
-      // them belong to the next block, which writes them in this launch -- their loads are clamped
-      // to the block's last row and the values masked to zero (they are never stored anyway)
+      // Only this block's output rows [R0, R0 + ro) are read: the window's rows either side of
+      // them belong to the neighbouring blocks, which write them in this launch -- their loads are
+      // clamped into the block's rows and the values masked to zero (they are never stored anyway)
     const unsigned mk = P.first ? 0u : 0xffffffffu;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
-      const int wrow = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + wrow;
-      const unsigned mo = wrow - 16 < P.ro ? mk : 0u;
-      const float sv = P.skip[(long long)min(max(min(R, R0 + P.ro - 1), 0), rows - 1) * C + n];
+    for (int i = 0; i < 24; ++i) {
+      const int wrow = skw(i), R = W0 + wrow;
+      const unsigned mo = (wrow >= HL && wrow - HL < P.ro) ? mk : 0u;
+      const float sv = P.skip[(long long)min(max(min(max(R, R0), R0 + P.ro - 1), 0), rows - 1) * C + n];
       SK[sko(i)] = __uint_as_float(__float_as_uint(sv) & mo);
     }
   }
   // conv zero padding: tap t-1 / t+1 of the lane's A rows (window row 32q + r32) outside its
   // utterance (or outside the batch) reads zero -- a select at the fragment read
   bool mlo[2], mhi[2];
+  // the per-layer epilogue's row conditions as bits of two lane words (bit 16 q + reg: window row
+  // inside the batch / in utterance bB), made opaque once per layer below: as 64 hoisted lane masks
+  // they took the SGPR file and spilled (r05)
+  unsigned vin = 0, vbb = 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      vin |= (R >= 0 && R < rows ? 1u : 0u) << (16 * q + reg);
+      vbb |= (R >= RB ? 1u : 0u) << (16 * q + reg);
+    }
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int R = W0 + 32 * q + r32, Rc = min(max(R, 0), rows - 1), bq = Rc / T, t = Rc - bq * T;
@@ -587,20 +600,19 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) xr[q][reg] = (xr[q][reg] + ar[q][reg] + brv) * rs2;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
-      SK[sko(i)] = SK[sko(i)] + as_[q][reg] + bsv;
-    }
+    for (int i = 0; i < 24; ++i) SK[sko(i)] = SK[sko(i)] + as_[skq(i)][skr(i)] + bsv;
     if (j + 1 < P.nl) {
       const float dA = P.dp[(long long)bA * P.dp_ld + (long long)(l + 1) * C + n];
       const float dB = P.dp[(long long)bB * P.dp_ld + (long long)(l + 1) * C + n];
+      unsigned vi = vin, vb = vbb;
+      asm volatile("" : "+v"(vi), "+v"(vb));
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-          const int r = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + r;
-          const float m = (R >= 0 && R < rows) ? 1.f : 0.f;
-          XW[r * WST_LD + n] = (__bf16)((xr[q][reg] + (R < RB ? dA : dB)) * m);
+          const int r = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, k = 16 * q + reg;
+          const float m = __uint_as_float(((vi >> k) & 1u) * 0x3f800000u);
+          XW[r * WST_LD + n] = (__bf16)((xr[q][reg] + (((vb >> k) & 1u) ? dB : dA)) * m);
         }
     }
     __syncthreads();   // XW written / Gs reads done before the next layer
@@ -612,24 +624,22 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) wsf[ks] = *reinterpret_cast<const bf16x8*>(P.Wsb + (long long)n * C + ks * 16 + h * 8);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {   // window rows 16..47 -> XW rows 0..31
-      const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
-      const int wrow = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      XW[(wrow - 16) * WST_LD + n] = (__bf16)(SK[sko(i)] * P.skip_scale);
-    }
+    for (int i = 0; i < 24; ++i)   // window rows 8..55 -> XW rows 0..47 (rows 48..63 keep finite
+      XW[(skw(i) - 8) * WST_LD + n] = (__bf16)(SK[sko(i)] * P.skip_scale);   // x values, never stored)
     __syncthreads();
-    {
+    const float bsv = P.bs[n];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 16; ++ks)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&XW[r32 * WST_LD + ks * 16 + h * 8]),
-                                                      wsf[ks], acc, 0, 0, 0);
-      const float bsv = P.bs[n];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            *reinterpret_cast<const bf16x8*>(&XW[(32 * q + r32) * WST_LD + ks * 16 + h * 8]), wsf[ks], acc, 0, 0, 0);
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg)
-        Gs[((reg & 3) + 8 * (reg >> 2) + 4 * h) * WST_LD + n] = (__bf16)act_apply(acc[reg] + bsv, ACT_RELU, 0.f);
+        Gs[(32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h) * WST_LD + n] = (__bf16)act_apply(acc[reg] + bsv, ACT_RELU, 0.f);
     }
     __syncthreads();
     const int col = wave * 32 + r32, M = P.M;
@@ -638,29 +648,32 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
       bf16x8 wof[16];
 #pragma unroll
       for (int ks = 0; ks < 16; ++ks) wof[ks] = *reinterpret_cast<const bf16x8*>(P.Wob + (long long)colc * C + ks * 16 + h * 8);
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 16; ++ks)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&Gs[r32 * WST_LD + ks * 16 + h * 8]),
-                                                      wof[ks], acc, 0, 0, 0);
       const float bov = P.bo[colc];
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + 16 + row;
-        if (row < P.ro && R < rows && col < M) {
-          // prodiff.py:106-126 (gemm.h EPI_POSTERIOR): x = c1 x0 + c2 x_t + sigma n
-          const int b = R / T, t = R - b * T;
-          const float v = acc[reg] + bov;
-          const float xt = P.mel[(long long)R * M + col];
-          float x = P.c1 * v + P.c2 * xt;
-          if (P.sigma != 0.f) {
-            const float z = P.noise ? P.noise[(long long)b * P.noise_bs + (long long)t * P.noise_ld + col]
-                                    : philox_normal_u(P.seed, utt_id(P.uid, b), (unsigned)(t * M + col), P.stream_id);
-            x += P.sigma * z;
+      for (int q = 0; q < 2; ++q) {
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              *reinterpret_cast<const bf16x8*>(&Gs[(32 * q + r32) * WST_LD + ks * 16 + h * 8]), wof[ks], acc, 0, 0, 0);
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int wrow = 8 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + wrow;
+          if (wrow >= HL && wrow - HL < P.ro && R < rows && col < M) {
+            // prodiff.py:106-126 (gemm.h EPI_POSTERIOR): x = c1 x0 + c2 x_t + sigma n
+            const int b = R / T, t = R - b * T;
+            const float v = acc[reg] + bov;
+            const float xt = P.mel[(long long)R * M + col];
+            float x = P.c1 * v + P.c2 * xt;
+            if (P.sigma != 0.f) {
+              const float z = P.noise ? P.noise[(long long)b * P.noise_bs + (long long)t * P.noise_ld + col]
+                                      : philox_normal_u(P.seed, utt_id(P.uid, b), (unsigned)(t * M + col), P.stream_id);
+              x += P.sigma * z;
+            }
+            P.mel[(long long)R * M + col] = x;
           }
-          P.mel[(long long)R * M + col] = x;
         }
       }
     }
@@ -669,11 +682,10 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   //      last layer's x feeds nothing, and the skip sum was consumed here)
   if constexpr (TAIL) return;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int q = i < 8 ? 0 : 1, reg = i < 8 ? 8 + i : i - 8;
-    const int wrow = 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + wrow;
-    if (R < rows && wrow - 16 < P.ro) {
-      P.xout[(long long)R * C + n] = xr[q][reg];
+  for (int i = 0; i < 24; ++i) {
+    const int wrow = skw(i), R = W0 + wrow;
+    if (R < rows && wrow >= HL && wrow - HL < P.ro) {
+      P.xout[(long long)R * C + n] = xr[skq(i)][skr(i)];
       P.skip[(long long)R * C + n] = SK[sko(i)];
     }
   }
@@ -1445,11 +1457,14 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       P.W1f = h->W1f; P.b1 = h->bl1; P.W2f = h->W2f; P.b2 = h->bl2;
       P.rows = rows; P.T = T; P.l0 = l0; P.nl = std::min(h->stack_nl, Ly - l0); P.first = l0 == 0; P.L = Ly;
       P.lens = lens;
-      // output rows per block (PD_WN_OPT_STACK_RO, default 32).  r04: spreading C3's 6888 rows over
+      // output rows per block (PD_WN_OPT_STACK_RO; r04 default 32).  r04: spreading C3's 6888 rows over
       // all 256 CUs (27 rows per block) measured slower than 216 blocks of 32 (214 vs 202-205 us per
       // 10 layers, profiles/r04_ab/): every block streams each layer's 1.3 MB of weights from its
       // XCD's L2, and 32 blocks per XCD instead of 27 share that L2's bandwidth
-      P.ro = h->stack_ro > 0 ? h->stack_ro : 32;
+      // r05: the halo is the launch's layer count (>= 8, the skip image's first row), and the
+      // default writes every exact row, 64 - 2 hl (44 at 10 layers)
+      P.hl = std::max(P.nl, 8);
+      P.ro = std::min(h->stack_ro > 0 ? h->stack_ro : 64, 64 - 2 * P.hl);
       if (fuse_in && l0 == 0) {
         P.spec = xin; P.Winb = Winb; P.b_in = h->b_in; P.M = M; P.ldw_in = h->ldw_in;
       }
@@ -1725,7 +1740,7 @@ int pd_wavenet_set_option(pd_wavenet* h, int option, int value) {
     return PD_OK;
   }
   if (option == PD_WN_OPT_STACK_RO) {
-    PD_CHECK_ARG(value == 0 || (value >= 16 && value <= 32), "PD_WN_OPT_STACK_RO is 0 (auto) or 16 .. 32");
+    PD_CHECK_ARG(value == 0 || (value >= 16 && value <= 48), "PD_WN_OPT_STACK_RO is 0 (auto) or 16 .. 48");
     h->stack_ro = value;
     return PD_OK;
   }
