@@ -327,10 +327,13 @@ size_t nsf_workspace_size(const nsf_model* m, int B, int T);
  * MFMA conv kernels (input window staged once in LDS for all taps), ahead of
  * NSF_OPT_SMALL_MAX; 0 = the implicit-GEMM engine / small kernel.  No effect on the fp32 path. */
 #define NSF_OPT_WCONV 1
-/* NSF_OPT_PAIR: 1 (default) runs each ResBlock1 conv pair c2(lrelu(c1(lrelu(x)))) + x with 64 or 128
- * channels as ONE windowed launch (the inner activation stays in LDS, x is read once); 0 = two
+/* NSF_OPT_PAIR: 1 (default) runs each ResBlock1 conv pair c2(lrelu(c1(lrelu(x)))) + x with 32, 64 or 128
+ * channels (16: NSF_OPT_PAIR16) as ONE windowed launch (the inner activation stays in LDS, x is read once); 0 = two
  * windowed launches with the inner activation through HBM in bf16.  Same roundings either way. */
 #define NSF_OPT_PAIR 2
+/* NSF_OPT_PAIR16: 1 (default) runs the 16-channel ResBlock1 pairs of the shipped shapes (taps 3/7/11,
+ * dilation 1/3/5) the same way, on 16x16x32 MFMAs; 0 = two launches for them.  Needs NSF_OPT_PAIR. */
+#define NSF_OPT_PAIR16 3
 int nsf_set_option(nsf_model* m, int option, int value);
 
 /* spec2wav_torch(mel, f0=f0) for a batch of independent utterances:

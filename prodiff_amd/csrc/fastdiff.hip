@@ -469,6 +469,9 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
   // a global weight load behind the prefetch would wait for the whole prefetch).
   // SUB (hop 8) stages the pre-conv weights too (WW): a global load per layer made every layer
   // start with an L2 round trip; its LVC biases stay per-frame global reads.
+  // (r05: without the staged weights SUB's 69 KB of LDS would fit two blocks per CU, but its
+  // registers do not: ~260 VGPRs -- the two-frame K pipeline alone is 96 -- and at the 168-VGPR cap of
+  // 3 waves per SIMD it spills 382)
   constexpr bool WL = PF, WW = PF || SUB;
   // frames a block touches: its GR rows span at most GR / hop + 2 frames, and PF (= WL) launches
   // have hop % 64 == 0 (r05: sized for hop >= 32 before, 18 frames -- 8 more than any PF launch reads,
@@ -1521,7 +1524,7 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
                                                                        const __bf16* __restrict__ W,
                                                                        const float* __restrict__ bias,
                                                                        __bf16* __restrict__ Kf, int Tc, int rows,
-                                                                       int nfg, const int* __restrict__ lens) {
+                                                                       int nfg) {
   __shared__ __attribute__((aligned(16))) __bf16 Hs[2][KP_F * KP_LDH];
   __shared__ __attribute__((aligned(16))) __bf16 Ot[8][32 * KP_LDO];   // swizzled (kp_swz)
   __shared__ __attribute__((aligned(16))) float Bq[8][64];   // wave-private: its rows' biases
@@ -1543,27 +1546,26 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
     hz = 0;
     // the item's first frame split once (wave-uniform); piece frames step forward from it
     const int R0 = fg * KP_F, b0 = R0 / Tc, f00 = R0 - b0 * Tc;
-    // ragged batch: the item's (at most two, when Tc >= KP_F) utterances' own ends -- uniform loads
-    const int tvA = lens ? lens[b0] : Tc, tvB = lens ? lens[min(b0 + 1, rows / Tc - 1)] : Tc;
+    // (ragged batch: kp_hidden_bf16_kernel writes zero h rows past each utterance's end, so the
+    // kernel conv's zero padding there needs no lengths here.  r05: reading lens in this loop put
+    // loads under branches whose joins waited for every outstanding load and K store: kp 85 -> 103 us)
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const int c = tid + KP_THREADS * i, fl = c / 24, v = (c - fl * 24) * 8, tap = v >> 6, ch = v & 63;
       const int R = R0 + fl, Rc = R < rows ? R : rows - 1;
-      int b = b0, f = f00 + (Rc - R0), Tv = tvA;
+      int b = b0, f = f00 + (Rc - R0);
       if (Tc >= KP_F) {                   // (uniform) the item crosses at most one utterance end
         const bool nx = f >= Tc;
         f -= nx ? Tc : 0;
         b += nx ? 1 : 0;
-        Tv = nx ? tvB : tvA;
       } else {
         b = Rc / Tc;
         f = Rc - b * Tc;
-        Tv = lens ? lens[b] : Tc;
       }
       const int ff = f + tap - 1;
       const int ffc = ff < 0 ? 0 : ff >= Tc ? Tc - 1 : ff;     // clamped: unconditional load
       hv[i] = *reinterpret_cast<const uint4*>(hin + ((long long)b * Tc + ffc) * HK + ch);
-      hz |= (R >= rows || ff < 0 || ff >= Tc || ff >= Tv) ? 1u << i : 0u;
+      hz |= (R >= rows || ff < 0 || ff >= Tc) ? 1u << i : 0u;
     }
   };
   auto h_store = [&](int buf) {
@@ -1688,8 +1690,9 @@ __global__ void kp_prescale_kernel(const float* __restrict__ w, const float* __r
   if (i % (3 * HK) == 0) bs[n] = b[n] * s;
 }
 
+// (ragged batches need no lengths here: hk rows past an utterance's end are zero, kp_hidden_bf16_kernel)
 int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B, int Tc, hipStream_t st,
-                   bool prescale = false, const int* lens = nullptr) {
+                   bool prescale = false) {
   const int rows = B * Tc;
   const int nfg = cdiv(rows, KP_F);
   // buffer-store offsets are 32-bit bytes, up to the last (partial) item's rows
@@ -1698,7 +1701,7 @@ int kp_kernels_all(const fd_model::Block& K, const __bf16* hk, __bf16* Kb, int B
   const int grid = items < 256 ? items : 256;   // persistent: one block per CU
   ProfScope ps("fd_kp_kernel", st);
   hipLaunchKernelGGL(kp_kernel_bf16_kernel, dim3(grid), dim3(KP_THREADS), 0, st, hk,
-                     prescale ? K.kks_w : lookup_bf16(K.kk_w), prescale ? K.kks_b : K.kk_b, Kb, Tc, rows, nfg, lens);
+                     prescale ? K.kks_w : lookup_bf16(K.kk_w), prescale ? K.kks_b : K.kk_b, Kb, Tc, rows, nfg);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -2109,7 +2112,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         Kc += (size_t)n * rows * NLY * KPERLAYER;
         PD_HIP(hipStreamWaitEvent(st, m->ev_kp[n], 0));
       } else {
-        PD_TRY(kp_kernels_all(K, hkb + (size_t)b0 * Tc * HK, Kc, nbk, Tc, st, true, lens ? lens + b0 : nullptr));
+        PD_TRY(kp_kernels_all(K, hkb + (size_t)b0 * Tc * HK, Kc, nbk, Tc, st, true));
       }
       LvcBlockArgs la{};
       for (int i = 0; i < NLY; ++i) {
@@ -2161,7 +2164,7 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
       PD_LAUNCH_CHECK();
     }
     // --- 4 LVC layers (modules.py:208-217)
-    if (bf) PD_TRY(kp_kernels_all(K, hkb, reinterpret_cast<__bf16*>(ws + W.Kf), B, Tc, st, false, lens));   // all 4 layers
+    if (bf) PD_TRY(kp_kernels_all(K, hkb, reinterpret_cast<__bf16*>(ws + W.Kf), B, Tc, st, false));   // all 4 layers
     for (int i = 0; i < NLY; ++i) {
       const __bf16* Kbl = reinterpret_cast<const __bf16*>(ws + W.Kf) + (size_t)i * B * Tc * KPERLAYER;
       if (!bf) {
@@ -2520,7 +2523,7 @@ int fd_sample_coefs(const fd_model* m, const float* mel, const float* ce_, const
           if (j > 0) PD_HIP(hipStreamWaitEvent(m->side, m->ev_lvc[b], 0));
           const __bf16* hkb = reinterpret_cast<const __bf16*>(ws + W.hall) + ((size_t)jl * nb + b) * rows * HK;
           __bf16* Kb = reinterpret_cast<__bf16*>(ws + W.Kf) + (size_t)b * rows * NLY * KPERLAYER;
-          PD_TRY(kp_kernels_all(m->blk[b], hkb, Kb, B, Tc, m->side, true, lens));
+          PD_TRY(kp_kernels_all(m->blk[b], hkb, Kb, B, Tc, m->side, true));
           PD_HIP(hipEventRecord(m->ev_kp[b], m->side));
         }
       }

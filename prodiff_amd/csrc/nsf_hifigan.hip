@@ -61,6 +61,7 @@ struct nsf_model {
   std::vector<NsfConv> res;      // [stage][kernel][conv] flattened in state-dict order
   bool ups_window = true;        // NSF_OPT_WCONV also selects the windowed ConvTranspose
   bool pair = true;              // NSF_OPT_PAIR: a ResBlock1 conv pair in one launch (nsf_pair_kernel)
+  bool pair16 = true;            // NSF_OPT_PAIR16: the C = 16 pairs too (nsf_pair16_kernel), with pair
   int convs_per_block = 0;
 };
 
@@ -388,6 +389,9 @@ __device__ __forceinline__ void stage_window(const void* __restrict__ in, int b,
 #define NSF_RING_PIN 0
 #endif
 constexpr int NSF_PF = NSF_PF_DEPTH;
+#ifndef NSF_PAIR_PF
+#define NSF_PAIR_PF NSF_PF_DEPTH   // the pair kernel's weight ring depth (k-steps)
+#endif
 
 template <int C, int FM, int FN, int WM, int WN, bool IN_BF, bool OUT_BF>
 __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
@@ -545,7 +549,7 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
   stage_window<C, false>(x, b, Tl, Tv, t0 - p2 - p1, WX, NSF_LRELU, 1.f, xwin, LDA, tid);
   __syncthreads();
   const int S = taps * KS;
-  constexpr int PF = KS >= NSF_PF ? NSF_PF : KS;
+  constexpr int PF = KS >= NSF_PAIR_PF ? NSF_PAIR_PF : KS;
   static_assert(KS % PF == 0, "ring depth divides the k-steps per tap");
   const int n = ct * 32 + r32;                           // this lane's output channel (C layout column)
   // ---- c1 on row tiles rt = rg + RG m (xt rows 32 rt ..)
@@ -660,10 +664,13 @@ __global__ __launch_bounds__(256, 2) void nsf_pair_kernel(const float* __restric
 #ifndef NSF_PAIR_FMO64
 #define NSF_PAIR_FMO64 8   // C = 64 output row tiles per block (r04: 4 -> 8, C5 -4%)
 #endif
+#ifndef NSF_PAIR_FMO128
+#define NSF_PAIR_FMO128 4  // C = 128 output row tiles per block
+#endif
 template <int C, int TAPS, int DIL>
 int launch_pair_ct(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
                    hipStream_t st, NsfRag rag_) {
-  constexpr int FMO = C == 32 ? NSF_PAIR_FMO32 : C == 64 ? NSF_PAIR_FMO64 : 4, TM = 32 * FMO;
+  constexpr int FMO = C == 32 ? NSF_PAIR_FMO32 : C == 64 ? NSF_PAIR_FMO64 : NSF_PAIR_FMO128, TM = 32 * FMO;
   // x / xt window + stage_window's spare row
   const size_t lds = (size_t)(32 * (FMO + 1) + (c1.taps - 1) * c1.dil + 1) * (C + 8) * sizeof(__bf16);
   static const hipError_t attr = hipFuncSetAttribute(
@@ -695,11 +702,16 @@ int launch_pair_c(const NsfConv& c1, const NsfConv& c2, const float* x, int B, i
 bool wconv_ok(const NsfConv& c);
 // The fused pair for these convs, if it has one: both windowed (bf16), 32, 64 or 128 channels, equal
 // taps and packing, c2 undilated.
+// C = 16 (nsf_pair16_kernel): the shipped shapes only -- taps 3 / 7 / 11, c1 dilation 1 / 3 / 5.
 bool pair_ok(const nsf_model* m, const NsfConv& c1, const NsfConv& c2) {
+  const bool c16 = c1.cout == 16 && c1.kpad == 32 && (c1.taps == 3 || c1.taps == 7 || c1.taps == 11) &&
+                   (c1.dil == 1 || c1.dil == 3 || c1.dil == 5);
   return m->pair && wconv_ok(c1) && wconv_ok(c2) && c1.cout == c2.cout &&
-         (c1.cout == 32 || c1.cout == 64 || c1.cout == 128) &&
+         (c1.cout == 32 || c1.cout == 64 || c1.cout == 128 || (c16 && m->pair16)) &&
          c1.taps == c2.taps && c1.kpad == c2.kpad && c2.dil == 1 && c1.taps <= 33;
 }
+int launch_pair16(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
+                  hipStream_t st, NsfRag rag_);
 
 int launch_pair(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
                 hipStream_t st, NsfRag rag_) {
@@ -707,6 +719,7 @@ int launch_pair(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int
     set_error("nsf pair: B * T * C >= 2^31 elements (32-bit epilogue offsets)");
     return PD_ERR_UNSUPPORTED;
   }
+  if (c1.cout == 16) return launch_pair16(c1, c2, x, B, Tl, out, accum, st, rag_);
   if (c1.cout == 128) return launch_pair_c<128>(c1, c2, x, B, Tl, out, accum, st, rag_);
   if (c1.cout == 32) return launch_pair_c<32>(c1, c2, x, B, Tl, out, accum, st, rag_);
   return launch_pair_c<64>(c1, c2, x, B, Tl, out, accum, st, rag_);
@@ -797,6 +810,136 @@ __global__ __launch_bounds__(256) void nsf_wconv16_kernel(const void* __restrict
       nsf_store_utt<OUT_BF>(ors, t * C + r16, v);   // rows t >= Tl dropped by the range check
     }
   }
+}
+
+// ResBlock1 conv pair at C = 16 in ONE launch (r05; models.py:57-63): nsf_pair_kernel's structure on
+// nsf_wconv16_kernel's 16x16x32 MFMA layout, for the shipped (taps, dilation) shapes.  Block = 256
+// output rows, 4 waves.  The x window (rows t0 - p2 - p1 .., lrelu'd, bf16) is staged once; c1 runs
+// on the 17 16-row tiles of xt that c2 reads (times t0 - p2 + i, i < 272 >= 256 + 2 p2), rounds them
+// to bf16 as the two-launch path's bf16 intermediate, applies lrelu, zeroes rows outside the
+// utterance and keeps them in their own LDS window; c2 adds bias and the residual x (+ out).  Same
+// roundings and the same MFMA order as two nsf_wconv16 launches: bit-identical, without the bf16
+// intermediate's HBM write and read (the C = 16 stage is the step's largest activation: 64 B per
+// row at 441k rows per utterance) and the second window staging.
+template <int TAPS, int DIL>
+__global__ __launch_bounds__(256, 3) void nsf_pair16_kernel(const float* __restrict__ x, const __bf16* __restrict__ w1,
+                                                         const __bf16* __restrict__ w2, const float* __restrict__ b1,
+                                                         const float* __restrict__ b2, int Tl, float* __restrict__ out,
+                                                         int accum, NsfRag rag_) {
+  constexpr int C = 16, TM = 256, LDA = 24, NP = (TAPS + 1) / 2, KP = 32;
+  constexpr int P2 = (TAPS - 1) / 2, P1 = (TAPS - 1) * DIL / 2;
+  constexpr int RT1 = 17, XR = 16 * RT1, WX = XR + (TAPS - 1) * DIL, MF1 = (RT1 + 3) / 4;
+  static_assert(TM + 2 * P2 <= XR, "c1's tiles cover c2's reach");
+  __shared__ __attribute__((aligned(16))) __bf16 xwin[(WX + 1) * LDA];   // + stage_window's spare row
+  __shared__ __attribute__((aligned(16))) __bf16 xtw[XR * LDA];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.y, t0 = blockIdx.x * TM;
+  const int Tv = nsf_tv(rag_, b, Tl);
+  stage_window<C, false>(x, b, Tl, Tv, t0 - P2 - P1, WX, NSF_LRELU, 1.f, xwin, LDA, tid);
+  const int r16 = lane & 15, g = lane >> 4, kg = g & 1, tg = g >> 1;
+  // a conv's tap-pair fragments, unconditional loads at a clamped tap, zeroed by a bit mask (c2's
+  // are loaded after c1's MFMAs: 24 fewer live registers through c1)
+  auto wload = [&](const __bf16* w, bf16x8 (&wf)[NP]) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int tap = 2 * p + tg, tc = min(tap, TAPS - 1);
+      const unsigned mk = tap < TAPS ? 0xffffffffu : 0u;
+      const uint4 r = *reinterpret_cast<const uint4*>(w + (long long)r16 * (TAPS * KP) + tc * KP + 8 * kg);
+      wf[p] = __builtin_bit_cast(bf16x8, make_uint4(r.x & mk, r.y & mk, r.z & mk, r.w & mk));
+    }
+  };
+  bf16x8 wf1[NP], wf2[NP];
+  wload(w1, wf1);
+  // c2's residual / accumulator operands, in flight under the MFMAs (nsf_wconv16_kernel's order)
+  float rv[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = min(t0 + wave * 64 + i * 16 + 4 * g + r, Tl - 1);
+      const long long o = ((long long)b * Tl + t) * C + r16;
+      const float a = out[o];
+      const float v = x[o];
+      rv[i][r] = accum ? v + a : v;
+    }
+  const float bn1 = b1[r16], bn2 = b2[r16];
+  __syncthreads();
+  const bf16x8 z8 = {};
+  // ---- c1 on xt tiles rt = wave + 4 m
+  {
+    f32x4 acc[MF1];
+#pragma unroll
+    for (int m = 0; m < MF1; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int tap = 2 * p + tg;
+#pragma unroll
+      for (int m = 0; m < MF1; ++m) {
+        const int rt = wave + 4 * m;
+        if (rt < RT1) {   // (wave-uniform)
+          bf16x8 af = *reinterpret_cast<const bf16x8*>(xwin + (rt * 16 + r16 + min(tap, TAPS - 1) * DIL) * LDA + 8 * kg);
+          if (TAPS % 2 == 1 && p == NP - 1) af = tap < TAPS ? af : z8;
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf1[p], acc[m], 0, 0, 0);
+        }
+      }
+    }
+    wload(w2, wf2);
+    // xt = bf16(acc + b1) (the two-launch path's bf16 intermediate), then c2's input lrelu(xt)
+    // rounded to bf16 again; rows outside the utterance are c2's zero padding
+#pragma unroll
+    for (int m = 0; m < MF1; ++m) {
+      const int rt = wave + 4 * m;
+      if (rt < RT1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = rt * 16 + 4 * g + r, t = t0 - P2 + i;
+          const float v = (float)(__bf16)(acc[m][r] + bn1);
+          const float u = (t >= 0 && t < Tv) ? (v >= 0.f ? v : NSF_LRELU * v) : 0.f;
+          xtw[i * LDA + r16] = (__bf16)u;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- c2 on output tiles wave * 4 + i, + bias + residual (+ out)
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int tap = 2 * p + tg;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 af = *reinterpret_cast<const bf16x8*>(xtw + (wave * 64 + i * 16 + r16 + min(tap, TAPS - 1)) * LDA + 8 * kg);
+      if (TAPS % 2 == 1 && p == NP - 1) af = tap < TAPS ? af : z8;
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf2[p], acc[i], 0, 0, 0);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t ors = nsf_utt_rsrc<false>(out, b * Tl, Tl, C);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = t0 + wave * 64 + i * 16 + 4 * g + r;
+      nsf_store_utt<false>(ors, t * C + r16, acc[i][r] + bn2 + rv[i][r]);   // rows t >= Tl dropped
+    }
+}
+
+int launch_pair16(const NsfConv& c1, const NsfConv& c2, const float* x, int B, int Tl, float* out, int accum,
+                  hipStream_t st, NsfRag rag_) {
+  const dim3 grid(cdiv(Tl, 256), B);
+  ProfScope ps("nsf_pair16", st);
+#define PD_PAIR16(K, D)                                                                                            \
+  if (c1.taps == K && c1.dil == D)                                                                                 \
+    hipLaunchKernelGGL((nsf_pair16_kernel<K, D>), grid, dim3(256), 0, st, x, lookup_bf16(c1.w), lookup_bf16(c2.w), \
+                       c1.b, c2.b, Tl, out, accum, rag_)
+  PD_PAIR16(3, 1); else PD_PAIR16(3, 3); else PD_PAIR16(3, 5);
+  else PD_PAIR16(7, 1); else PD_PAIR16(7, 3); else PD_PAIR16(7, 5);
+  else PD_PAIR16(11, 1); else PD_PAIR16(11, 3); else PD_PAIR16(11, 5);
+  else { set_error("nsf pair16: not a shipped (taps, dilation) shape"); return PD_ERR_UNSUPPORTED; }
+#undef PD_PAIR16
+  PD_LAUNCH_CHECK();
+  return PD_OK;
 }
 
 int launch_wconv16(const NsfConv& c, const __bf16* wb, const void* in, bool in_bf, float alpha, float scale, int B,
@@ -1371,6 +1514,11 @@ int nsf_set_option(nsf_model* m, int option, int value) {
     m->pair = value != 0;
     return PD_OK;
   }
+  if (option == NSF_OPT_PAIR16) {
+    PD_CHECK_ARG(value == 0 || value == 1, "NSF_OPT_PAIR16 is 0 or 1");
+    m->pair16 = value != 0;
+    return PD_OK;
+  }
   set_error("nsf_set_option: unknown option " + std::to_string(option));
   return PD_ERR_ARG;
 }
@@ -1549,6 +1697,12 @@ const char* nsf_build_flags() {
 #endif
 #if NSF_PAIR_FMO32 != 15
          " NSF_PAIR_FMO32"
+#endif
+#if NSF_PAIR_FMO128 != 4
+         " NSF_PAIR_FMO128"
+#endif
+#if NSF_PAIR_PF != NSF_PF_DEPTH
+         " NSF_PAIR_PF"
 #endif
 #if NSF_PAIR_FMO64 != 8
          " NSF_PAIR_FMO64"

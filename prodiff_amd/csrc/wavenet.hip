@@ -68,6 +68,16 @@ __global__ void pack_frag_kernel(__bf16* dst, const float* src, int N, int K, in
 // columns [32w, 32w+32) / [C+32w, ...) of GEMM1 and residual/skip columns of GEMM2,
 // so both epilogues pair their halves in registers.  The K=1024 input row lives in
 // LDS (bf16); weights stream from L2 in fragment order (1 KB per wave-load).
+// Ragged batch: row b's utterance length (lens null: T).  The load is unconditional -- from `any`, a
+// readable int array, when lens is null, masked off -- because a load under `lens ?` made hipcc wait
+// at the branch join for every load issued before it (r05: the stack kernel's prologue then waited
+// for its x / skip loads, ~+7 us per launch at C3).  `any` must hold at least b + 1 ints.
+__device__ __forceinline__ int wn_len(const int* lens, const void* any, int b, int T) {
+  const unsigned lm = lens ? 0xffffffffu : 0u;
+  const int v = (lens ? lens : reinterpret_cast<const int*>(any))[lens ? b : 0];
+  return (int)(((unsigned)min(v, T) & lm) | ((unsigned)T & ~lm));
+}
+
 struct WnLayerArgs {
   const float* xin;       // [B][T][C] layer input (other blocks read its halo rows,
   float* xout;            //            so the update goes to a second buffer)
@@ -184,7 +194,7 @@ __global__ __launch_bounds__(512) void wn_layer_bf16_kernel(const WnLayerArgs P)
         while (tq >= P.T) { tq -= P.T; ++bq; }
       }
       const int b = bq, t = tq, tt = isx ? t + sh : t;
-      const int lb = P.lens ? P.lens[b] : P.T;    // ragged batch: the utterance's own end
+      const int lb = wn_len(P.lens, P.b1, b, P.T);   // ragged batch: the utterance's own end
       const bool v = R < rows && tt >= 0 && tt < P.T && tt < lb;
       const int ttc = tt < 0 ? 0 : tt >= P.T ? P.T - 1 : tt;
       ok[it] = v ? 1.f : 0.f;
@@ -507,7 +517,7 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int R = W0 + 32 * q + r32, Rc = min(max(R, 0), rows - 1), bq = Rc / T, t = Rc - bq * T;
-    const int lb = P.lens ? min(P.lens[bq], T) : T;   // ragged batch: the utterance's own end
+    const int lb = wn_len(P.lens, P.b1, bq, T);       // ragged batch: the utterance's own end
     mlo[q] = R >= 0 && R < rows && t >= 1;
     mhi[q] = R >= 0 && R < rows && t <= lb - 2;
   }
@@ -787,7 +797,7 @@ __global__ __launch_bounds__(NW * 64) void wn_f32_layer_kernel(const WnF32Args P
     if constexpr (GATE) {
       const int sg = wave / (NW / 4), k0 = (wave % (NW / 4)) * (C / (NW / 4));   // segment, offset in it
       if (sg < 3) {   // tap segment: x(t + (sg - 1) d) + dp, zero outside the utterance
-        const int lb = P.lens ? P.lens[b] : P.T;   // ragged batch: the utterance's own end
+        const int lb = wn_len(P.lens, P.bias, b, P.T);   // ragged batch: the utterance's own end
         const int tt = t + (sg - 1) * P.dil, ok = R < P.rows && tt >= 0 && tt < P.T && tt < lb;
         const float* arow = P.a + ((long long)b * P.T + min(max(tt, 0), P.T - 1)) * C + k0;
         wf32_seg<NCH, true>(arow, P.dp + (long long)b * P.dp_ld + k0, ok, w0 + sg * C + k0, w1 + sg * C + k0, h, acc0,
