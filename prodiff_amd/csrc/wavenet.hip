@@ -395,30 +395,81 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   // T >= 64 (the host's condition) puts at most two utterances, bA and bB, in the window
   const int bA = min(max(W0, 0), rows - 1) / T, RB = (bA + 1) * T;   // rows >= RB: utterance bB
   const int bB = min(bA + 1, (rows - 1) / T);
-  // ---- staging: window rows of bf16(x + dp_l0) and bf16(cond); zero outside [0, rows)
+  // ---- staging: window rows of bf16(x + dp_l0) and bf16(cond); zero outside [0, rows).
+  //      Every prologue load is issued before any of them is used (sched_barrier): interleaved
+  //      with the conversions and LDS stores, hipcc issued them one or two at a time with a full
+  //      wait after each -- ~40 round trips per block (r05 asm)
+  constexpr int NXS = IN ? 1 : WR * 64 / 512, NSP = IN ? WR * 32 / 512 : 1, NCD = WR * 32 / 512;
+  float4 xv4[NXS], dv4[NXS], sp4[NSP];
+  uint4 cd4[NCD];
   if constexpr (!IN) {
 #pragma unroll
-    for (int it = 0; it < WR * 64 / 512; ++it) {
+    for (int it = 0; it < NXS; ++it) {
       const int i = tid + it * 512, wr = i >> 6, c = (i & 63) * 4, R = W0 + wr;
       const int Rc = min(max(R, 0), rows - 1);
-      const float4 v = *reinterpret_cast<const float4*>(P.xin + (long long)Rc * C + c);
+      xv4[it] = *reinterpret_cast<const float4*>(P.xin + (long long)Rc * C + c);
       const int b = Rc < RB ? bA : bB;
-      const float4 d = *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + (long long)P.l0 * C + c);
+      dv4[it] = *reinterpret_cast<const float4*>(P.dp + (long long)b * P.dp_ld + (long long)P.l0 * C + c);
+    }
+  } else {
+    // fused input projection: bf16(spec) of the window rows into Gs (k >= M zero, as the GEMM
+    // engine's padded K chunks): 64 rows x 32 column quads (128 columns, zero past M), loads
+    // unconditional (clamped column, zeroed by a multiply; spec is finite)
+#pragma unroll
+    for (int it = 0; it < NSP; ++it) {
+      const int i = tid + 512 * it, wr = i >> 5, c = (i & 31) * 4;
+      const int Rc = min(max(W0 + wr, 0), rows - 1);
+      sp4[it] = *reinterpret_cast<const float4*>(P.spec + (long long)Rc * P.M + min(c, P.M - 4));
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < NCD; ++it) {
+    const int i = tid + it * 512, wr = i >> 5, c = (i & 31) * 8, R = W0 + wr;
+    cd4[it] = *reinterpret_cast<const uint4*>(P.condb + (long long)min(max(R, 0), rows - 1) * H + c);
+  }
+  // x (fp32) of the lane's 32 window rows, column n, in registers (the GEMM2 C layout: tile q,
+  // register reg -> window row 32 q + (reg & 3) + 8 (reg >> 2) + 4 h); the skip sums of its 24
+  // rows in [8, 56) (tile 0 regs 4..15 = window rows 8..31, tile 1 regs 0..11 = window rows 32..55),
+  // a superset of the output rows, in LDS, entries only this lane touches
+  float xr[2][16];
+  auto skq = [](int i) { return i < 12 ? 0 : 1; };          // SK value i: tile, register
+  auto skr = [](int i) { return i < 12 ? 4 + i : i - 12; };
+  auto skw = [&](int i) { const int reg = skr(i); return 32 * skq(i) + (reg & 3) + 8 * (reg >> 2) + 4 * h; };
+  auto sko = [&](int i) { return (skw(i) - 8) * C + n; };
+  if constexpr (!IN) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        xr[q][reg] = P.xin[(long long)min(max(R, 0), rows - 1) * C + n];
+      }
+  }
+  // the skip sums: only this block's output rows [R0, R0 + ro) are read -- the window's rows either
+  // side of them belong to the neighbouring blocks, which write them in this launch: their loads are
+  // clamped into the block's rows and the values masked to zero (they are never stored anyway)
+  float skv[24];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) {
+    const int R = W0 + skw(i);
+    skv[i] = P.skip[(long long)min(max(min(max(R, R0), R0 + P.ro - 1), 0), rows - 1) * C + n];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (!IN) {
+#pragma unroll
+    for (int it = 0; it < NXS; ++it) {
+      const int i = tid + it * 512, wr = i >> 6, c = (i & 63) * 4, R = W0 + wr;
       const float m = (R >= 0 && R < rows) ? 1.f : 0.f;
+      const float4 v = xv4[it], d = dv4[it];
       *reinterpret_cast<bf16x4*>(&XW[wr * WST_LD + c]) =
           bf16x4{(__bf16)((v.x + d.x) * m), (__bf16)((v.y + d.y) * m), (__bf16)((v.z + d.z) * m), (__bf16)((v.w + d.w) * m)};
     }
   } else {
-    // fused input projection: bf16(spec) of the window rows into Gs (k >= M zero, as the GEMM
-    // engine's padded K chunks)
-    // 64 rows x 32 column quads (128 columns, zero past M), unrolled with unconditional loads
-    // (clamped column, zeroed by a multiply; spec is finite) so all of them are in flight together
 #pragma unroll
-    for (int it = 0; it < WR * 32 / 512; ++it) {
+    for (int it = 0; it < NSP; ++it) {
       const int i = tid + 512 * it, wr = i >> 5, c = (i & 31) * 4;
-      const int Rc = min(max(W0 + wr, 0), rows - 1);
-      const float4 v = *reinterpret_cast<const float4*>(P.spec + (long long)Rc * P.M + min(c, P.M - 4));
       const float m = c < P.M ? 1.f : 0.f;
+      const float4 v = sp4[it];
       *reinterpret_cast<bf16x4*>(&Gs[wr * WST_LD + c]) =
           bf16x4{(__bf16)(v.x * m), (__bf16)(v.y * m), (__bf16)(v.z * m), (__bf16)(v.w * m)};
     }
@@ -426,17 +477,21 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   // (rows outside the batch zeroed by a bit mask, not a select: hipcc turned the select into a
   // branch and waited for each load at its join -- four round trips instead of one, r04)
 #pragma unroll
-  for (int it = 0; it < WR * 32 / 512; ++it) {
+  for (int it = 0; it < NCD; ++it) {
     const int i = tid + it * 512, wr = i >> 5, c = (i & 31) * 8, R = W0 + wr;
-    const uint4 v = *reinterpret_cast<const uint4*>(P.condb + (long long)min(max(R, 0), rows - 1) * H + c);
     const unsigned mk = (R >= 0 && R < rows) ? 0xffffffffu : 0u;
+    const uint4 v = cd4[it];
     *reinterpret_cast<uint4*>(&CW[wr * WST_LD + c]) = make_uint4(v.x & mk, v.y & mk, v.z & mk, v.w & mk);
   }
-  // x (fp32) of the lane's 32 window rows, column n, in registers (the GEMM2 C layout: tile q,
-  // register reg -> window row 32 q + (reg & 3) + 8 (reg >> 2) + 4 h); the skip sums of its 24
-  // rows in [8, 56) (tile 0 regs 4..15 = window rows 8..31, tile 1 regs 0..11 = window rows 32..55),
-  // a superset of the output rows, in LDS, entries only this lane touches
-  float xr[2][16];
+  {   // (the first launch's zero by a bit mask: see the cond staging above)
+    const unsigned mk = P.first ? 0u : 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      const int wrow = skw(i);
+      const unsigned mo = (wrow >= HL && wrow - HL < P.ro) ? mk : 0u;
+      SK[sko(i)] = __uint_as_float(__float_as_uint(skv[i]) & mo);
+    }
+  }
   if constexpr (IN) {
     // x = relu(W_in . bf16(spec) + b_in): the GEMM engine's k order (ldw_in / 16 k-steps)
     bf16x8 wi[8];
@@ -471,32 +526,6 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
         xr[q][reg] = x;
         XW[r * WST_LD + no] = (__bf16)((x + (min(max(R, 0), rows - 1) < RB ? dA0 : dB0)) * m);
       }
-    }
-  }
-  auto skq = [](int i) { return i < 12 ? 0 : 1; };          // SK value i: tile, register
-  auto skr = [](int i) { return i < 12 ? 4 + i : i - 12; };
-  auto skw = [&](int i) { const int reg = skr(i); return 32 * skq(i) + (reg & 3) + 8 * (reg >> 2) + 4 * h; };
-  auto sko = [&](int i) { return (skw(i) - 8) * C + n; };
-  if constexpr (!IN) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int R = W0 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        xr[q][reg] = P.xin[(long long)min(max(R, 0), rows - 1) * C + n];
-      }
-  }
-  {   // (unconditional loads, the first launch's zero by a bit mask: see the cond staging above).
-      // Only this block's output rows [R0, R0 + ro) are read: the window's rows either side of
-      // them belong to the neighbouring blocks, which write them in this launch -- their loads are
-      // clamped into the block's rows and the values masked to zero (they are never stored anyway)
-    const unsigned mk = P.first ? 0u : 0xffffffffu;
-#pragma unroll
-    for (int i = 0; i < 24; ++i) {
-      const int wrow = skw(i), R = W0 + wrow;
-      const unsigned mo = (wrow >= HL && wrow - HL < P.ro) ? mk : 0u;
-      const float sv = P.skip[(long long)min(max(min(max(R, R0), R0 + P.ro - 1), 0), rows - 1) * C + n];
-      SK[sko(i)] = __uint_as_float(__float_as_uint(sv) & mo);
     }
   }
   // conv zero padding: tap t-1 / t+1 of the lane's A rows (window row 32q + r32) outside its
@@ -659,6 +688,24 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
       for (int ks = 0; ks < 16; ++ks) wof[ks] = *reinterpret_cast<const bf16x8*>(P.Wob + (long long)colc * C + ks * 16 + h * 8);
       const float bov = P.bo[colc];
+      // the posterior's operands (x_t, explicit noise, the window's two utterance ids) loaded before
+      // the MFMAs, unconditionally at clamped rows, and the results stored through a buffer resource
+      // whose range check drops the rows this block does not own: with loads and stores under the
+      // row test, every output waited for its own load (r05 asm: 32 round trips per lane)
+      const unsigned uA = utt_id(P.uid, bA), uB = utt_id(P.uid, bB);
+      const float* nzp = P.noise ? P.noise : P.mel;   // a readable array when the noise is drawn here
+      float xt[2][16], zx[2][16];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int R = W0 + 8 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, Rc = min(max(R, 0), rows - 1);
+          const int b = Rc / T, t = Rc - b * T;
+          xt[q][reg] = P.mel[(long long)Rc * M + colc];
+          zx[q][reg] = nzp[P.noise ? (long long)b * P.noise_bs + (long long)t * P.noise_ld + colc : (long long)Rc * M + colc];
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(P.mel, 0, (unsigned)rows * (unsigned)M * 4u, 0x00020000);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         f32x16 acc;
@@ -671,19 +718,17 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const int wrow = 8 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + wrow;
-          if (wrow >= HL && wrow - HL < P.ro && R < rows && col < M) {
-            // prodiff.py:106-126 (gemm.h EPI_POSTERIOR): x = c1 x0 + c2 x_t + sigma n
-            const int b = R / T, t = R - b * T;
-            const float v = acc[reg] + bov;
-            const float xt = P.mel[(long long)R * M + col];
-            float x = P.c1 * v + P.c2 * xt;
-            if (P.sigma != 0.f) {
-              const float z = P.noise ? P.noise[(long long)b * P.noise_bs + (long long)t * P.noise_ld + col]
-                                      : philox_normal_u(P.seed, utt_id(P.uid, b), (unsigned)(t * M + col), P.stream_id);
-              x += P.sigma * z;
-            }
-            P.mel[(long long)R * M + col] = x;
+          const bool ok = wrow >= HL && wrow - HL < P.ro && R < rows && col < M;
+          // prodiff.py:106-126 (gemm.h EPI_POSTERIOR): x = c1 x0 + c2 x_t + sigma n
+          const int Rc = min(R, rows - 1), b = Rc / T, t = Rc - b * T;
+          const float v = acc[reg] + bov;
+          float x = P.c1 * v + P.c2 * xt[q][reg];
+          if (P.sigma != 0.f) {
+            const float z = P.noise ? zx[q][reg]
+                                    : philox_normal_u(P.seed, Rc < RB ? uA : uB, (unsigned)(t * M + col), P.stream_id);
+            x += P.sigma * z;
           }
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), mrs, ok ? (unsigned)(R * M + col) * 4u : 0xfffffff0u, 0, 0);
         }
       }
     }
@@ -691,13 +736,19 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   // ---- output rows: x (layer l0 + nl's input) and the skip sum (not after a fused tail: the
   //      last layer's x feeds nothing, and the skip sum was consumed here)
   if constexpr (TAIL) return;
+  // (rows and addresses from an opaque copy of the lane's half: computed here, not hoisted into the
+  // prologue and spilled across the layer loop; stores through buffer resources whose range check
+  // drops the rows the block does not own, so no store waits at a branch join)
+  int hq = h;
+  asm volatile("" : "+v"(hq));
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(P.xout, 0, (unsigned)rows * (unsigned)C * 4u, 0x00020000);
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(P.skip, 0, (unsigned)rows * (unsigned)C * 4u, 0x00020000);
 #pragma unroll
   for (int i = 0; i < 24; ++i) {
-    const int wrow = skw(i), R = W0 + wrow;
-    if (R < rows && wrow >= HL && wrow - HL < P.ro) {
-      P.xout[(long long)R * C + n] = xr[skq(i)][skr(i)];
-      P.skip[(long long)R * C + n] = SK[sko(i)];
-    }
+    const int reg = skr(i), wrow = 32 * skq(i) + (reg & 3) + 8 * (reg >> 2) + 4 * hq, R = W0 + wrow;
+    const unsigned off = (R < rows && wrow >= HL && wrow - HL < P.ro) ? (unsigned)(R * C + n) * 4u : 0xfffffff0u;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xr[skq(i)][reg]), xrs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(SK[(wrow - 8) * C + n]), srs, off, 0, 0);
   }
 }
 
@@ -1393,7 +1444,9 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
   const __bf16* Wsb = lookup_bf16(h->Ws);
   const __bf16* Wob = lookup_bf16(h->Wo);
   const bool fuse_in = stack && h->stack_fuse && Winb && h->ldw_in <= 128 && M % 4 == 0;
-  const bool fuse_tail = fuse_in && tail && Wsb && Wob && M <= 8 * 32 && C == WNF_C && Ly > h->stack_nl;
+  // (the fused tail stores mel through a buffer resource: 32-bit byte offsets)
+  const bool fuse_tail = fuse_in && tail && Wsb && Wob && M <= 8 * 32 && C == WNF_C && Ly > h->stack_nl &&
+                         (long long)B * T * M * 4 < (1ll << 31) && (long long)B * T * C * 4 < (1ll << 31);
   if (!fuse_in) {  // x = relu(W_in spec + b)   (wavenet.py:108-111)
     GemmArgs a = make_gemm(B, T, C, h->Win, h->ldw_in, h->b_in, x, BTs * C, C);
     add_seg(a, make_seg(xin, BTs * M, M, M, 0));
