@@ -863,14 +863,17 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
     // the exp2 arguments.  z = x + a lives in registers: x_{l+1} = z_l + o, and
     // z_{l+1} = x_{l+1} + a except after the last layer.
     const f32x2 cg = {-LOG2E, -LOG2E}, cf = {2.f * LOG2E, 2.f * LOG2E};
-    auto gate_update = [&](int j, const f32x16& g, const f32x16& f, const float* bq, bool live) {
+    // bb: the frame's gate / filter biases (bb[i], bb[4 + i]: channels 8i + 4h ..), loaded by the
+    // caller all at once -- null when they are folded into the accumulators (PF).  r05: read here, one
+    // pair per channel group, they were four L2 round trips in a row per tile and layer (SUB asm)
+    auto gate_update = [&](int j, const f32x16& g, const f32x16& f, const float4* bb, bool live) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         f32x2 gs0 = {g[4 * i], g[4 * i + 1]}, gs1 = {g[4 * i + 2], g[4 * i + 3]};
         f32x2 fs0 = {f[4 * i], f[4 * i + 1]}, fs1 = {f[4 * i + 2], f[4 * i + 3]};
-        if (bq) {   // bias not folded into the accumulators yet
-          const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
-          const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
+        if (bb) {   // bias not folded into the accumulators yet
+          const float4 bg = bb[i];
+          const float4 bl = bb[4 + i];
           gs0 = efma(f32x2{bg.x, bg.y}, cg, gs0);
           gs1 = efma(f32x2{bg.z, bg.w}, cg, gs1);
           fs0 = efma(f32x2{bl.x, bl.y}, cf, fs0);
@@ -986,7 +989,14 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
         }
         // hop < 32: a tile can straddle the utterance end; rows past it stay zero
         // (they are the next layer's conv padding)
-        gate_update(j, g, f, bq, !SUB || ts + n < Le);
+        float4 bb[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          bb[i] = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
+          bb[4 + i] = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // all eight in flight together
+        gate_update(j, g, f, bb, !SUB || ts + n < Le);
       }
     }
     }
@@ -1598,6 +1608,11 @@ __global__ __launch_bounds__(KP_THREADS, 1) void kp_kernel_bf16_kernel(const __b
     if (ng != ng_cur) {   // wave-uniform; once or twice per block
       w_load(ng);
       ng_cur = ng;
+      // wait for the weight fragments HERE: otherwise the waitcnt pass cannot tell at the loop's
+      // merge point whether wa is still in flight, and waits before its first MFMAs in EVERY item --
+      // with vmcnt retiring in order, for all of the previous item's K stores too (r05: a store
+      // drain per item; the asm had vmcnt(7) / vmcnt(6) inside the first frame tile's MFMAs)
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     }
     h_load(min(item + 1, ie - 1));   // the next item's frames, under this item's work
     const int nb = ng * KP_NG + wave * 64, layer = nb / KPERLAYER, n0 = nb - layer * KPERLAYER;
