@@ -196,6 +196,7 @@ TAG_KERNEL = {
     "wn_gate2": ("wn_gate_bf16_kernel",),
     "wn_resskip2": ("wn_resskip_bf16_kernel",),
     "nsf_pair": ("nsf_pair_kernel<",),
+    "nsf_pair16": ("nsf_pair16_kernel<",),
     "nsf_res": ("nsf_wconv_kernel<",),
     "nsf_ups": ("nsf_ups_kernel<",),
 }
@@ -313,6 +314,7 @@ def nsf_stage_dims(h=None):
 
 
 NSF_PAIR_C = (32, 64, 128)     # ResBlock1 conv pairs fused into one nsf_pair launch (bf16, NSF_OPT_PAIR)
+NSF_PAIR16_C = (16,)           # ... and into one nsf_pair16 launch (bf16, NSF_OPT_PAIR16, r05)
 NSF_KS = (3, 7, 11)            # resblock kernel sizes; 3 dilation pairs each (ResBlock1)
 NSF_HOP, NSF_MELS, NSF_C0, NSF_HARM = 512, 128, 512, 9
 
@@ -333,18 +335,20 @@ def svs_tables(B, T, Tt, dtype, small_max=16, H=256, k_ffn=9):
     rows = B * Tt
     st = nsf_stage_dims()
     paired = [(r, c) for r, c in st if dtype == "bf16" and c in NSF_PAIR_C]
-    single = [(r, c) for r, c in st if (r, c) not in paired]
+    paired16 = [(r, c) for r, c in st if dtype == "bf16" and c in NSF_PAIR16_C]
+    single = [(r, c) for r, c in st if (r, c) not in paired and (r, c) not in paired16]
     fl, by = {}, {}
     # pair (k, d): c1 (k, dil d) and c2 (k, dil 1) over F r rows; x read once (fp32), the pair's
     # output written once (fp32), the last pair of resblocks 1, 2 also reads + writes the ResBlock sum
-    pf, pb = [], []
-    for r, c in paired:
-        for k in NSF_KS:
-            for q in range(3):
-                pf.append(2 * 2 * F * r * c * c * k)
-                acc = q == 2 and k != NSF_KS[0]
-                pb.append(F * r * c * 4 * (2 + (1 if acc else 0)) + 2 * c * c * k * wb)
-    fl["nsf_pair"], by["nsf_pair"] = _mean(pf), _mean(pb)
+    for tag, stages in (("nsf_pair", paired), ("nsf_pair16", paired16)):
+        pf, pb = [], []
+        for r, c in stages:
+            for k in NSF_KS:
+                for q in range(3):
+                    pf.append(2 * 2 * F * r * c * c * k)
+                    acc = q == 2 and k != NSF_KS[0]
+                    pb.append(F * r * c * 4 * (2 + (1 if acc else 0)) + 2 * c * c * k * wb)
+        fl[tag], by[tag] = _mean(pf), _mean(pb)
     for tag, sel in (("nsf_res", lambda c: c > small_max), ("nsf_res_small", lambda c: c <= small_max)):
         cf, cb = [], []
         for r, c in single:
