@@ -576,6 +576,9 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
   // loads that phase's weights once; otherwise jobs run in chunks of 4 (wfj[q]).
   const bool by_phase = NW % r == 0 && ntj <= 4 * (NW / r);
   bf16x8 wfj[4][4];
+  // (r05: loading these unconditionally -- no wait at the branch join, the whole prologue's loads in
+  // flight together, layer 0's kernel prefetch issued earlier -- measured slower, as r04's fully
+  // batched prologue: final block 471-483 -> 505-514 us, lvc_prologue_batch_ab.txt)
   auto wup_load = [&](int job0) {
     if (by_phase) {
       const __bf16* wa = P.Wup + ((long long)(wave % r) * 32 + n) * 64 + 8 * h;
@@ -1312,7 +1315,7 @@ struct KPArgs {
 // padding.  The halo shrinks by 1 row per conv (9 rows needed, 16 kept).
 __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   constexpr int LDC = 104, LDH = 72;               // 208 B / 144 B rows: conflict-free b128 reads
-  __shared__ __attribute__((aligned(16))) __bf16 Cs[100 * LDC];
+  __shared__ __attribute__((aligned(16))) __bf16 Cs[101 * LDC];   // + a spare row for the staging's overflow items
   __shared__ __attribute__((aligned(16))) __bf16 Hb[3][98 * LDH];   // H0, R0, R1 (+1 zero row each side)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, f0 = blockIdx.x * 64, Tc = A.Tc;
@@ -1323,6 +1326,19 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
   __bf16* hout = A.hout + (long long)z * A.B * Tc * HK;
   float* Bfo = A.Bf + (long long)z * A.B * Tc * (2 * CI * NLY);
 
+  // c' = c + fc_t(e) on frames f0-18 .. f0+81 (channels 80..95 zero).  All loads are issued
+  // before any is used (clamped addresses, masked at the store): one round trip, not ten.  r05:
+  // issued FIRST, ahead of the weight fragments below -- vmcnt retires in order, so staging them
+  // last made the LDS stores wait for every weight load too (the asm: vmcnt(0) after 51 loads)
+  constexpr int NCI = (100 * 24 + 255) / 256;
+  float4 cv[NCI], nv[NCI];
+#pragma unroll
+  for (int u = 0; u < NCI; ++u) {
+    const int i = min(tid + 256 * u, 100 * 24 - 1), p = i / 24, g = min((i - p * 24) * 4, CC - 4);
+    const int f = min(max(f0 - 18 + p, 0), Tc - 1);
+    cv[u] = *reinterpret_cast<const float4*>(A.condT + (rb + f) * CC + g);
+    nv[u] = *reinterpret_cast<const float4*>(nzrow + g);
+  }
   // Stage 0's weight fragments (30 k-steps; both of a wave's jobs use column tile wave & 1)
   // run through a KH0-deep register ring, primed here so the first ones land with the
   // staging loads: a load right before each MFMA made stage 0 thirty L2 round trips per job.
@@ -1346,29 +1362,21 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk) bwn[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 16);
   }
-  // c' = c + fc_t(e) on frames f0-18 .. f0+81 (channels 80..95 zero).  All loads are issued
-  // before any is used (clamped addresses, masked at the store): one round trip, not ten.
-  constexpr int NCI = (100 * 24 + 255) / 256;
-  float4 cv[NCI], nv[NCI];
-#pragma unroll
-  for (int u = 0; u < NCI; ++u) {
-    const int i = min(tid + 256 * u, 100 * 24 - 1), p = i / 24, g = min((i - p * 24) * 4, CC - 4);
-    const int f = min(max(f0 - 18 + p, 0), Tc - 1);
-    cv[u] = *reinterpret_cast<const float4*>(A.condT + (rb + f) * CC + g);
-    nv[u] = *reinterpret_cast<const float4*>(nzrow + g);
-  }
+  __builtin_amdgcn_sched_barrier(0);   // every load above in flight before the staging stores
+  // (branch-free: items past the 100 rows go to a spare row, padding is masked -- with the stores
+  // and conversions under `if`, hipcc sank the last item's loads into the branch and waited there
+  // for every load in flight, r05 asm)
 #pragma unroll
   for (int u = 0; u < NCI; ++u) {
     const int i = tid + 256 * u;
-    if (i < 100 * 24) {
-      const int p = i / 24, g = (i - p * 24) * 4, f = f0 - 18 + p;
-      bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-      if (g < CC && f >= 0 && f < Tv) {
-        const float4 c = cv[u], n = nv[u];
-        v = bf16x4{(__bf16)(c.x + n.x), (__bf16)(c.y + n.y), (__bf16)(c.z + n.z), (__bf16)(c.w + n.w)};
-      }
-      *reinterpret_cast<bf16x4*>(Cs + p * LDC + g) = v;
-    }
+    const bool in = i < 100 * 24;
+    const int p = in ? i / 24 : 100, g = in ? (i - p * 24) * 4 : 0, f = f0 - 18 + p;
+    const unsigned mk = (in && g < CC && f >= 0 && f < Tv) ? 0xffffffffu : 0u;
+    const float4 c = cv[u], n = nv[u];
+    const bf16x4 v = bf16x4{(__bf16)(c.x + n.x), (__bf16)(c.y + n.y), (__bf16)(c.z + n.z), (__bf16)(c.w + n.w)};
+    uint2 vb = __builtin_bit_cast(uint2, v);
+    vb.x &= mk; vb.y &= mk;
+    *reinterpret_cast<uint2*>(Cs + p * LDC + g) = vb;
   }
   for (int i = tid; i < 3 * 2 * LDH; i += 256) {   // zero guard rows 0 and 97
     const int buf = i / (2 * LDH), j = i - buf * 2 * LDH;
