@@ -463,7 +463,7 @@ def port_cpu_baseline(frames, vocoder=True):
             "rtf": round(dt / audio_s, 4)}
 
 
-def denoiser_roofline(kern_all, nprof, B, T, cfg, dtype, peak_tf, cfg_name):
+def denoiser_roofline(kern_all, nprof, B, T, cfg, dtype, peak_tf, cfg_name, pmc_key=None):
     """The north star's denoiser figure: the WaveNet residual stack (every launch of the ProDiff
     sampler's denoiser, tags DENOISER_TAGS) against the MFMA roof at its algorithmic FLOPs
     (26.43 MFLOP per mel frame per pass at M = 80), and -- where a PMC summary of
@@ -481,7 +481,9 @@ def denoiser_roofline(kern_all, nprof, B, T, cfg, dtype, peak_tf, cfg_name):
            "flop_per_step": passes * prodiff_step_flops(B, T, M=M),
            "timing": "the untimed all-launch pass (HIP events around every launch)"}
     if "wn_stack" in kern_all:
-        tb, src, tlib = pmc_traffic("wn_stack", cfg_name, B, T)
+        # pmc_key: the (per-launch batch, frames) the PMC summaries are keyed by (B, T here are the
+        # rank's totals, the FLOP count's basis)
+        tb, src, tlib = pmc_traffic("wn_stack", cfg_name, *(pmc_key or (B, T)))
         if tb:
             cnt, sms = kern_all["wn_stack"]
             gbs = tb * cnt / (sms * 1e-3) / 1e9
@@ -521,6 +523,9 @@ def main():
                     help="ds: the reference song's 30 segment lengths (and phoneme counts) per GPU "
                          "(tests/golden/ds_lengths.json, from samples/00_*.ds), run as ragged batches")
     ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline_port sample length (0 = skip)")
+    ap.add_argument("--max-frames", type=int, default=0,
+                    help="cap on a ragged batch's padded frames (0 = none): a rank's utterances then run as "
+                         "several batches on concurrent HIP streams")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
                     help="compute dtype (default: the config's; fp32 is the exact parity path)")
     ap.add_argument("--no-graph", action="store_true", help="C2: launch eagerly instead of replaying a hipGraph")
@@ -586,7 +591,7 @@ def main():
     mine = shards[rank]
     B = len(mine)                                           # utterances this rank runs per step
     F_rank = sum(lengths[i] for i in mine)
-    n_batches = max(1, len(ragged_batches(lengths, mine)))
+    n_batches = max(1, len(ragged_batches(lengths, mine, max_frames=args.max_frames or None)))
     rng = np.random.default_rng(1000 + rank)
     conds = [(L_, None) for L_ in lengths]
     from prodiff_amd import synth as _synth
@@ -628,7 +633,8 @@ def main():
     if cfg["vocoder"]:
         def step(i, timed=False):
             st = {} if (timed and world > 1) else None
-            out = distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop, stats=st)
+            out = distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop, stats=st,
+                                         max_frames=args.max_frames or None)
             if st:
                 phase["compute_ms"] += st["compute_ms"]
                 phase["gather_ms"] += st["gather_ms"]
@@ -651,7 +657,7 @@ def main():
     # batch, F_rank / n_batches real frames (padding is not algorithmic work)
     ds_mode = args.lengths == "ds"
     wl_name = cfg_name + ("DS" if ds_mode else "")        # workload key of the PMC / SQ summaries
-    Bl = B / n_batches if ds_mode else B
+    Bl = B / n_batches
     Tl = F_rank / B if ds_mode else T
     if svs:
         fl = flops_per_launch(Bl, Tl, dtype, M=128)
@@ -771,7 +777,8 @@ def main():
             ach = fl[dom] * cnt / sec / 1e12
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf, "unit": "TFLOP/s",
                         "frac": round(ach / peak_tf, 4)}
-        traffic, tsrc, tlib = pmc_traffic(dom, wl_name, B, T, args.traffic)
+        # keyed by a launch's batch (a split batch's launches cover B / n_batches utterances)
+        traffic, tsrc, tlib = pmc_traffic(dom, wl_name, B if ds_mode else int(Bl), T, args.traffic)
         roofline.update({"bound_basis": "model estimate: algorithmic intensity vs the ridge; the measured limiter "
                                         "is in `utilisation` (MFMA / VALU busy, wait fractions)",
                          "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
@@ -783,7 +790,8 @@ def main():
                          "timing": ("HIP events around this kernel only, over untimed eager runs of the same "
                                     "sampler (the timed steps replay a hipGraph)") if graph_prof else
                                    "HIP events around this kernel only, over the timed steps"})
-        roofline["denoiser"] = denoiser_roofline(kern_all, nprof, 1, F_rank, cfg, dtype, peak_tf, wl_name)
+        roofline["denoiser"] = denoiser_roofline(kern_all, nprof, 1, F_rank, cfg, dtype, peak_tf, wl_name,
+                                                 pmc_key=(B if ds_mode else int(Bl), T))
     if svs:
         step_fl = svs_step_flops(n_total, sum(lengths) / n_total, sum(tokens) / n_total)
     else:
@@ -813,6 +821,7 @@ def main():
                    f"ragged: the reference song's {nb} segments per GPU ({min(lengths)}..{max(lengths)} frames, "
                    f"{sum(lengths[i] for i in mine)} per GPU; samples/00_*.ds via tests/golden/ds_lengths.json), "
                    f"{n_batches} padded batches per GPU (ragged_batches, <= 15% padding)",
+                   "batches_per_gpu": n_batches,
                    "parallelism": f"dp{world} (utterance shards, RCCL gather to rank 0)" if cfg["vocoder"]
                    else "single GPU" + ("" if args.no_graph else ", hipGraph replay")},
         "rtf": round(dt / audio_s, 6),

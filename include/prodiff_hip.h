@@ -334,6 +334,10 @@ size_t nsf_workspace_size(const nsf_model* m, int B, int T);
 /* NSF_OPT_PAIR16: 1 (default) runs the 16-channel ResBlock1 pairs of the shipped shapes (taps 3/7/11,
  * dilation 1/3/5) the same way, on 16x16x32 MFMAs; 0 = two launches for them.  Needs NSF_OPT_PAIR. */
 #define NSF_OPT_PAIR16 3
+/* NSF_OPT_UPS_NC: 1 (default) lets the bf16 windowed upsample compute the noise conv of its stage itself when
+ * the source kernel has at most 8 taps (the last three stages) instead of reading nsf_noise_conv's output;
+ * 0 = always the separate noise conv.  Same fp32 operations in the same order. */
+#define NSF_OPT_UPS_NC 4
 int nsf_set_option(nsf_model* m, int option, int value);
 
 /* spec2wav_torch(mel, f0=f0) for a batch of independent utterances:

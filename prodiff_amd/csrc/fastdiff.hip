@@ -1516,6 +1516,10 @@ __global__ __launch_bounds__(256) void kp_hidden_bf16_kernel(const KPArgs A) {
 // ran ~77 us for its GEMM alone and ~86 us for its stores alone (profiles/r03_ab/kp_kernel_ab.txt).
 // A lane of C holds 4 consecutive kernel values of one frame; a per-wave LDS transpose turns
 // them into 128-B row segments (8 frames per 1-KiB store: 6.0 TB/s in tools/store_probe.hip).
+// r05, measured and not kept (profiles/r05_ab/kp_units_w4_ab.txt): each h row staged once (130 rows
+// per item, the tap-0 / tap-2 fragments masked at utterance edges: 76 KB of LDS instead of 141) with
+// the work dealt as equal runs of 32-frame tiles (C3's 128-frame items fall 10 or 11 per block): 85-87
+// vs 84-85 us; the same as two 4-wave blocks per CU, each with its own barrier phase: 86-87 us.
 constexpr int KP_F = 128, KP_NG = 512, KP_LDH = 200;   // 400-B LDS rows: conflict-free b128 reads
 // Output transpose tile.  KP_SWZ 0 (default): 32 frames x (64 + 8 pad) bf16 rows (144 B: 16-B aligned
 // for the b128 reads; 68 measured 15% slower).  KP_SWZ 1 (r05 A/B): unpadded 128-B rows with an XOR

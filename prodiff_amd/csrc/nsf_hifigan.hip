@@ -62,6 +62,7 @@ struct nsf_model {
   bool ups_window = true;        // NSF_OPT_WCONV also selects the windowed ConvTranspose
   bool pair = true;              // NSF_OPT_PAIR: a ResBlock1 conv pair in one launch (nsf_pair_kernel)
   bool pair16 = true;            // NSF_OPT_PAIR16: the C = 16 pairs too (nsf_pair16_kernel), with pair
+  bool ups_nc = true;            // NSF_OPT_UPS_NC: the windowed upsample computes short noise convs itself
   int convs_per_block = 0;
 };
 
@@ -1020,12 +1021,25 @@ __global__ __launch_bounds__(256) void nsf_post_kernel(const float* __restrict__
 // input 2u times); weights of all phases are contiguous [phi][cout][ntap*kpad] (bf16 mirror),
 // streamed in a PF-deep register ring across the phase boundaries.  NPAD: cout < 32 channels
 // on a 32-wide tile (weight rows clamped, extra columns dropped).
-template <int CIN, int FM, int FN, int WM, int WN, bool NPAD>
+// The noise conv (models.py:271-272: Conv1d(1, cout, k = 2s, stride s, padding s / 2) of the
+// harmonic source) fused into the upsample's epilogue (r05, NC): the block stages its rows' source
+// samples in LDS after the input window and adds b + sum_j w[j] har[R s - pad + j] -- the order of
+// nsf_noise_conv_kernel -- where the unfused path reads that kernel's fp32 output back.
+struct NsfNoise {
+  const float* har = nullptr;   // [B][L] harmonic source
+  long long L = 0;
+  const float* w = nullptr;     // tap-major [k][cout]
+  const float* b = nullptr;
+  int k = 0, stride = 1, pad = 0;
+  NsfRag rag;                   // the source's ragged ends (rate = samples per frame)
+};
+constexpr int NSF_NC_KMAX = 8;   // fused for k <= 8 (the last three stages: LDS of the source window)
+template <int CIN, int FM, int FN, int WM, int WN, bool NPAD, bool NC = false>
 __global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict__ in, const __bf16* __restrict__ w,
                                                       long long wstride, int kpad, int ntap, int u, int p, int dlo,
                                                       int cout, const float* __restrict__ bias, float alpha,
                                                       float scale, int Tin, const float* __restrict__ res,
-                                                      float* __restrict__ out, NsfRag rag_) {
+                                                      float* __restrict__ out, NsfRag rag_, NsfNoise nz) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN, LDA = CIN + 8, KS = CIN / 16;
   constexpr int PF = KS >= NSF_PF ? NSF_PF : KS;
@@ -1034,6 +1048,28 @@ __global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict
   const int wm = wave % WM, wn = wave / WM;
   const int b = blockIdx.z, i0 = blockIdx.x * TQ, n0 = blockIdx.y * TN;
   const int W = TQ + ntap;                 // rows i0 + dlo ... (dlo = 1 - ntap, top offset q0 <= 1)
+  // NC: source samples [s0, s0 + nwin) of output rows [i0 u, (i0 + TQ) u), after the input window
+  float* s_har = reinterpret_cast<float*>(nsf_uwin + ((W + 1) * LDA + 7) / 8 * 8);
+  const long long s0 = (long long)i0 * u * nz.stride - nz.pad;
+  const int nwin = NC ? TQ * u * nz.stride + nz.k : 0;
+  if constexpr (NC) {
+    const float* hb = nz.har + (long long)b * nz.L;
+    const long long Lv = nz.rag.lens ? min((long long)nz.rag.lens[b] * nz.rag.rate, nz.L) : nz.L;
+    for (int base = tid; base < nwin; base += 256 * 8) {   // 8 loads per thread in flight together
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const long long si = s0 + base + 256 * e;
+        v[e] = hb[si < 0 ? 0 : si >= nz.L ? nz.L - 1 : si];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = base + 256 * e;
+        const long long si = s0 + i;
+        s_har[min(i, nwin)] = (si >= 0 && si < Lv && i < nwin) ? v[e] : 0.f;   // (slot nwin: spare)
+      }
+    }
+  }
   stage_window<CIN, false>(in, b, Tin, nsf_tv(rag_, b, Tin), i0 + dlo, W, alpha, scale, nsf_uwin, LDA, tid);
   __syncthreads();
   const int r32 = lane & 31, h = lane >> 5;
@@ -1104,10 +1140,27 @@ __global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict
         const int n = n0 + (wn * FN + j) * 32 + r32;
         const int nc = NPAD ? min(n, cout - 1) : n;
         float rv[16];
+        if constexpr (NC) {   // the noise conv of output row o + q u, nsf_noise_conv_kernel's order
+          float wv[NSF_NC_KMAX];
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int q = min(i0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tin - 1);
-          rv[reg] = res[((long long)b * Lc + o + (long long)q * u) * cout + nc];
+          for (int jj = 0; jj < NSF_NC_KMAX; ++jj) wv[jj] = nz.w[(long long)min(jj, nz.k - 1) * cout + nc];
+          const float bo = nz.b[nc];
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int q = min(i0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tin - 1);
+            const float* sh = s_har + (o + (q - i0) * u) * nz.stride;
+            float acc = bo;
+#pragma unroll
+            for (int jj = 0; jj < NSF_NC_KMAX; ++jj)
+              if (jj < nz.k) acc = fmaf(wv[jj], sh[jj], acc);   // (uniform)
+            rv[reg] = acc;
+          }
+        } else {
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int q = min(i0 + wm * FM * 32 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, Tin - 1);
+            rv[reg] = res[((long long)b * Lc + o + (long long)q * u) * cout + nc];
+          }
         }
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
@@ -1122,19 +1175,30 @@ __global__ __launch_bounds__(256, 2) void nsf_ups_kernel(const float* __restrict
 
 template <int CIN, int FM, int FN, int WM, int WN, bool NPAD>
 int launch_ups_c(const NsfUps& U, const __bf16* wb, const float* in, float scale, int B, int Tin, const float* res,
-                 float* out, hipStream_t st, NsfRag rag_) {
+                 float* out, hipStream_t st, NsfRag rag_, const NsfNoise& nz) {
   constexpr int TQ = 32 * FM * WM, TN = 32 * FN * WN;
   const int p = (U.k - U.u) / 2;
-  const size_t lds = (size_t)(TQ + U.ntap + 1) * (CIN + 8) * sizeof(__bf16);   // + stage_window's spare row
+  // input window + stage_window's spare row (+ NC: the source window and its spare slot)
+  const size_t win = (size_t)((U.ntap + TQ + 1) * (CIN + 8) + 7) / 8 * 8 * sizeof(__bf16);
+  const size_t lds = win + (nz.har ? (size_t)(TQ * U.u * nz.stride + nz.k + 1) * sizeof(float) : 0);
   static const hipError_t attr = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD>),
       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (attr != hipSuccess) { set_error("nsf ups: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
+  static const hipError_t attr_nc = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD, true>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess || attr_nc != hipSuccess) { set_error("nsf ups: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
+  if (lds > 160 * 1024) { set_error("nsf ups: LDS window too large"); return PD_ERR_UNSUPPORTED; }
   dim3 grid(cdiv(Tin, TQ), NPAD ? 1 : U.cout / TN, B);
   ProfScope ps("nsf_ups", st);
-  hipLaunchKernelGGL((nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD>), grid, dim3(256), lds, st, in, wb,
-                     (long long)(U.w[1] - U.w[0]), U.kpad, U.ntap, U.u, p, 1 - U.ntap, U.cout, U.b, NSF_LRELU,
-                     scale, Tin, res, out, rag_);
+  if (nz.har)
+    hipLaunchKernelGGL((nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD, true>), grid, dim3(256), lds, st, in, wb,
+                       (long long)(U.w[1] - U.w[0]), U.kpad, U.ntap, U.u, p, 1 - U.ntap, U.cout, U.b, NSF_LRELU,
+                       scale, Tin, res, out, rag_, nz);
+  else
+    hipLaunchKernelGGL((nsf_ups_kernel<CIN, FM, FN, WM, WN, NPAD>), grid, dim3(256), lds, st, in, wb,
+                       (long long)(U.w[1] - U.w[0]), U.kpad, U.ntap, U.u, p, 1 - U.ntap, U.cout, U.b, NSF_LRELU,
+                       scale, Tin, res, out, rag_, nz);
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -1158,14 +1222,14 @@ bool ups_window_ok(const NsfUps& U, bool wconv) {
 }
 
 int launch_ups_window(const NsfUps& U, const float* in, float scale, int B, int Tin, const float* res, float* out,
-                      hipStream_t st, NsfRag rag_) {
+                      hipStream_t st, NsfRag rag_, const NsfNoise& nz) {
   const __bf16* wb = lookup_bf16(U.w[0]);
   // (r02: one row-wave per column tile, <512,2,1,1,4> / <256,4,1,1,4>, measured slower: 188 vs 178 us avg)
-  if (U.cin == 512) return launch_ups_c<512, 1, 2, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_);
-  if (U.cin == 256) return launch_ups_c<256, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_);
-  if (U.cin == 128) return launch_ups_c<128, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_);
-  if (U.cin == 64) return launch_ups_c<64, 1, 1, 4, 1, false>(U, wb, in, scale, B, Tin, res, out, st, rag_);
-  return launch_ups_c<32, 1, 1, 4, 1, true>(U, wb, in, scale, B, Tin, res, out, st, rag_);
+  if (U.cin == 512) return launch_ups_c<512, 1, 2, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_, nz);
+  if (U.cin == 256) return launch_ups_c<256, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_, nz);
+  if (U.cin == 128) return launch_ups_c<128, 2, 1, 2, 2, false>(U, wb, in, scale, B, Tin, res, out, st, rag_, nz);
+  if (U.cin == 64) return launch_ups_c<64, 1, 1, 4, 1, false>(U, wb, in, scale, B, Tin, res, out, st, rag_, nz);
+  return launch_ups_c<32, 1, 1, 4, 1, true>(U, wb, in, scale, B, Tin, res, out, st, rag_, nz);
 }
 
 template <int C, int FM, int FN, int WM, int WN>
@@ -1519,6 +1583,11 @@ int nsf_set_option(nsf_model* m, int option, int value) {
     m->pair = value != 0;
     return PD_OK;
   }
+  if (option == NSF_OPT_UPS_NC) {
+    PD_CHECK_ARG(value == 0 || value == 1, "NSF_OPT_UPS_NC is 0 or 1");
+    m->ups_nc = value != 0;
+    return PD_OK;
+  }
   if (option == NSF_OPT_PAIR16) {
     PD_CHECK_ARG(value == 0 || value == 1, "NSF_OPT_PAIR16 is 0 or 1");
     m->pair16 = value != 0;
@@ -1582,7 +1651,15 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
   for (int i = 0; i < d.num_upsamples; ++i) {
     const NsfUps& U = m->ups[i];
     const int Lc = Tin * U.u;
-    {
+    const bool upsw = ups_window_ok(U, m->ups_window);
+    // NSF_OPT_UPS_NC: the windowed upsample computes the noise conv itself (short source kernels:
+    // the last three stages); otherwise nsf_noise_conv_kernel writes it for the upsample to add
+    NsfNoise nz;
+    if (upsw && m->ups_nc && U.nc_k <= NSF_NC_KMAX) {
+      nz.har = har; nz.L = L; nz.w = U.nc_w; nz.b = U.nc_b;
+      nz.k = U.nc_k; nz.stride = U.nc_stride; nz.pad = U.nc_pad; nz.rag = rag(m->upp);
+    }
+    if (!nz.har) {
       const int CT = U.cout < 256 ? U.cout : 256, G = 256 / CT;
       const size_t lds = (size_t)((G * NC_ROWS - 1) * U.nc_stride + U.nc_k) * sizeof(float);
       ProfScope ps("nsf_noise_conv", st);
@@ -1593,8 +1670,7 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
     // x = ups(leaky_relu(x, 0.1)) + noise_conv(har)  (models.py:270-274): the windowed bf16
     // kernel, or one GEMM per phase
     const int p = (U.k - U.u) / 2;
-    const bool upsw = ups_window_ok(U, m->ups_window);
-    if (upsw) PD_TRY(launch_ups_window(U, XS, in_scale, B, Tin, XSRC, X, st, rag(Tin / T)));
+    if (upsw) PD_TRY(launch_ups_window(U, XS, in_scale, B, Tin, XSRC, X, st, rag(Tin / T), nz));
     for (int phi = 0; phi < (upsw ? 0 : U.u); ++phi) {
       const int q0 = U.qmin[phi];
       const int o = q0 * U.u + phi - p;        // first output row of this phase, in [0, u)

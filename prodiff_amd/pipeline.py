@@ -285,7 +285,7 @@ def _default_collate(items):
 
 
 def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None,
-                           collectives=False, max_waste=0.15, streams=4):
+                           collectives=False, max_waste=0.15, streams=4, max_frames=None):
     """Synthesize utterances sharded over the ranks of the default process group
     (SURVEY §8(e)); the reference runs them one by one, B=1 per segment
     (handler/infer/handler.py:373-388).
@@ -314,7 +314,10 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     ``streams``: a shard of several ragged batches runs them side by side on up to this many HIP
     streams (each with its own workspaces, ``_lib.Workspace``): a long utterance alone in its batch
     fills a fraction of the GPU (the WaveNet stack puts 32 frames on a CU), so it overlaps the
-    others instead of running after them.  1 = one after the other on the current stream."""
+    others instead of running after them.  1 = one after the other on the current stream.
+    ``max_frames``: cap on a batch's padded frames (``ragged_batches``); a shard split into several
+    batches runs them on the streams side by side, so one batch's low-occupancy launches (the
+    WaveNet stack puts 44 frames on a CU) overlap another's."""
     import time
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -323,7 +326,7 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     mel_parts, wav_parts = [], []
     M = getattr(synth_fn, "mel_bins", None)
     collate = getattr(synth_fn, "collate", _default_collate)
-    plans = [ragged_batches(lengths, s, max_waste) for s in shards]
+    plans = [ragged_batches(lengths, s, max_waste, max_frames) for s in shards]
 
     def sync():
         if stats is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
@@ -361,6 +364,19 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         for mel, wav, _, _ in outs:     # made on a side stream, read (and freed) on the current one
             mel.record_stream(cur)
             wav.record_stream(cur)
+    if world == 1 and not (collectives and dist.is_initialized()):
+        # one rank, no gather: each utterance's outputs are views of its batch (no flatten / cat
+        # copies of the whole job on the device)
+        mels, wavs = [None] * len(lengths), [None] * len(lengths)
+        for (mel, wav, lens, T), (_, idx) in zip(outs, plan):
+            for r, (i, n) in enumerate(zip(idx, lens)):
+                mels[i] = mel[r, :n]
+                wavs[i] = wav[r, :n * hop]
+        sync()
+        if stats is not None:
+            stats["compute_ms"] = (time.perf_counter() - t0) * 1e3
+            stats["gather_ms"] = 0.0
+        return mels, wavs
     for mel, wav, lens, T in outs:
         M = mel.shape[-1]
         if all(n == T for n in lens):

@@ -128,6 +128,20 @@ def test_distributed_synthesize_ragged(world, lengths):
         np.testing.assert_array_equal(g[r], np.full((r + 1, 2 + r), float(r)))
 
 
+@pytest.mark.parametrize("max_frames", [None, 20, 9])
+def test_distributed_synthesize_max_frames_one_rank(max_frames):
+    """One rank (no process group): a frame cap splits the shard into several batches (run side
+    by side on streams on a GPU); every utterance still comes back in input order, equal to
+    running it alone."""
+    lengths = [5, 9, 3, 7, 7, 2, 9]
+    conds = _conds(lengths)
+    mels, wavs = distributed_synthesize(stub_synth, conds, hop=HOP, max_frames=max_frames)
+    for i, c in enumerate(conds):
+        em, ew = stub_synth(c[None], 0, utt_ids=[i])
+        np.testing.assert_array_equal(mels[i].numpy(), em[0].numpy())
+        np.testing.assert_array_equal(wavs[i].numpy(), ew[0].numpy())
+
+
 def test_bench_self_launches_n_ranks_dry_run():
     """`bench.py --gpus 2` without torchrun spawns 2 ranks itself (CPU dry run: gloo,
     stub synthesis, no GPU) and rank 0 reports n_gpus 2."""
