@@ -27,6 +27,7 @@ Rank 0 prints ONE JSON line.  Synthetic inputs and random-init weights of the
 reference architectures (no checkpoints or datasets offline).
 """
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -523,6 +524,8 @@ def main():
                     help="ds: the reference song's 30 segment lengths (and phoneme counts) per GPU "
                          "(tests/golden/ds_lengths.json, from samples/00_*.ds), run as ragged batches")
     ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline_port sample length (0 = skip)")
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="jobs in flight: step i runs on HIP stream i %% N, so consecutive jobs overlap")
     ap.add_argument("--max-frames", type=int, default=0,
                     help="cap on a ragged batch's padded frames (0 = none): a rank's utterances then run as "
                          "several batches on concurrent HIP streams")
@@ -631,10 +634,21 @@ def main():
     phase = {"compute_ms": 0.0, "gather_ms": 0.0, "n": 0}    # N > 1: where each timed step went
 
     if cfg["vocoder"]:
+        ovl = None
+        if args.overlap > 1 and not dry:
+            # consecutive jobs on alternating HIP streams: one job's low-occupancy launches (the
+            # ProDiff WaveNet stack fills 157 of 256 CUs at C3) overlap the previous job's vocoder
+            if getattr(synth_fn, "prepare", None):
+                synth_fn.prepare()
+            torch.cuda.synchronize()
+            ovl = [torch.cuda.Stream(dev) for _ in range(args.overlap)]
+
         def step(i, timed=False):
             st = {} if (timed and world > 1) else None
-            out = distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop, stats=st,
-                                         max_frames=args.max_frames or None)
+            ctx = torch.cuda.stream(ovl[i % len(ovl)]) if ovl else contextlib.nullcontext()
+            with ctx:
+                out = distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop, stats=st,
+                                             max_frames=args.max_frames or None)
             if st:
                 phase["compute_ms"] += st["compute_ms"]
                 phase["gather_ms"] += st["gather_ms"]
@@ -822,6 +836,7 @@ def main():
                    f"{sum(lengths[i] for i in mine)} per GPU; samples/00_*.ds via tests/golden/ds_lengths.json), "
                    f"{n_batches} padded batches per GPU (ragged_batches, <= 15% padding)",
                    "batches_per_gpu": n_batches,
+                   "jobs_in_flight": args.overlap if cfg["vocoder"] else 1,
                    "parallelism": f"dp{world} (utterance shards, RCCL gather to rank 0)" if cfg["vocoder"]
                    else "single GPU" + ("" if args.no_graph else ", hipGraph replay")},
         "rtf": round(dt / audio_s, 6),

@@ -121,3 +121,26 @@ def test_bf16_resblock_pair_bitexact(T, B):
         outs.append(g.synthesize(mel, f0, 2.30259, seed=9).cpu().numpy())
     assert np.isfinite(outs[1]).all()
     np.testing.assert_array_equal(outs[1], outs[0])
+
+
+@pytest.mark.parametrize("T,B,lens", [(24, 1, None), (37, 2, [37, 21]), (1, 3, None)])
+def test_bf16_ups_noise_conv_fused_bitexact(T, B, lens):
+    """NSF_OPT_UPS_NC (the k <= 8 noise convs computed in the upsample's epilogue from a source
+    window in LDS) against the separate nsf_noise_conv_kernel launches: same fp32 tap order, so
+    the waveform is bit-identical -- partial tiles, T = 1, and a ragged row (its source reads zero
+    past its own end)."""
+    h = dict(synth.NSF_DEFAULTS)
+    g, _ = _gen(h, 7)
+    rng = np.random.default_rng(6)
+    mel = torch.from_numpy(rng.normal(-2.0, 1.0, size=(B, T, 128)).astype(np.float32)).to(DEV)
+    f0 = torch.from_numpy(rng.uniform(60.0, 900.0, size=(B, T)).astype(np.float32)).to(DEV)
+    outs = []
+    for nc in (0, 1):
+        g.set_compute_dtype("bf16").set_options(ups_nc=nc)
+        outs.append(g.synthesize(mel, f0, 2.30259, seed=9, lens=lens).cpu().numpy())
+    assert np.isfinite(outs[1]).all()
+    if lens is None:
+        np.testing.assert_array_equal(outs[1], outs[0])
+    else:
+        for r, n in enumerate(lens):
+            np.testing.assert_array_equal(outs[1][r, :n * g.upp], outs[0][r, :n * g.upp])
