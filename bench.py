@@ -524,8 +524,9 @@ def main():
                     help="ds: the reference song's 30 segment lengths (and phoneme counts) per GPU "
                          "(tests/golden/ds_lengths.json, from samples/00_*.ds), run as ragged batches")
     ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline_port sample length (0 = skip)")
-    ap.add_argument("--overlap", type=int, default=1,
-                    help="jobs in flight: step i runs on HIP stream i %% N, so consecutive jobs overlap")
+    ap.add_argument("--overlap", type=int, default=None,
+                    help="jobs in flight: step i runs on HIP stream i %% N, so consecutive jobs overlap "
+                         "(default: 2 for C3 / C5 on one GPU, else 1)")
     ap.add_argument("--max-frames", type=int, default=0,
                     help="cap on a ragged batch's padded frames (0 = none): a rank's utterances then run as "
                          "several batches on concurrent HIP streams")
@@ -575,7 +576,7 @@ def main():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
 
-    from prodiff_amd.pipeline import distributed_synthesize, lpt_shards
+    from prodiff_amd.pipeline import JobStreams, distributed_synthesize, lpt_shards
 
     # utterance list (all ranks know every length; only the own shard is resident)
     from prodiff_amd.pipeline import ragged_batches
@@ -632,20 +633,25 @@ def main():
         synth_fn = syn
 
     phase = {"compute_ms": 0.0, "gather_ms": 0.0, "n": 0}    # N > 1: where each timed step went
+    ovl = None      # JobStreams when --overlap > 1
+    if args.overlap is None:
+        # jobs in flight: 2 on one GPU for the C3 / C5 lines (measured); 1 with N > 1
+        # ranks (each rank's gather runs on its job's stream) and for C4 (the scaling line)
+        args.overlap = 2 if (world == 1 and cfg_name in ("C3", "C5")) else 1
 
     if cfg["vocoder"]:
-        ovl = None
         if args.overlap > 1 and not dry:
-            # consecutive jobs on alternating HIP streams: one job's low-occupancy launches (the
-            # ProDiff WaveNet stack fills 157 of 256 CUs at C3) overlap the previous job's vocoder
+            # consecutive jobs on alternating HIP streams (pipeline.JobStreams): one job's
+            # low-occupancy launches (the ProDiff WaveNet stack fills 157 of 256 CUs at C3) overlap
+            # the previous job's vocoder.  Handles are packed first (stream-ordered packing).
             if getattr(synth_fn, "prepare", None):
                 synth_fn.prepare()
             torch.cuda.synchronize()
-            ovl = [torch.cuda.Stream(dev) for _ in range(args.overlap)]
+            ovl = JobStreams(args.overlap, dev)
 
-        def step(i, timed=False):
+        def step(i, timed=False, iso=False):
             st = {} if (timed and world > 1) else None
-            ctx = torch.cuda.stream(ovl[i % len(ovl)]) if ovl else contextlib.nullcontext()
+            ctx = ovl.next() if (ovl and not iso) else contextlib.nullcontext()
             with ctx:
                 out = distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop, stats=st,
                                              max_frames=args.max_frames or None)
@@ -696,13 +702,14 @@ def main():
         _lib.profile_filter(None)
         _lib.profile_enable(True)
         for i in range(nprof):
-            step(args.warmup + i)
+            step(args.warmup + i, iso=True)      # one job at a time: per-kernel times unshared
         torch.cuda.synchronize()
         kern_all = _lib.profile_summary()
         _lib.profile_enable(False)
         dom = dominant_kernel(kern_all, fl, by)
-        _lib.profile_filter([dom])
-        _lib.profile_enable(True)
+        if ovl is None:
+            _lib.profile_filter([dom])
+            _lib.profile_enable(True)
     if not dry:
         torch.cuda.synchronize()
     if world > 1:
@@ -717,6 +724,19 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    dt_iso = None
+    if timing and ovl is not None:
+        # jobs in flight share the GPU, so a kernel's launch time in the timed region is not its own:
+        # the roofline's launch time comes from K more steps run one job at a time, HIP events
+        # around the dominant kernel only (and their wall time is reported beside `value`)
+        _lib.profile_filter([dom])
+        _lib.profile_enable(True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            step(args.warmup + nprof + args.steps + i, timed=True, iso=True)
+        torch.cuda.synchronize()
+        dt_iso = time.perf_counter() - t1
     kern = _lib.profile_summary() if timing else {}
     if timing:
         _lib.profile_enable(False)
@@ -800,9 +820,12 @@ def main():
                          "flop_per_launch": fl[dom], "bytes_per_launch": by.get(dom),
                          "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(ridge, 1),
                          "avg_launch_us": round(ms / cnt * 1e3, 2), "launches": cnt,
-                         "share_of_step": round(ms / (dt * 1e3), 3),
+                         "share_of_step": round(ms / ((dt_iso or dt) * 1e3), 3),
                          "timing": ("HIP events around this kernel only, over untimed eager runs of the same "
                                     "sampler (the timed steps replay a hipGraph)") if graph_prof else
+                                   ("HIP events around this kernel only, over K steps run one job at a time right "
+                                    f"after the timed region (which keeps {args.overlap} jobs in flight on "
+                                    f"{args.overlap} HIP streams: their kernels share the GPU)") if dt_iso else
                                    "HIP events around this kernel only, over the timed steps"})
         roofline["denoiser"] = denoiser_roofline(kern_all, nprof, 1, F_rank, cfg, dtype, peak_tf, wl_name,
                                                  pmc_key=(B if ds_mode else int(Bl), T))
@@ -836,7 +859,10 @@ def main():
                    f"{sum(lengths[i] for i in mine)} per GPU; samples/00_*.ds via tests/golden/ds_lengths.json), "
                    f"{n_batches} padded batches per GPU (ragged_batches, <= 15% padding)",
                    "batches_per_gpu": n_batches,
-                   "jobs_in_flight": args.overlap if cfg["vocoder"] else 1,
+                   "jobs_in_flight": ovl.depth if ovl is not None else 1,
+                   "one_job_in_flight": None if dt_iso is None else
+                   {"value": round(frames / dt_iso, 1), "ms_per_step": round(dt_iso / args.steps * 1e3, 3),
+                    "note": "the same K steps run one after the other right after the timed region"},
                    "parallelism": f"dp{world} (utterance shards, RCCL gather to rank 0)" if cfg["vocoder"]
                    else "single GPU" + ("" if args.no_graph else ", hipGraph replay")},
         "rtf": round(dt / audio_s, 6),

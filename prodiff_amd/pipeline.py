@@ -284,6 +284,35 @@ def _default_collate(items):
     return torch.stack([torch.nn.functional.pad(c, (0, 0, 0, T - int(c.shape[0]))) for c in items])
 
 
+class JobStreams:
+    """Keeps up to ``depth`` synthesis jobs in flight on their own HIP streams (a serving loop's
+    double buffering): ``with js.next(): distributed_synthesize(...)`` runs job i on stream
+    i % depth, so one job's low-occupancy launches -- the ProDiff WaveNet stack puts one 64-frame
+    window on a CU, 157 of 256 CUs at 8 x 861 frames; the NSF stages' small grids -- overlap the
+    previous job's vocoder (bench.py --overlap: C3 -6%, C5 -11% per job on one MI355X,
+    profiles/r05_ab/job_overlap_ab.txt).  The outputs of a job live on its stream: read them
+    after ``torch.cuda.synchronize()`` or a wait on that stream.  depth 1 or a CPU device: the
+    current stream, no-op."""
+
+    def __init__(self, depth=2, device=None):
+        self.depth = max(1, int(depth))
+        dev = torch.device(device) if device is not None else None
+        self.streams = None
+        if self.depth > 1 and dev is not None and dev.type == "cuda":
+            cur = torch.cuda.current_stream(dev)
+            self.streams = [torch.cuda.Stream(dev) for _ in range(self.depth)]
+            for s in self.streams:
+                s.wait_stream(cur)      # inputs made on the current stream are ready
+        self.i = 0
+
+    def next(self):
+        if self.streams is None:
+            return contextlib.nullcontext()
+        s = self.streams[self.i % self.depth]
+        self.i += 1
+        return torch.cuda.stream(s)
+
+
 def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None,
                            collectives=False, max_waste=0.15, streams=4, max_frames=None):
     """Synthesize utterances sharded over the ranks of the default process group

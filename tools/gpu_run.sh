@@ -6,6 +6,8 @@
 #   tests[=<pytest -k expr>]  every -m gpu test (or the selected ones)       -> gpu_tests.log
 #   bench=<cfg>[,<cfg>...]    one bench.py line per config (C3 C2 C4 C5 C5DS) -> bench_<cfg>.json
 #   trace=<cfg>               rocprofv3 --kernel-trace --stats of that bench -> trace_<cfg>/
+#   (trace / traffic / sq run one job at a time, --overlap 1: the bench line's roofline launch times
+#   come from its isolated pass, bench.py)
 #   traffic=<cfg>             FETCH_SIZE / WRITE_SIZE passes on the hot kernels -> <cfg>_traffic.json
 #   sq=<cfg>                  SQ-counter passes (tools/pmc_sq.sh) + summary  -> <cfg>_sq.json
 #   ab=<lib|->:<args>;...     same-box A/B bench lines (tools/gpu_ab_libs.sh), ';'-separated specs
@@ -46,18 +48,18 @@ print(sys.argv[2], d['ms_per_step'], 'ms/step', d['value'], d['roofline']['kerne
       done ;;
     trace)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_$val -o run --output-format csv -- \
-        python -u $R/bench.py $(bench_args $val) --cpu-frames 0 --no-kernel-timing > $O/trace_$val.log 2>&1) ;;
+        python -u $R/bench.py $(bench_args $val) --overlap 1 --cpu-frames 0 --no-kernel-timing > $O/trace_$val.log 2>&1) ;;
     traffic)
       for pmc in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && timeout -s KILL 180 rocprofv3 --pmc $pmc --kernel-include-regex "$(regex $val)" \
           -d $O/pmc_$val/pmc_$pmc -o run --output-format csv -- \
-          python -u $R/bench.py $(bench_args $val) --steps 2 --warmup 1 --cpu-frames 0 --no-kernel-timing \
+          python -u $R/bench.py $(bench_args $val) --overlap 1 --steps 2 --warmup 1 --cpu-frames 0 --no-kernel-timing \
           > $O/pmc_${val}_$pmc.log 2>&1)
       done
       case $val in C4) b=32 ;; *) b=8 ;; esac
       python tools/pmc_traffic.py $O/pmc_$val $O/${val}_traffic.json $TAG ${val%DS} $b 861 ;;
     sq)
-      timeout -k 10 500 tools/pmc_sq.sh $TAG/sq_$val "$(regex $val)|enc_|dblock_bf16" $(bench_args $val) --steps 1
+      timeout -k 10 500 tools/pmc_sq.sh $TAG/sq_$val "$(regex $val)|enc_|dblock_bf16" $(bench_args $val) --overlap 1 --steps 1
       python tools/sq_summary.py gpurun_out/$TAG/sq_$val --config ${val%DS} -o $O/${val}_sq.json ;;
     ab)
       IFS=';' read -ra specs <<< "$val"
