@@ -635,9 +635,14 @@ def main():
     phase = {"compute_ms": 0.0, "gather_ms": 0.0, "n": 0}    # N > 1: where each timed step went
     ovl = None      # JobStreams when --overlap > 1
     if args.overlap is None:
-        # jobs in flight: 2 on one GPU for the C3 / C5 lines (measured); 1 with N > 1
-        # ranks (each rank's gather runs on its job's stream) and for C4 (the scaling line)
-        args.overlap = 2 if (world == 1 and cfg_name in ("C3", "C5")) else 1
+        # jobs in flight on one GPU (measured, profiles/r05_ab/job_overlap*_ab.txt): C3 2 (3: the same),
+        # C5 3 (2 on the .ds lengths, whose ragged batches already run on 4 streams); 1 with N > 1 ranks
+        # (each rank's gather runs on its job's stream) and for C4 (the scaling line)
+        args.overlap = 1
+        if world == 1 and cfg_name == "C3":
+            args.overlap = 2
+        elif world == 1 and cfg_name == "C5":
+            args.overlap = 2 if args.lengths == "ds" else 3
 
     if cfg["vocoder"]:
         if args.overlap > 1 and not dry:

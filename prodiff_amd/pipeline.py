@@ -289,8 +289,8 @@ class JobStreams:
     double buffering): ``with js.next(): distributed_synthesize(...)`` runs job i on stream
     i % depth, so one job's low-occupancy launches -- the ProDiff WaveNet stack puts one 64-frame
     window on a CU, 157 of 256 CUs at 8 x 861 frames; the NSF stages' small grids -- overlap the
-    previous job's vocoder (bench.py --overlap: C3 -6%, C5 -11% per job on one MI355X,
-    profiles/r05_ab/job_overlap_ab.txt).  The outputs of a job live on its stream: read them
+    previous job's vocoder (bench.py --overlap: C3 -6% per job with 2 in flight, C5 -15% with 3, on
+    one MI355X; profiles/r05_ab/job_overlap_ab.txt, job_overlap_depth_ab.txt).  The outputs of a job live on its stream: read them
     after ``torch.cuda.synchronize()`` or a wait on that stream.  depth 1 or a CPU device: the
     current stream, no-op."""
 
