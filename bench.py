@@ -238,7 +238,8 @@ def traffic_workload(d, fname):
 
 
 def sq_utilisation(config):
-    """Per-kernel MFMA-busy / VALU-busy fractions of the newest SQ-counter summary of this config
+    """Per-kernel MFMA-busy / VALU-busy fractions of the SQ-counter summary of this config (one of the
+    running library if there is one, else the newest round's)
     (profiles/rNN_*/<config>_sq.json, written by tools/sq_summary.py from separate rocprofv3 SQ
     passes over a short bench of the same workload).  None when no summary covers the config."""
     import glob
@@ -252,7 +253,8 @@ def sq_utilisation(config):
             continue
         if d.get("config") != config or not m:
             continue
-        key = (int(m.group(1)), os.path.getmtime(f))
+        # a summary of the running library first, then the newest round
+        key = (d.get("lib_sha16") == lib_sha16(), int(m.group(1)), os.path.getmtime(f))
         if best is None or key > best[0]:
             best = (key, f, d)
     if best is None:
