@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void nsf_noise_conv_kernel(const float* __rest
                                                              const float* __restrict__ bias, int C, int K,
                                                              int stride, int pad, long long Tout,
                                                              float* __restrict__ out, NsfRag rag_) {
-  extern __shared__ __attribute__((aligned(16))) float s_har[];
+  extern __shared__ float s_har[];
   const int CT = C < 256 ? C : 256, G = 256 / CT;
   const int tid = threadIdx.x;
   const int o = blockIdx.y * CT + tid % CT, rg = tid / CT;
@@ -193,25 +193,11 @@ __global__ __launch_bounds__(256) void nsf_noise_conv_kernel(const float* __rest
   const float bo = bias[o];
 #pragma unroll
   for (int i = 0; i < NC_ROWS; ++i) acc[i] = bo;
-  // (r05: loading the taps' weights in batches of 8 ran 87 vs 82 us -- kept one load per tap)
-  if (stride % 4 == 0 && K % 4 == 0) {
-    // (uniform; the first two stages, k = 128 / 16, stride 64 / 8) four taps per 16-B LDS read: the
-    // broadcast reads, one per FMA in the scalar loop, were the kernel's issue limit.  Same tap order.
-    for (int j = 0; j < K; j += 4) {
-      const float w0 = wt[(long long)j * C + o], w1 = wt[(long long)(j + 1) * C + o];
-      const float w2 = wt[(long long)(j + 2) * C + o], w3 = wt[(long long)(j + 3) * C + o];
+  // (r05: taps' weights loaded in batches of 8: 87 vs 82 us; four taps per 16-B LDS read: 105 us either way, noise_conv_lds4_ab.txt)
+  for (int j = 0; j < K; ++j) {
+    const float w = wt[(long long)j * C + o];
 #pragma unroll
-      for (int i = 0; i < NC_ROWS; ++i) {
-        const float4 v = *reinterpret_cast<const float4*>(&s_har[(rg + G * i) * stride + j]);
-        acc[i] = fmaf(w3, v.w, fmaf(w2, v.z, fmaf(w1, v.y, fmaf(w0, v.x, acc[i]))));
-      }
-    }
-  } else {
-    for (int j = 0; j < K; ++j) {
-      const float w = wt[(long long)j * C + o];
-#pragma unroll
-      for (int i = 0; i < NC_ROWS; ++i) acc[i] = fmaf(w, s_har[(rg + G * i) * stride + j], acc[i]);
-    }
+    for (int i = 0; i < NC_ROWS; ++i) acc[i] = fmaf(w, s_har[(rg + G * i) * stride + j], acc[i]);
   }
 #pragma unroll
   for (int i = 0; i < NC_ROWS; ++i) {
