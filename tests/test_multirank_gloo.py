@@ -142,6 +142,24 @@ def test_distributed_synthesize_max_frames_one_rank(max_frames):
         np.testing.assert_array_equal(wavs[i].numpy(), ew[0].numpy())
 
 
+def test_job_streams_cpu_is_a_no_op():
+    """JobStreams on a CPU device (or depth 1) hands out null contexts: jobs run in order on the
+    current stream, with the same outputs."""
+    from prodiff_amd.pipeline import JobStreams
+    lengths = [5, 9, 3]
+    conds = _conds(lengths)
+    for js in (JobStreams(2, "cpu"), JobStreams(1, None)):
+        assert js.streams is None
+        outs = []
+        for j in range(3):
+            with js.next():
+                outs.append(distributed_synthesize(stub_synth, conds, seed=j, hop=HOP))
+        for j, (mels, wavs) in enumerate(outs):
+            for i, c in enumerate(conds):
+                em, ew = stub_synth(c[None], j, utt_ids=[i])
+                np.testing.assert_array_equal(mels[i].numpy(), em[0].numpy())
+
+
 def test_bench_self_launches_n_ranks_dry_run():
     """`bench.py --gpus 2` without torchrun spawns 2 ranks itself (CPU dry run: gloo,
     stub synthesis, no GPU) and rank 0 reports n_gpus 2."""
