@@ -74,6 +74,50 @@ template <int S, bool NT, bool SEQ> int run(char* buf, const char* name) {
   return 0;
 }
 
+// r05: the same 8-rows-x-128-B pattern from exactly W waves per CU (one W-wave block per CU, held
+// there by 100 KB of dynamic LDS; each wave takes every (256 W)-th 32-row job): does the store rate
+// depend on the waves per CU?  (kp_kernel_bf16_kernel runs 8 per CU at ~4 TB/s with its MFMAs)
+template <int W>
+__global__ __launch_bounds__(64 * W, 1) void store_occ_kernel(char* __restrict__ out, int njobs) {
+  extern __shared__ char occ_pad[];
+  const int lane = threadIdx.x & 63;
+  const int w0 = blockIdx.x * W + (threadIdx.x >> 6);
+  if (threadIdx.x == 0) occ_pad[0] = 0;
+  const long long colblocks = ROWB / WAVE_COLB;
+  const u32x4 v = {(unsigned)w0, (unsigned)lane, 7u, 9u};
+  for (int w = w0; w < njobs; w += gridDim.x * W) {
+    const long long rb = w / colblocks, cb = w - rb * colblocks;
+    for (int c = 0; c < WAVE_COLB / 128; ++c) {
+#pragma unroll 4
+      for (int rg = 0; rg < 4; ++rg) {
+        const long long row = rb * 32 + rg * 8 + lane / 8;
+        *reinterpret_cast<u32x4*>(out + row * ROWB + cb * WAVE_COLB + (long long)c * 128 + (lane % 8) * 16) = v;
+      }
+    }
+  }
+}
+
+template <int W> int run_occ(char* buf) {
+  const int njobs = (int)(ROWS / 32 * (ROWB / WAVE_COLB));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&store_occ_kernel<W>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                         100 * 1024));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(store_occ_kernel<W>, dim3(256), dim3(64 * W), 100 * 1024, 0, buf, njobs);
+  CK(hipDeviceSynchronize());
+  const int reps = 20;
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(store_occ_kernel<W>, dim3(256), dim3(64 * W), 100 * 1024, 0, buf, njobs);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double us = ms * 1e3 / reps, bytes = (double)ROWS * ROWB;
+  printf("%2d waves per CU, 8 rows x 128 B  %8.1f us  %6.2f TB/s\n", W, us, bytes / us * 1e-6);
+  return 0;
+}
+
 int main() {
   char* buf;
   if (hipMalloc((void**)&buf, ROWS * ROWB) != hipSuccess) return 1;
@@ -88,6 +132,10 @@ int main() {
   e |= run<1024, true, false>(buf, "1 row x 1 KiB, nt");
   e |= run<1024, false, true>(buf, "seq 96 KiB per wave, plain");
   e |= run<1024, true, true>(buf, "seq 96 KiB per wave, nt");
+  e |= run_occ<4>(buf);
+  e |= run_occ<8>(buf);
+  e |= run_occ<12>(buf);
+  e |= run_occ<16>(buf);
   (void)hipFree(buf);
   return e;
 }
