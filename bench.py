@@ -645,6 +645,10 @@ def main():
             args.overlap = 2
         elif world == 1 and cfg_name == "C5":
             args.overlap = 2 if args.lengths == "ds" else 3
+    elif world > 1 and args.overlap > 1:
+        # every rank's gather is an RCCL collective on its job's stream: jobs in flight would put
+        # collectives of one communicator on several streams at once, which this bench does not do
+        raise SystemExit("--overlap > 1 is for one GPU (N > 1 ranks run one job at a time)")
 
     if cfg["vocoder"]:
         if args.overlap > 1 and not dry:
