@@ -310,6 +310,9 @@ class JobStreams:
             return contextlib.nullcontext()
         s = self.streams[self.i % self.depth]
         self.i += 1
+        # inputs the caller made on its own stream since the last job are ready for this one (the
+        # jobs themselves run on the side streams, so this does not order one job after another)
+        s.wait_stream(torch.cuda.current_stream(s.device))
         return torch.cuda.stream(s)
 
 
