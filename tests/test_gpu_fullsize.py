@@ -184,3 +184,25 @@ def test_c5_full_bf16_vs_fp32(B):
     assert np.isfinite(outs["fp32"][1]).all() and np.abs(outs["fp32"][1]).max() <= 1.0
     assert_bf16_close(outs["bf16"][0], outs["fp32"][0], f"C5 mel bf16 vs fp32, {B}x861")
     assert_bf16_close(outs["bf16"][1], outs["fp32"][1], f"C5 wav bf16 vs fp32, {B}x861")
+
+
+def test_c3_jobs_in_flight_bitexact():
+    """The bench's C3 job (8 x 861 frames, bf16) with two jobs in flight on two HIP streams
+    (pipeline.JobStreams, bench.py's default at N = 1) gives the same bits as the jobs run one
+    after the other -- per-stream workspaces, draws keyed by seed and utterance id."""
+    from prodiff_amd.pipeline import JobStreams, Synthesizer, distributed_synthesize
+    syn = Synthesizer.synthetic(DEV, seed=0, dtype="bf16")
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    conds = [torch.randn(861, 256, device=DEV, generator=gen) for _ in range(8)]
+    seq = [distributed_synthesize(syn, conds, seed=100 + j) for j in range(3)]
+    torch.cuda.synchronize()
+    js = JobStreams(2, DEV)
+    ovl = []
+    for j in range(3):
+        with js.next():
+            ovl.append(distributed_synthesize(syn, conds, seed=100 + j))
+    torch.cuda.synchronize()
+    for (m0, w0), (m1, w1) in zip(seq, ovl):
+        for i in range(8):
+            assert torch.equal(m1[i], m0[i]) and torch.equal(w1[i], w0[i])
+    assert not torch.equal(seq[0][1][0], seq[1][1][0])    # different seeds, different jobs
