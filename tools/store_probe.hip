@@ -97,6 +97,183 @@ __global__ __launch_bounds__(64 * W, 1) void store_occ_kernel(char* __restrict__
   }
 }
 
+// r05: the kp_kernel rhythm without its data: per 32-frame tile a wave runs NM MFMAs (two
+// independent 32x32x16 bf16 chains, as kp's 24) and then its 4 stores of 1 KiB; 8 waves per CU.
+// Does the chip overlap the MFMA phases with the store stream?
+typedef float f32x16p __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8p __attribute__((ext_vector_type(8)));
+template <int NM>
+__global__ __launch_bounds__(512, 1) void store_mfma_kernel(char* __restrict__ out, int njobs, float* sink) {
+  extern __shared__ char occ_pad2[];
+  const int lane = threadIdx.x & 63;
+  const int w0 = blockIdx.x * 8 + (threadIdx.x >> 6);
+  if (threadIdx.x == 0) occ_pad2[0] = 0;
+  const long long colblocks = ROWB / WAVE_COLB;
+  bf16x8p a, bb;
+  for (int i = 0; i < 8; ++i) { a[i] = (__bf16)(0.001f * (lane + i)); bb[i] = (__bf16)(0.002f * (lane - i)); }
+  f32x16p c0 = {}, c1 = {};
+  for (int w = w0; w < njobs; w += gridDim.x * 8) {
+    const long long rb = w / colblocks, cb = w - rb * colblocks;
+    for (int c = 0; c < WAVE_COLB / 128; ++c) {
+#pragma unroll
+      for (int m = 0; m < NM / 2; ++m) {
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb, a, c1, 0, 0, 0);
+      }
+      const u32x4 v = {__float_as_uint(c0[0]), __float_as_uint(c1[1]), (unsigned)w, (unsigned)lane};
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const long long row = rb * 32 + rg * 8 + lane / 8;
+        *reinterpret_cast<u32x4*>(out + row * ROWB + cb * WAVE_COLB + (long long)c * 128 + (lane % 8) * 16) = v;
+      }
+    }
+  }
+  if (c0[3] == 1234.5f) sink[0] = c1[2];
+}
+
+template <int NM> int run_mfma(char* buf, float* sink) {
+  const int njobs = (int)(ROWS / 32 * (ROWB / WAVE_COLB));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&store_mfma_kernel<NM>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                         100 * 1024));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(store_mfma_kernel<NM>, dim3(256), dim3(512), 100 * 1024, 0, buf, njobs, sink);
+  CK(hipDeviceSynchronize());
+  const int reps = 20;
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(store_mfma_kernel<NM>, dim3(256), dim3(512), 100 * 1024, 0, buf, njobs, sink);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double us = ms * 1e3 / reps, bytes = (double)ROWS * ROWB;
+  // MFMA-only time of the same launch: NM MFMAs x 32 cycles per tile, 2 waves per SIMD, 2.4 GHz
+  const double tiles = (double)njobs * (WAVE_COLB / 128) / (256.0 * 8), mfma_us = tiles * NM * 32 * 2 / 2.4e3;
+  printf("8 waves/CU, %2d MFMAs + 4 stores per tile  %8.1f us  %6.2f TB/s  (MFMA alone ~%.1f us)\n", NM, us,
+         bytes / us * 1e-6, mfma_us);
+  return 0;
+}
+
+// r05: kp_kernel's stores straight from the MFMA C layout (no LDS transpose): per tile 8 stores of 8 B
+// per lane, lane -> frame row lane & 31, 8-B chunk 2 j4 + (lane >> 5) -- 32 rows x 16 B per
+// instruction, the 8 instructions of a tile covering the same 32 rows x 128 B as kp's 4 x 1 KiB.
+typedef unsigned int u32x2p __attribute__((ext_vector_type(2)));
+template <int NM>
+__global__ __launch_bounds__(512, 1) void store_cl_kernel(char* __restrict__ out, int njobs, float* sink) {
+  extern __shared__ char occ_pad3[];
+  const int lane = threadIdx.x & 63;
+  const int w0 = blockIdx.x * 8 + (threadIdx.x >> 6);
+  if (threadIdx.x == 0) occ_pad3[0] = 0;
+  const long long colblocks = ROWB / WAVE_COLB;
+  bf16x8p a, bb;
+  for (int i = 0; i < 8; ++i) { a[i] = (__bf16)(0.001f * (lane + i)); bb[i] = (__bf16)(0.002f * (lane - i)); }
+  f32x16p c0 = {}, c1 = {};
+  for (int w = w0; w < njobs; w += gridDim.x * 8) {
+    const long long rb = w / colblocks, cb = w - rb * colblocks;
+    for (int c = 0; c < WAVE_COLB / 128; ++c) {
+#pragma unroll
+      for (int m = 0; m < NM / 2; ++m) {
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb, a, c1, 0, 0, 0);
+      }
+      const long long row = rb * 32 + (lane & 31);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const u32x2p v = {__float_as_uint(c0[q]), __float_as_uint(c1[q])};
+        *reinterpret_cast<u32x2p*>(out + row * ROWB + cb * WAVE_COLB + (long long)c * 128 + (2 * q + (lane >> 5)) * 8) = v;
+      }
+    }
+  }
+  if (c0[3] == 1234.5f) sink[0] = c1[2];
+}
+
+template <int NM> int run_cl(char* buf, float* sink) {
+  const int njobs = (int)(ROWS / 32 * (ROWB / WAVE_COLB));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&store_cl_kernel<NM>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                         100 * 1024));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(store_cl_kernel<NM>, dim3(256), dim3(512), 100 * 1024, 0, buf, njobs, sink);
+  CK(hipDeviceSynchronize());
+  const int reps = 20;
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(store_cl_kernel<NM>, dim3(256), dim3(512), 100 * 1024, 0, buf, njobs, sink);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double us = ms * 1e3 / reps, bytes = (double)ROWS * ROWB;
+  printf("8 waves/CU, %2d MFMAs + 8 C-layout stores (32 rows x 16 B) per tile  %8.1f us  %6.2f TB/s\n", NM, us,
+         bytes / us * 1e-6);
+  return 0;
+}
+
+// r05: kp's whole epilogue without its data: per tile NM MFMAs, the bf16 conversion into a
+// wave-private 32 x (64 + 8) LDS tile (8 ds_write_b64), lgkmcnt wait, 4 ds_read_b128, 4 stores of
+// 1 KiB (8 rows x 128 B) -- kp_kernel_bf16_kernel's epi() with its wave barriers.
+typedef __bf16 bf16x4p __attribute__((ext_vector_type(4)));
+template <int NM>
+__global__ __launch_bounds__(512, 1) void store_tr_kernel(char* __restrict__ out, int njobs, float* sink) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ot[8][32 * 72];
+  const int lane = threadIdx.x & 63, r32 = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int w0 = blockIdx.x * 8 + wave;
+  const long long colblocks = ROWB / WAVE_COLB;
+  bf16x8p a, bb;
+  for (int i = 0; i < 8; ++i) { a[i] = (__bf16)(0.001f * (lane + i)); bb[i] = (__bf16)(0.002f * (lane - i)); }
+  __bf16* ot = Ot[wave];
+  for (int w = w0; w < njobs; w += gridDim.x * 8) {
+    const long long rb = w / colblocks, cb = w - rb * colblocks;
+    for (int c = 0; c < WAVE_COLB / 128; ++c) {
+      f32x16p acc[2];
+      for (int r = 0; r < 16; ++r) { acc[0][r] = 0.f; acc[1][r] = (float)c; }
+#pragma unroll
+      for (int m = 0; m < NM / 2; ++m) {
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb, a, acc[1], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<bf16x4p*>(&ot[r32 * 72 + 4 * (8 * j + 2 * g + h)]) =
+              bf16x4p{(__bf16)acc[j][4 * g], (__bf16)acc[j][4 * g + 1], (__bf16)acc[j][4 * g + 2], (__bf16)acc[j][4 * g + 3]};
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fl = i * 8 + (lane >> 3);
+        const uint4 v = *reinterpret_cast<const uint4*>(&ot[fl * 72 + 8 * (lane & 7)]);
+        const long long row = rb * 32 + fl;
+        *reinterpret_cast<uint4*>(out + row * ROWB + cb * WAVE_COLB + (long long)c * 128 + (lane & 7) * 16) = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  (void)sink;
+}
+
+template <int NM> int run_tr(char* buf, float* sink) {
+  const int njobs = (int)(ROWS / 32 * (ROWB / WAVE_COLB));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(store_tr_kernel<NM>, dim3(256), dim3(512), 0, 0, buf, njobs, sink);
+  CK(hipDeviceSynchronize());
+  const int reps = 20;
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(store_tr_kernel<NM>, dim3(256), dim3(512), 0, 0, buf, njobs, sink);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double us = ms * 1e3 / reps, bytes = (double)ROWS * ROWB;
+  printf("8 waves/CU, %2d MFMAs + kp's LDS-transpose epilogue + 4 stores per tile  %8.1f us  %6.2f TB/s\n", NM, us,
+         bytes / us * 1e-6);
+  return 0;
+}
+
 template <int W> int run_occ(char* buf) {
   const int njobs = (int)(ROWS / 32 * (ROWB / WAVE_COLB));
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&store_occ_kernel<W>), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -136,6 +313,18 @@ int main() {
   e |= run_occ<8>(buf);
   e |= run_occ<12>(buf);
   e |= run_occ<16>(buf);
+  float* sink;
+  if (hipMalloc((void**)&sink, 64) != hipSuccess) return 1;
+  e |= run_mfma<0>(buf, sink);
+  e |= run_mfma<8>(buf, sink);
+  e |= run_mfma<16>(buf, sink);
+  e |= run_mfma<24>(buf, sink);
+  e |= run_mfma<48>(buf, sink);
+  e |= run_cl<0>(buf, sink);
+  e |= run_cl<24>(buf, sink);
+  e |= run_tr<0>(buf, sink);
+  e |= run_tr<24>(buf, sink);
+  (void)hipFree(sink);
   (void)hipFree(buf);
   return e;
 }
