@@ -177,6 +177,19 @@ def test_bench_self_launches_n_ranks_dry_run():
     assert d["config"]["global_batch"] == 2 * d["config"]["per_gpu_batch"]
 
 
+def test_bench_refuses_jobs_in_flight_with_ranks():
+    """Jobs in flight are a one-GPU mode: with N > 1 ranks every job's gather is an RCCL collective,
+    so bench.py refuses --overlap > 1 there instead of putting collectives on several streams."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                          "--warmup", "1", "--dry-run", "--overlap", "2"], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode != 0
+    assert "--overlap > 1 is for one GPU" in (out.stderr + out.stdout)
+
+
 class StubSvs:
     """Per-utterance dict inputs like SvsSynthesizer's (phoneme tokens + frame features),
     batched by the real SvsSynthesizer.collate; output independent of the batch."""
