@@ -12,6 +12,9 @@ wav [B,220416] (10 s at 22.05 kHz, hop 256).  Configurations (BASELINE.json):
   C2                     ProDiff 2-iter only, B=1, T=1000, fp32, mel-only (hipGraph replay)
   C5                     SVS path: teacher condition (FFT encoder) + ProDiff 4-iter (M=128) +
                          NSF-HiFiGAN (44.1 kHz, hop 512), 8 segments per GPU (64 at N=8), bf16
+  PITCH                  SURVEY §8(f)1: the pitch predictor's sampler (PitchRectifiedFlow, 20 Euler
+                         steps of WaveNet 20x256, M=64 repeat bins, dilation cycle 5) + denorm,
+                         8 segments x 861 frames, bf16, one GPU
 
 For N>1 every rank runs its LPT shard (pipeline.distributed_synthesize: no
 data-path collective) and the step ends with the ragged point-to-point gather of
@@ -65,14 +68,41 @@ CONFIGS = {
                desc="C5: SVS path (modules/svs) -- ProDiffTeacher condition (FFT encoder, {n} phonemes, speaker mix, "
                     "zh/jp lang ids, voicing/breath) + ProDiff 4-iter (WaveNet 20x256, M=128) + NSF-HiFiGAN "
                     "(44.1 kHz, hop 512), {b} x {t}-frame segments per GPU (64 at N=8)"),
+    # the pitch predictor's diffusion (handler/base_config.yaml:135-149 f0_prediction_args: repeat_bins 64,
+    # residual_layers 20, residual_channels 256, dilation_cycle_length 5; sampling_algorithm euler :204;
+    # infer_step 20, pitch_predictor.py:63,120; reflow.py:86-144)
+    "PITCH": dict(batch=8, strong=False, frames=861, dtype="bf16", vocoder=False, timesteps=20, pitch=True, mels=64,
+                  cyc=5,
+                  desc="PITCH: pitch predictor sampler -- PitchRectifiedFlow, 20 Euler steps of WaveNet 20x256 "
+                       "(M = 64 repeat bins, dilation cycle 5) + denorm_spec (mean over the bins, clamp), "
+                       "{b} x {t}-frame segments per GPU"),
 }
 
 
 WN_LAYERS, WN_STACK_NL = 20, 10          # residual layers; layers per wn_stack_bf16_kernel launch
+WN_STACK_HMAX = 16                        # wavenet.hip WST_HMAX: a launch's dilations sum to at most this
 FD_STEPS, FD_BLOCKS = 4, 3                # FastDiff sampler passes per call; LVC blocks (hop 8, 64, 256)
 
 
-def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256):
+def wn_stack_launches(cyc=1, L=WN_LAYERS, nl_max=WN_STACK_NL, hmax=WN_STACK_HMAX):
+    """The stack launches of one denoiser call, as wavenet.hip groups the layers: at most nl_max
+    layers per launch whose dilations 2^(l % cyc) sum to at most hmax (cycle 1: 2 launches of 10;
+    cycle 5: {1,2,4,8}, {16} four times -- 8 launches)."""
+    n, l0 = 0, 0
+    while l0 < L:
+        nl, s = 0, 0
+        while l0 + nl < L and nl < nl_max:
+            d = 1 << ((l0 + nl) % cyc)
+            if nl > 0 and s + d > hmax:
+                break
+            s += d
+            nl += 1
+        l0 += nl
+        n += 1
+    return n
+
+
+def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256, cyc=1):
     """Algorithmic FLOPs (2 x MAC) of ONE launch of each tagged kernel.
     Tags used by several block sizes report the mean over their launches in one call."""
     F = B * T
@@ -81,7 +111,7 @@ def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256):
     dblock = sum(2 * r * 32 * 96 * 2 + 2 * r * 32 * 128 for r in d_rows) / 9.0
     kp_layers = 4 if dtype == "bf16" else 1           # bf16: one launch computes all 4 layers' kernels
     gate, resskip = 2 * F * 2 * C * (3 * C + H), 2 * F * 2 * C * C
-    nstack = -(-WN_LAYERS // WN_STACK_NL)
+    nstack = wn_stack_launches(cyc)
     return {
         "wn_inproj": 2 * F * M * C,
         "wn_gate": gate,
@@ -122,7 +152,7 @@ def flops_per_launch(B, T, dtype="bf16", hops=(8, 64, 256), M=80, C=256, H=256):
     }
 
 
-def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
+def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256, cyc=1):
     """Compulsory HBM bytes of ONE launch of each tagged kernel with the layouts the
     kernels use (activations fp32 time-major; weights and LVC kernels bf16 in the
     bf16 path, fp32 otherwise).  Mean over launches where the block size varies."""
@@ -136,14 +166,14 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256):
     lvc_f = [r * 3 * per_row_io + F * kf_frame for r in rows[1:]]
     lvc_v = [r * 4 * per_row_io + F * kf_frame for r in rows]          # unfused: x r/w, a, y
     layer_w = 2 * C * (4 * C + H) * wb
-    nstack = -(-WN_LAYERS // WN_STACK_NL)
+    nstack = wn_stack_launches(cyc)
     return {
         "wn_inproj": F * (M + C) * 4 + C * M * wb,
         # first launch: spec in, bf16 cond in, x and skip out; last: x and skip in, bf16 cond in,
         # mel read + written (posterior); inner launches (none at 20 layers / 10): x, skip in + out.
         # Plus each launch's layers' weights once (the compulsory HBM bytes; blocks re-read them from L2)
         "wn_stack": (F * (M * 4 + H * 2 + 2 * C * 4) + F * (2 * C * 4 + H * 2 + 2 * M * 4) +
-                     max(nstack - 2, 0) * F * (4 * C * 4 + H * 2)) / nstack + WN_STACK_NL * layer_w,
+                     max(nstack - 2, 0) * F * (4 * C * 4 + H * 2)) / nstack + WN_LAYERS / nstack * layer_w,
         "wn_condb": F * H * (4 + 2),
         "wn_gate": F * (C + H + C) * 4 + 2 * C * (3 * C + H) * wb,
         "wn_resskip": F * (C + 2 * C + 2 * C) * 4 + 2 * C * C * wb,
@@ -426,7 +456,7 @@ def ref_cpu_baseline(config):
         return None
     with open(path) as f:
         d = json.load(f)
-    key = config if config in ("C2", "C5") else "C3"
+    key = config if config in ("C2", "C5", "PITCH") else "C3"
     e = d.get("configs", {}).get(key)
     if not e:
         return None
@@ -471,7 +501,7 @@ def denoiser_roofline(kern_all, nprof, B, T, cfg, dtype, peak_tf, cfg_name, pmc_
     sampler's denoiser, tags DENOISER_TAGS) against the MFMA roof at its algorithmic FLOPs
     (26.43 MFLOP per mel frame per pass at M = 80), and -- where a PMC summary of
     this workload holds the stack kernel -- its measured HBM bytes against the 8 TB/s roof."""
-    M = 128 if cfg.get("svs") else 80
+    M = cfg.get("mels", 128 if cfg.get("svs") else 80)
     tags = [t for t in kern_all if t in DENOISER_TAGS]
     if not tags:
         return None
@@ -562,13 +592,15 @@ def main():
     cfg_name = args.config if args.config != "auto" else ("C3" if world == 1 else "C4")
     cfg = CONFIGS[cfg_name]
     svs = cfg.get("svs", False)
-    hop, sample_rate = (512, 44100) if svs else (HOP, SAMPLE_RATE)
+    # (the pitch predictor runs at the SVS frame rate, handler/base_config.yaml: hop 512 at 44.1 kHz)
+    hop, sample_rate = (512, 44100) if (svs or cfg.get("pitch")) else (HOP, SAMPLE_RATE)
     dtype = args.dtype or cfg["dtype"]
     nb = args.batch or cfg["batch"]
     T = args.frames or cfg["frames"]
     dry = args.dry_run
-    if cfg_name == "C2" and world > 1:
-        raise SystemExit("C2 is a single-GPU latency config")
+    if cfg_name in ("C2", "PITCH") and world > 1:
+        raise SystemExit(f"{cfg_name} is a single-GPU config")
+    pitch = cfg.get("pitch", False)
     if world > 1:
         dist.init_process_group("gloo" if dry else "nccl", init_method="env://")
         assert dist.get_world_size() == args.gpus
@@ -613,8 +645,8 @@ def main():
     _lib = None
     if dry:
         synth_fn = stub_synth
-        if svs:
-            raise SystemExit("--dry-run covers the C3/C4 launcher; C5 needs the GPU")
+        if svs or pitch:
+            raise SystemExit("--dry-run covers the C3/C4 launcher; C5 / PITCH need the GPU")
     elif svs:
         from prodiff_amd import _lib
         from prodiff_amd.pipeline import SvsSynthesizer
@@ -624,6 +656,19 @@ def main():
         if args.nsf_opt:
             syn.generator.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.nsf_opt)})
         synth_fn = syn
+    elif pitch:
+        # the pitch predictor's sampler alone (its note / phoneme encoders are out of scope, SURVEY §2
+        # row 15): PitchRectifiedFlow over a WaveNet(64, 256, 20, 256, cycle 5) with random-init weights
+        from prodiff_amd import PitchRectifiedFlow, WaveNet, _lib
+        M_p = cfg["mels"]
+        net = WaveNet(M_p, 256, 20, 256, cfg["cyc"])
+        net.load_state_dict({k: torch.from_numpy(v) for k, v in
+                             _synth.synth_params(_synth.wavenet_param_shapes(M_p, 256, 20, 256), 0).items()})
+        rf = PitchRectifiedFlow(M_p, net, time_scale=1000, sampling_algorithm="euler").to(dev).eval()
+        rf.set_compute_dtype(dtype)
+        if args.wn_opt:
+            net.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.wn_opt)})
+        synth_fn = None
     else:
         from prodiff_amd import _lib
         from prodiff_amd.pipeline import Synthesizer
@@ -671,6 +716,13 @@ def main():
                 phase["gather_ms"] += st["gather_ms"]
                 phase["n"] += 1
             return out
+    elif pitch:
+        # PITCH: 20 Euler steps (every velocity evaluation the fused WaveNet stack, x += v dt in its
+        # last launch) then denorm_spec: mean over the 64 repeat bins, clamp -> pitch [B, T]
+        cond_b = torch.stack([conds[i] for i in mine])
+
+        def step(i, timed=False, iso=False):
+            return rf.denorm_spec(rf.sample(cond_b, infer_step=cfg["timesteps"], seed=10_000 * i))
     else:
         # C2: the ProDiff sampler alone on one utterance (B=1), mel only
         gd = syn.diffusion
@@ -679,7 +731,7 @@ def main():
         if not args.no_graph:
             graph = gd.capture(cond_b, seed=1)             # hipGraph of the whole 2-step sampler
 
-        def step(i, timed=False):
+        def step(i, timed=False, iso=False):
             if graph is not None:
                 return graph.replay()
             return gd.sample(cond_b, seed=10_000 * i)
@@ -697,8 +749,8 @@ def main():
         fl.update(sf)
         by.update(sb)
     else:
-        fl = flops_per_launch(Bl, Tl, dtype)
-        by = bytes_per_launch(Bl, Tl, dtype)
+        fl = flops_per_launch(Bl, Tl, dtype, M=cfg.get("mels", 80), cyc=cfg.get("cyc", 1))
+        by = bytes_per_launch(Bl, Tl, dtype, M=cfg.get("mels", 80), cyc=cfg.get("cyc", 1))
     for i in range(args.warmup):
         step(i)
     if ovl is not None:
@@ -802,6 +854,8 @@ def main():
             assert all(torch.isfinite(w).all() for w in wavs)
         else:
             assert torch.isfinite(out).all()
+            if pitch:
+                assert out.shape == (B, T) and float(out.abs().max()) <= 12.0   # clamp_min / clamp_max
 
     frames = sum(lengths) * args.steps
     audio_s = frames * hop / sample_rate
@@ -846,6 +900,8 @@ def main():
                                                  pmc_key=(B if ds_mode else int(Bl), T))
     if svs:
         step_fl = svs_step_flops(n_total, sum(lengths) / n_total, sum(tokens) / n_total)
+    elif pitch:
+        step_fl = cfg["timesteps"] * prodiff_step_flops(1, sum(lengths), M=cfg["mels"])
     else:
         Fa = sum(lengths)
         step_fl = 2 * prodiff_step_flops(1, Fa) + (4 * fastdiff_step_flops(1, Fa) if cfg["vocoder"] else 0)
@@ -862,7 +918,8 @@ def main():
         "vs_baseline": None,
         "dtype": dtype,
         "data": ("synthetic SVS segments (phonemes, durations summing to T, f0 with unvoiced gaps, voicing/breath, "
-                 "speaker mix)" if svs else "synthetic (cond ~ N(0,1))") +
+                 "speaker mix)" if svs else "synthetic (cond ~ N(0,1): the pitch predictor's encoder output)" if pitch
+                 else "synthetic (cond ~ N(0,1))") +
                 "; random-init weights of the reference architectures; on-device Philox draws",
         "config": {"workload": cfg["desc"].format(b=nb, t=T if not ds_mode else f"{min(lengths)}..{max(lengths)}",
                                                   n=cfg.get("tokens") if not ds_mode else "the .ds file's"),
@@ -879,7 +936,7 @@ def main():
                    {"value": round(frames / dt_iso, 1), "ms_per_step": round(dt_iso / args.steps * 1e3, 3),
                     "note": "the same K steps run one after the other right after the timed region"},
                    "parallelism": f"dp{world} (utterance shards, RCCL gather to rank 0)" if cfg["vocoder"]
-                   else "single GPU" + ("" if args.no_graph else ", hipGraph replay")},
+                   else "single GPU" + ("" if (args.no_graph or pitch) else ", hipGraph replay")},
         "rtf": round(dt / audio_s, 6),
         "x_realtime": round(audio_s / dt, 1),
         "model_tflops": round(step_fl * args.steps / dt / 1e12, 2),
@@ -896,7 +953,7 @@ def main():
     }
     if rank == 0 and world == 1 and not dry:
         out_line["cpu_baseline"] = ref_cpu_baseline(cfg_name)
-        if args.cpu_frames > 0 and not svs:
+        if args.cpu_frames > 0 and not svs and not pitch:
             out_line["cpu_baseline_port"] = port_cpu_baseline(args.cpu_frames if cfg["vocoder"] else T,
                                                               vocoder=cfg["vocoder"])
     if rank == 0:

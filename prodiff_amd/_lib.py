@@ -194,19 +194,36 @@ def _device_rows(vals, B, device, name, lo, hi):
         if len(_UTT_CACHE) >= 256:
             _UTT_CACHE.pop(next(iter(_UTT_CACHE)))
         h = t.to(torch.int32).contiguous()
+        ev = None
         if dev.type == "cuda":
             # pinned source + non_blocking: a pageable copy would block the host until the stream
             # drains (no queuing ahead, no overlap of batches on other streams); the pinned host
-            # buffer lives in the cache entry, so it outlives the copy
+            # buffer lives in the cache entry, so it outlives the copy.  The event marks the copy's
+            # end on the stream that issued it: a later hit on ANOTHER stream waits for it (ADVICE
+            # r05: a job on stream B reusing the key job k just created on a busy stream A read the
+            # lengths / utterance ids before A's copy had landed)
             h = h.pin_memory()
             d = h.to(device=dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
         else:
             d = h
-        _UTT_CACHE[key] = (d, h)
+        _UTT_CACHE[key] = [d, h, ev]
     else:
-        d = d[0]
+        ent = d
+        d = ent[0]
         if dev.type == "cuda":
-            d.record_stream(torch.cuda.current_stream(dev))
+            cur = torch.cuda.current_stream(dev)
+            ev = ent[2]
+            if ev is not None:
+                if ev.query():
+                    ent[2] = None           # the copy has landed: no stream needs to wait any more
+                elif not torch.cuda.is_current_stream_capturing():
+                    cur.wait_event(ev)
+                else:
+                    raise HipError(f"{name}: the device copy of these values is still in flight on "
+                                   "another stream; synchronize before capturing a graph")
+            d.record_stream(cur)
     return d
 
 
@@ -290,15 +307,19 @@ class Workspace:
     """Grow-only device scratch buffers (torch caching allocator), one per (device, stream): the
     library's calls are stream-ordered, so calls on different streams -- distributed_synthesize
     runs ragged batches side by side -- must not share scratch (include/prodiff_hip.h: "concurrent
-    calls on different streams need separate workspaces")."""
+    calls on different streams need separate workspaces").  ``per_stream=False``: one buffer per
+    device whatever the stream (a captured graph's workspace: sized by an eager warm-up call, then
+    reused by the capture on torch's capture stream; the caller orders the two)."""
 
-    def __init__(self):
+    def __init__(self, per_stream=True):
         self.bufs = {}
+        self.per_stream = per_stream
 
     def get(self, nbytes, device):
         import torch
         device = torch.device(device)
-        sid = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
+        sid = (torch.cuda.current_stream(device).cuda_stream
+               if device.type == "cuda" and self.per_stream else 0)
         key = (str(device), sid)
         buf = self.bufs.get(key)
         if buf is None or buf.numel() < nbytes:

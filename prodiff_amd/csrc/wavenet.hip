@@ -350,6 +350,7 @@ struct WnStackArgs {
   int rows, T, l0, nl, first, L;
   const int* lens;        // frames of each row's utterance (null: T): the conv's zero padding starts there
   int ro, hl;             // output rows per block: window rows [hl, hl + ro) (8 <= hl, hl + ro <= 56)
+  int cyc;                // dilation_cycle_length: layer l dilates by 2^(l % cyc) (DIL instantiations)
   // PD_WN_OPT_STACK_FUSE, first launch: x = relu(W_in spec + b_in) of the window rows computed
   // here (spec [rows][M] fp32, Winb [C][ldw_in] bf16, M <= ldw_in <= 128) instead of read
   const float* spec;
@@ -372,6 +373,9 @@ struct WnStackArgs {
   const int* uid;
 };
 constexpr int WST_LD = WNF_C + 8;                    // LDS row: 528 B, conflict-free b128 reads
+// a launch's halo budget: the sum of its layers' dilations (window rows [hl, 64 - hl) stay exact);
+// 16 keeps >= 32 output rows of the 64-row window per block
+constexpr int WST_HMAX = 16;
 #ifndef WST_WD
 #define WST_WD 6
 #endif
@@ -379,8 +383,18 @@ constexpr int WST_LD = WNF_C + 8;                    // LDS row: 528 B, conflict
 // skip tiles w / 8 + w of GEMM2, as wn_layer_bf16_kernel.  r04: a 4-wave variant (one wave per
 // SIMD, 12-deep rings) ran 24 us per layer against 21 us for this one (no partner wave to issue
 // beside a wave's MFMA-dependent epilogues).
-// IN: the fused input projection (first launch); TAIL: the fused sampler output stage (last launch)
-template <bool IN, bool TAIL>
+// IN: the fused input projection (first launch); TAIL: the fused sampler output stage (last launch).
+// RAG: a ragged batch (P.lens non-null); the dense instantiation reads no lengths (r06: the lens
+// loads of the r05 build sat between the prologue's two barriers, an exposed round trip per block).
+// DIL (r06): dilation cycles > 1 (the pitch predictor's WaveNet, dilation_cycle_length 5,
+// pitch_predictor.py:40-55): layer l's taps read window rows r -+ 2^(l % cyc), so a launch's layers
+// shrink the exact window by the SUM of their dilations and the host groups layers with that sum
+// <= hl (cycle 5: {1,2,4,8} with hl 15 and 34 output rows, {16} with hl 16 and 32).  The cycle-1
+// instantiations (DIL false) keep the +-1 taps as immediates: unchanged code for the ProDiff stack.
+// TAIL: 0 none, 1 on-device (Philox) or no draws, 2 explicit draws (P.noise): the noise operand loads
+// and their 32 registers exist only in the explicit-draw build (r06; the Philox tail the bench runs
+// spilled 28 VGPRs with them).
+template <bool IN, int TAIL, bool RAG = false, bool DIL = false>
 __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs P) {
   constexpr int C = WNF_C, H = WNF_C, K1 = 3 * C + H, KS1 = K1 / 16, KS2 = C / 16, WD = WST_WD, WD2 = 4;
   constexpr int WR = 64;                             // window rows: 2 MFMA row tiles
@@ -528,9 +542,11 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
       }
     }
   }
-  // conv zero padding: tap t-1 / t+1 of the lane's A rows (window row 32q + r32) outside its
-  // utterance (or outside the batch) reads zero -- a select at the fragment read
+  // conv zero padding: tap t-d / t+d of the lane's A rows (window row 32q + r32) outside its
+  // utterance (or outside the batch) reads zero -- a select at the fragment read.  DIL: the room to
+  // the utterance's start / end (-1 outside the batch), compared with each layer's dilation
   bool mlo[2], mhi[2];
+  int dlo[2], dhi[2];
   // the per-layer epilogue's row conditions as bits of two lane words (bit 16 q + reg: window row
   // inside the batch / in utterance bB), made opaque once per layer below: as 64 hoisted lane masks
   // they took the SGPR file and spilled (r05)
@@ -546,14 +562,25 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int R = W0 + 32 * q + r32, Rc = min(max(R, 0), rows - 1), bq = Rc / T, t = Rc - bq * T;
-    const int lb = wn_len(P.lens, P.b1, bq, T);       // ragged batch: the utterance's own end
-    mlo[q] = R >= 0 && R < rows && t >= 1;
-    mhi[q] = R >= 0 && R < rows && t <= lb - 2;
+    const int lb = RAG ? wn_len(P.lens, P.b1, bq, T) : T;   // ragged batch: the utterance's own end
+    const bool inb = R >= 0 && R < rows;
+    mlo[q] = inb && t >= 1;
+    mhi[q] = inb && t <= lb - 2;
+    dlo[q] = inb ? t : -1;
+    dhi[q] = inb ? lb - 1 - t : -1;
   }
   __syncthreads();
   const bf16x8 z8 = {};
   for (int j = 0; j < P.nl; ++j) {
     const int l = P.l0 + j;
+    const int dil = DIL ? 1 << (l % P.cyc) : 1;
+    if constexpr (DIL) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        mlo[q] = dlo[q] >= dil;
+        mhi[q] = dhi[q] >= dil;
+      }
+    }
     const bf16x8* wg = reinterpret_cast<const bf16x8*>(P.W1f + (long long)l * 2 * C * K1) + (long long)wave * KS1 * 64 + lane;
     const bf16x8* wf = reinterpret_cast<const bf16x8*>(P.W1f + (long long)l * 2 * C * K1) + (long long)(8 + wave) * KS1 * 64 + lane;
     const bf16x8* wr = reinterpret_cast<const bf16x8*>(P.W2f + (long long)l * 2 * C * C) + (long long)wave * KS2 * 64 + lane;
@@ -574,7 +601,7 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (tap < 3) {
-          const int wrow = min(max(32 * q + r32 + tap - 1, 0), WR - 1);
+          const int wrow = min(max(32 * q + r32 + (tap - 1) * dil, 0), WR - 1);
           a[q] = *reinterpret_cast<const bf16x8*>(&XW[wrow * WST_LD + cc]);
           if (tap == 0) a[q] = mlo[q] ? a[q] : z8;
           if (tap == 2) a[q] = mhi[q] ? a[q] : z8;
@@ -656,17 +683,22 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
     }
     __syncthreads();   // XW written / Gs reads done before the next layer
   }
-  if constexpr (TAIL) {
+  if constexpr (TAIL > 0) {
     // ---- fused tail: skip head, output projection and posterior on the output rows, with the
-    //      GEMM engine's roundings and k order (A = bf16(activation), 16 k-steps of 16)
+    //      GEMM engine's roundings and k order (A = bf16(activation), 16 k-steps of 16).
+    //      The lane's column / half through opaque copies: with n and h themselves, hipcc computed
+    //      the tail's ~27 LDS addresses in the prologue and spilled them across the layer loop (r06)
+    int nq = n, hq = h;
+    asm volatile("" : "+v"(nq), "+v"(hq));
+    auto skwq = [&](int i) { const int reg = skr(i); return 32 * skq(i) + (reg & 3) + 8 * (reg >> 2) + 4 * hq; };
     bf16x8 wsf[16];
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks) wsf[ks] = *reinterpret_cast<const bf16x8*>(P.Wsb + (long long)n * C + ks * 16 + h * 8);
+    for (int ks = 0; ks < 16; ++ks) wsf[ks] = *reinterpret_cast<const bf16x8*>(P.Wsb + (long long)nq * C + ks * 16 + hq * 8);
 #pragma unroll
     for (int i = 0; i < 24; ++i)   // window rows 8..55 -> XW rows 0..47 (rows 48..63 keep finite
-      XW[(skw(i) - 8) * WST_LD + n] = (__bf16)(SK[sko(i)] * P.skip_scale);   // x values, never stored)
+      XW[(skwq(i) - 8) * WST_LD + nq] = (__bf16)(SK[(skwq(i) - 8) * C + nq] * P.skip_scale);   // x values, never stored)
     __syncthreads();
-    const float bsv = P.bs[n];
+    const float bsv = P.bs[nq];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       f32x16 acc;
@@ -675,10 +707,10 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
       for (int ks = 0; ks < 16; ++ks)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            *reinterpret_cast<const bf16x8*>(&XW[(32 * q + r32) * WST_LD + ks * 16 + h * 8]), wsf[ks], acc, 0, 0, 0);
+            *reinterpret_cast<const bf16x8*>(&XW[(32 * q + r32) * WST_LD + ks * 16 + hq * 8]), wsf[ks], acc, 0, 0, 0);
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg)
-        Gs[(32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h) * WST_LD + n] = (__bf16)act_apply(acc[reg] + bsv, ACT_RELU, 0.f);
+        Gs[(32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * hq) * WST_LD + nq] = (__bf16)act_apply(acc[reg] + bsv, ACT_RELU, 0.f);
     }
     __syncthreads();
     const int col = wave * 32 + r32, M = P.M;
@@ -686,23 +718,24 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
       const int colc = min(col, M - 1);
       bf16x8 wof[16];
 #pragma unroll
-      for (int ks = 0; ks < 16; ++ks) wof[ks] = *reinterpret_cast<const bf16x8*>(P.Wob + (long long)colc * C + ks * 16 + h * 8);
+      for (int ks = 0; ks < 16; ++ks) wof[ks] = *reinterpret_cast<const bf16x8*>(P.Wob + (long long)colc * C + ks * 16 + hq * 8);
       const float bov = P.bo[colc];
       // the posterior's operands (x_t, explicit noise, the window's two utterance ids) loaded before
       // the MFMAs, unconditionally at clamped rows, and the results stored through a buffer resource
       // whose range check drops the rows this block does not own: with loads and stores under the
       // row test, every output waited for its own load (r05 asm: 32 round trips per lane)
       const unsigned uA = utt_id(P.uid, bA), uB = utt_id(P.uid, bB);
-      const float* nzp = P.noise ? P.noise : P.mel;   // a readable array when the noise is drawn here
       float xt[2][16], zx[2][16];
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-          const int R = W0 + 8 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, Rc = min(max(R, 0), rows - 1);
-          const int b = Rc / T, t = Rc - b * T;
+          const int R = W0 + 8 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * hq, Rc = min(max(R, 0), rows - 1);
           xt[q][reg] = P.mel[(long long)Rc * M + colc];
-          zx[q][reg] = nzp[P.noise ? (long long)b * P.noise_bs + (long long)t * P.noise_ld + colc : (long long)Rc * M + colc];
+          if constexpr (TAIL == 2) {
+            const int b = Rc / T, t = Rc - b * T;
+            zx[q][reg] = P.noise[(long long)b * P.noise_bs + (long long)t * P.noise_ld + colc];
+          }
         }
       __builtin_amdgcn_sched_barrier(0);
       const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(P.mel, 0, (unsigned)rows * (unsigned)M * 4u, 0x00020000);
@@ -714,18 +747,19 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks)
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              *reinterpret_cast<const bf16x8*>(&Gs[(32 * q + r32) * WST_LD + ks * 16 + h * 8]), wof[ks], acc, 0, 0, 0);
+              *reinterpret_cast<const bf16x8*>(&Gs[(32 * q + r32) * WST_LD + ks * 16 + hq * 8]), wof[ks], acc, 0, 0, 0);
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-          const int wrow = 8 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * h, R = W0 + wrow;
+          const int wrow = 8 + 32 * q + (reg & 3) + 8 * (reg >> 2) + 4 * hq, R = W0 + wrow;
           const bool ok = wrow >= HL && wrow - HL < P.ro && R < rows && col < M;
           // prodiff.py:106-126 (gemm.h EPI_POSTERIOR): x = c1 x0 + c2 x_t + sigma n
           const int Rc = min(R, rows - 1), b = Rc / T, t = Rc - b * T;
           const float v = acc[reg] + bov;
           float x = P.c1 * v + P.c2 * xt[q][reg];
           if (P.sigma != 0.f) {
-            const float z = P.noise ? zx[q][reg]
-                                    : philox_normal_u(P.seed, Rc < RB ? uA : uB, (unsigned)(t * M + col), P.stream_id);
+            float z;
+            if constexpr (TAIL == 2) z = zx[q][reg];
+            else z = philox_normal_u(P.seed, Rc < RB ? uA : uB, (unsigned)(t * M + col), P.stream_id);
             x += P.sigma * z;
           }
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), mrs, ok ? (unsigned)(R * M + col) * 4u : 0xfffffff0u, 0, 0);
@@ -735,7 +769,7 @@ __global__ __launch_bounds__(512, 1) void wn_stack_bf16_kernel(const WnStackArgs
   }
   // ---- output rows: x (layer l0 + nl's input) and the skip sum (not after a fused tail: the
   //      last layer's x feeds nothing, and the skip sum was consumed here)
-  if constexpr (TAIL) return;
+  if constexpr (TAIL > 0) return;
   // (rows and addresses from an opaque copy of the lane's half: computed here, not hoisted into the
   // prologue and spilled across the layer loop; stores through buffer resources whose range check
   // drops the rows the block does not own, so no store waits at a branch join)
@@ -1411,6 +1445,25 @@ int launch_small_gemm(const GemmArgs& a, hipStream_t st, const char* tag) {
   return launch_gemm<1, 1, 1, 4, EPI, ID>(a, st, tag);
 }
 
+// One stack launch: the instantiation for the launch's stage (IN / TAIL / middle), ragged or dense,
+// dilation cycle 1 or longer.
+template <bool RAG, bool DIL>
+void launch_wn_stack_v(const WnStackArgs& P, dim3 grid, hipStream_t st) {
+  if (P.spec) hipLaunchKernelGGL((wn_stack_bf16_kernel<true, 0, RAG, DIL>), grid, dim3(512), 0, st, P);
+  else if (P.Wsb && P.noise) hipLaunchKernelGGL((wn_stack_bf16_kernel<false, 2, RAG, DIL>), grid, dim3(512), 0, st, P);
+  else if (P.Wsb) hipLaunchKernelGGL((wn_stack_bf16_kernel<false, 1, RAG, DIL>), grid, dim3(512), 0, st, P);
+  else hipLaunchKernelGGL((wn_stack_bf16_kernel<false, 0, RAG, DIL>), grid, dim3(512), 0, st, P);
+}
+void launch_wn_stack(const WnStackArgs& P, dim3 grid, bool dil, hipStream_t st) {
+  if (P.lens) {
+    if (dil) launch_wn_stack_v<true, true>(P, grid, st);
+    else launch_wn_stack_v<true, false>(P, grid, st);
+  } else {
+    if (dil) launch_wn_stack_v<false, true>(P, grid, st);
+    else launch_wn_stack_v<false, false>(P, grid, st);
+  }
+}
+
 // A ProDiff sampler pass's output stage (prodiff.py:106-126) for wavenet_core to fuse into the
 // last stack launch: x0 = W_out relu(W_skip skip / sqrt(L) + b) + b_out, then the posterior update.
 struct StackTail {
@@ -1441,14 +1494,33 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
   float* skip = ws + Lw.skip;
   float* hs = ws + Lw.hs;
   if (tail_done) *tail_done = false;
-  const bool stack = h->W1f && h->stack_nl > 0 && h->layer_mode == 2 && h->cyc == 1 && H == WNF_C && T >= 64;
+  // (stores through buffer resources: 32-bit byte offsets into [rows][C] fp32)
+  const bool stack = h->W1f && h->stack_nl > 0 && h->layer_mode == 2 && H == WNF_C && T >= 64 && Ly <= 64 &&
+                     (long long)B * T * C * 4 < (1ll << 31);
+  // the stack launches' layer groups [l0, l0 + nl): at most stack_nl layers whose dilations sum to
+  // at most the window's halo budget (cycle 1: nl layers, halo nl; cycle 5: {1,2,4,8}, {16}, ...)
+  int grp[64][2], ngrp = 0;
+  if (stack) {
+    for (int l0 = 0; l0 < Ly && ngrp < 64;) {
+      int nl = 0, sum = 0;
+      while (l0 + nl < Ly && nl < h->stack_nl) {
+        const int d = 1 << ((l0 + nl) % h->cyc);
+        if (nl > 0 && sum + d > WST_HMAX) break;
+        sum += d;
+        ++nl;
+      }
+      grp[ngrp][0] = l0; grp[ngrp][1] = sum;
+      ++ngrp;
+      l0 += nl;
+    }
+  }
   // fused input projection / output stage: bf16 mirrors of W_in, W_skip, W_out present
   const __bf16* Winb = lookup_bf16(h->Win);
   const __bf16* Wsb = lookup_bf16(h->Ws);
   const __bf16* Wob = lookup_bf16(h->Wo);
   const bool fuse_in = stack && h->stack_fuse && Winb && h->ldw_in <= 128 && M % 4 == 0;
   // (the fused tail stores mel through a buffer resource: 32-bit byte offsets)
-  const bool fuse_tail = fuse_in && tail && Wsb && Wob && M <= 8 * 32 && C == WNF_C && Ly > h->stack_nl &&
+  const bool fuse_tail = fuse_in && tail && Wsb && Wob && M <= 8 * 32 && C == WNF_C && ngrp > 1 &&
                          (long long)B * T * M * 4 < (1ll << 31) && (long long)B * T * C * 4 < (1ll << 31);
   if (!fuse_in) {  // x = relu(W_in spec + b)   (wavenet.py:108-111)
     GemmArgs a = make_gemm(B, T, C, h->Win, h->ldw_in, h->b_in, x, BTs * C, C);
@@ -1506,7 +1578,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       }
     }
   } else if (stack) {
-    // bf16, dilation 1: stack_nl residual layers per launch (wn_stack_bf16_kernel), x ping-pongs
+    // bf16: the layer groups above, one wn_stack_bf16_kernel launch each, x ping-pongs
     __bf16* condb = reinterpret_cast<__bf16*>(ws + Lw.condb);
     {
       ProfScope ps("wn_condb", st);
@@ -1515,26 +1587,27 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       PD_LAUNCH_CHECK();
     }
     float* xb[2] = {x, ws + Lw.x2};
-    int k = 0;
-    for (int l0 = 0; l0 < Ly; l0 += h->stack_nl, ++k) {
+    for (int k = 0; k < ngrp; ++k) {
+      const int l0 = grp[k][0], l1 = k + 1 < ngrp ? grp[k + 1][0] : Ly;
       WnStackArgs P{};
       P.xin = xb[k & 1]; P.xout = xb[(k + 1) & 1]; P.skip = skip; P.condb = condb;
       P.dp = dproj; P.dp_ld = Ly * C;
       P.W1f = h->W1f; P.b1 = h->bl1; P.W2f = h->W2f; P.b2 = h->bl2;
-      P.rows = rows; P.T = T; P.l0 = l0; P.nl = std::min(h->stack_nl, Ly - l0); P.first = l0 == 0; P.L = Ly;
-      P.lens = lens;
+      P.rows = rows; P.T = T; P.l0 = l0; P.nl = l1 - l0; P.first = l0 == 0; P.L = Ly;
+      P.lens = lens; P.cyc = h->cyc;
       // output rows per block (PD_WN_OPT_STACK_RO; r04 default 32).  r04: spreading C3's 6888 rows over
       // all 256 CUs (27 rows per block) measured slower than 216 blocks of 32 (214 vs 202-205 us per
       // 10 layers, profiles/r04_ab/): every block streams each layer's 1.3 MB of weights from its
       // XCD's L2, and 32 blocks per XCD instead of 27 share that L2's bandwidth
       // r05: the halo is the launch's layer count (>= 8, the skip image's first row), and the
       // default writes every exact row, 64 - 2 hl (44 at 10 layers)
-      P.hl = std::max(P.nl, 8);
+      // (cycle > 1: the sum of the group's dilations)
+      P.hl = std::max(grp[k][1], 8);
       P.ro = std::min(h->stack_ro > 0 ? h->stack_ro : 64, 64 - 2 * P.hl);
       if (fuse_in && l0 == 0) {
         P.spec = xin; P.Winb = Winb; P.b_in = h->b_in; P.M = M; P.ldw_in = h->ldw_in;
       }
-      if (fuse_tail && l0 + P.nl >= Ly) {   // (not the first launch: it reads mel, this one writes it)
+      if (fuse_tail && k == ngrp - 1) {   // (not the first launch: it reads mel, this one writes it)
         P.Wsb = Wsb; P.bs = h->bs; P.Wob = Wob; P.bo = h->bo; P.M = M;
         P.skip_scale = 1.0f / sqrtf((float)Ly);   // the skip head's segment scale below
         P.mel = tail->mel; P.c1 = tail->c1; P.c2 = tail->c2; P.sigma = tail->sigma;
@@ -1543,9 +1616,7 @@ int wavenet_core(const pd_wavenet* h, float* ws, const WsLayout& Lw, const float
       }
       ProfScope ps("wn_stack", st);
       const dim3 grid((unsigned)cdiv(rows, P.ro));
-      if (P.spec) hipLaunchKernelGGL((wn_stack_bf16_kernel<true, false>), grid, dim3(512), 0, st, P);
-      else if (P.Wsb) hipLaunchKernelGGL((wn_stack_bf16_kernel<false, true>), grid, dim3(512), 0, st, P);
-      else hipLaunchKernelGGL((wn_stack_bf16_kernel<false, false>), grid, dim3(512), 0, st, P);
+      launch_wn_stack(P, grid, h->cyc > 1, st);
       PD_LAUNCH_CHECK();
     }
   } else if (h->W1f) {
@@ -2003,8 +2074,14 @@ int pd_reflow_sample(const pd_wavenet* h, const float* cond, int S, int algo, fl
         xin = xs;
       }
       const int e = i * tb.s + j;
-      PD_TRY(wavenet_core(h, ws, Lw, xin, cond, ws + Lw.dproj + (size_t)e * B * Ly * C, B, T, st, nullptr, nullptr,
-                          lens));
+      // Euler (the reference's default, handler/base_config.yaml:204): x += v dt is the posterior
+      // epilogue with c1 = dt, c2 = 1, sigma = 0, fused into the last stack launch when it can be
+      StackTail tl{};
+      tl.mel = x; tl.c1 = dts; tl.c2 = 1.f; tl.sigma = 0.f;
+      bool done = false;
+      PD_TRY(wavenet_core(h, ws, Lw, xin, cond, ws + Lw.dproj + (size_t)e * B * Ly * C, B, T, st,
+                          tb.s == 1 ? &tl : nullptr, &done, lens));
+      if (done) continue;
       GemmArgs a = make_gemm(B, T, M, h->Wo, C, h->bo, tb.s == 1 ? x : kb + (size_t)j * kstride, BTs * M, M);
       add_seg(a, make_seg(ws + Lw.hs, BTs * C, C, C, 0));
       if (tb.s == 1) {   // Euler: x += v dt fused into the output projection (reflow.py:50)

@@ -316,6 +316,21 @@ class JobStreams:
         return torch.cuda.stream(s)
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_streams(dev, cur, n):
+    """``n`` side streams for ragged batches issued from stream ``cur``, created once and reused
+    by every later call (new streams per call came round-robin from torch's pool, and
+    every module keeps one grow-only workspace per stream, so a serving loop accumulated up to ~32
+    full-size workspaces).  Keyed by the issuing stream, so jobs in flight on different
+    ``JobStreams`` streams keep separate side streams (and workspaces) and still overlap."""
+    lst = _SIDE_STREAMS.setdefault((str(dev), cur.cuda_stream), [])
+    while len(lst) < n:
+        lst.append(torch.cuda.Stream(dev))
+    return lst[:n]
+
+
 def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None,
                            collectives=False, max_waste=0.15, streams=4, max_frames=None):
     """Synthesize utterances sharded over the ranks of the default process group
@@ -374,7 +389,7 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         if getattr(synth_fn, "prepare", None):
             synth_fn.prepare()
         cur = torch.cuda.current_stream(dev)
-        side = [torch.cuda.Stream(dev) for _ in range(min(streams, len(plan)))]
+        side = _side_streams(dev, cur, min(streams, len(plan)))
         for s in side:
             s.wait_stream(cur)          # the inputs and the packed handles are ready
 

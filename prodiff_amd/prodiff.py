@@ -285,7 +285,11 @@ class GaussianDiffusion(nn.Module):
         cond = cond.float().contiguous()
         xT = None if x_T is None else x_T.float().contiguous().clone()
         nz = None if noise is None else noise.float().contiguous().clone()
-        ws = _lib.Workspace()    # the graph's own: later eager calls may grow (reallocate) self._ws
+        # the graph's own workspace, one buffer for every stream: the warm-up call below sizes it on
+        # the current stream and the capture (on torch's capture stream) reuses it instead of
+        # allocating a second full-size buffer from the graph pool; later eager calls may grow
+        # (reallocate) self._ws without touching it
+        ws = _lib.Workspace(per_stream=False)
         uid = _lib.utt_ids(utt_ids, cond.shape[0], cond.device)
         self.sample(cond, infer_step=infer_step, seed=seed, x_T=xT, noise=nz, workspace=ws, utt_ids=uid)   # packs, sizes ws
         torch.cuda.synchronize()

@@ -507,6 +507,100 @@ def gen_cond():
              cond=cond, enc=enc_out["enc"].numpy(), grow=grow, **{k: v for k, v in x.items()}, **extra)
 
 
+# --------------------------------------------------------------------------
+# Full-size SVS chain (C5's shapes at real segment lengths): the reference teacher's
+# forward_condition (prodiff_teacher.py:103-146) -> GaussianDiffusion 4-iter at M=128
+# (prodiff.py:136-153) -> NSF-HiFiGAN spec2wav_torch (component/vocoder/nsf_hifigan.py:29-58,
+# models.py:21-297), each segment alone (B=1: the reference SineGen is batch-1 only,
+# models.py:162-163, and the handler runs one segment at a time, handler/infer/handler.py:373-388).
+# Lengths and phoneme counts are two real segments of the reference's sample song
+# (tests/golden/ds_lengths.json: segment 21, 286 frames / 6 phonemes; segment 0, 504 / 24).
+# Weights are SvsSynthesizer.synthetic(seed)'s (cond seed, WaveNet seed + 1, NSF seed + 2);
+# inputs come from synth.synth_svs_utterance; every draw from synth.synth_inputs keyed by
+# (draw seed * 1000 + draw index) -- torch.rand (x_T) and 4 x torch.randn for the sampler,
+# torch.rand(1, 9) and torch.randn_like for the SineGen -- so only outputs are stored.
+# --------------------------------------------------------------------------
+FULLSIZE_C5 = {
+    # name: (ds segment, frames, phonemes, utterance seed, prodiff draw seed, nsf draw seed)
+    "fullsize_c5_s21": (21, 286, 6, 171, 173, 175),
+    "fullsize_c5_s0": (0, 504, 24, 172, 174, 176),
+}
+C5_WEIGHT_SEED = 71
+
+
+def gen_fullsize_c5():
+    import json
+    from modules.nsf_hifigan.env import AttrDict
+    from modules.nsf_hifigan.models import Generator
+    from modules.svs.prodiff_teacher import ProDiffTeacher
+    from prodiff_amd.pipeline import SVS_TEACHER, SVS_VOCAB
+    ds = json.load(open(os.path.join(HERE, "ds_lengths.json")))
+    hp = dict(SVS_TEACHER)
+    t = ProDiffTeacher(SVS_VOCAB, hp).eval()
+    cp = synth.synth_cond_params(synth.cond_param_shapes(SVS_VOCAB, num_langs=len(hp["languages"]) + 1,
+                                                         **{k: v for k, v in hp.items() if k != "num_langs"}),
+                                 C5_WEIGHT_SEED)
+    wn = synth.synth_params(synth.wavenet_param_shapes(hp["audio_num_mel_bins"], hp["hidden_size"],
+                                                       hp["residual_layers"], hp["residual_channels"]),
+                            C5_WEIGHT_SEED + 1)
+    sd = t.state_dict()
+    full = {k: torch.from_numpy(v) for k, v in cp.items()}
+    full.update({"diffusion.denoise_fn." + k: torch.from_numpy(v) for k, v in wn.items()})
+    for k, v in full.items():
+        assert tuple(sd[k].shape) == tuple(v.shape), (k, sd[k].shape, v.shape)
+    t.load_state_dict(full, strict=False)
+    h = dict(synth.NSF_DEFAULTS)
+    g = Generator(AttrDict(num_mels=h["num_mels"], upsample_initial_channel=h["upsample_initial_channel"],
+                           upsample_rates=list(h["upsample_rates"]),
+                           upsample_kernel_sizes=list(h["upsample_kernel_sizes"]), resblock=h["resblock"],
+                           resblock_kernel_sizes=list(h["resblock_kernel_sizes"]),
+                           resblock_dilation_sizes=[list(d) for d in h["resblock_dilation_sizes"]],
+                           sampling_rate=h["sampling_rate"]))
+    g.remove_weight_norm()
+    g.load_state_dict({k: torch.from_numpy(v)
+                       for k, v in synth.synth_params(synth.nsf_param_shapes(**h), C5_WEIGHT_SEED + 2).items()},
+                      strict=True)
+    g.eval()
+    for name, (seg, T, ntok, us, ps, ns) in FULLSIZE_C5.items():
+        assert ds["frames"][seg] == T and ds["phonemes"][seg] == ntok, (seg, T, ntok)
+        u = synth.synth_svs_utterance(us, T, ntok, SVS_VOCAB)
+        ins = {k: torch.from_numpy(v)[None] for k, v in u.items()}
+        conds = {}
+        hk = t.diffusion.register_forward_pre_hook(lambda mod, a: conds.setdefault("cond", a[0].detach().clone()))
+        with torch.no_grad(), Recorder(ps) as rec:
+            mel = t(ins["txt_tokens"], ins["mel2ph"], ins["f0"], lang_seq=ins["lang_seq"],
+                    spk_mix_embed=ins["spk_mix_embed"], voicing=ins["voicing"], breath=ins["breath"],
+                    infer=True)
+        hk.remove()
+        assert len(rec.rand) == 1 and len(rec.randn) == 4
+        # spec2wav_torch (nsf_hifigan.py:50-56) with the SineGen draws replayed from synth
+        cnt = [0]
+        r0, rl = torch.rand, torch.randn_like
+
+        def rand(*size, device=None, **kw):
+            assert cnt[0] == 0 and tuple(size) == (1, 9), size
+            cnt[0] += 1
+            return torch.from_numpy(synth.synth_inputs(ns * 1000, (1, 9), kind="uniform"))
+
+        def randn_like(x, **kw):
+            assert cnt[0] == 1
+            cnt[0] += 1
+            return torch.from_numpy(synth.synth_inputs(ns * 1000 + 1, tuple(x.shape)))
+
+        torch.rand, torch.randn_like = rand, randn_like
+        try:
+            with torch.no_grad():
+                c = 2.30259 * mel.transpose(2, 1)
+                wav = g(c, ins["f0"]).view(-1).numpy()
+        finally:
+            torch.rand, torch.randn_like = r0, rl
+        assert cnt[0] == 2 and wav.shape == (T * 512,)
+        w64 = wav.astype(np.float64)
+        save(name, segment=seg, T=T, ntok=ntok, weight_seed=C5_WEIGHT_SEED, utt_seed=us, prodiff_seed=ps,
+             nsf_seed=ns, cond=conds["cond"].numpy()[0], mel=mel.numpy()[0], wav=wav.astype(np.float32),
+             wav_l2=np.linalg.norm(w64), wav_mean=w64.mean(), wav_absmax=np.abs(w64).max())
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:          # e.g. `gen_golden.py reflow` regenerates one family
         globals()["gen_" + sys.argv[1]]()

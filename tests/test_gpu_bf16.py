@@ -324,3 +324,59 @@ def test_prodiff_stack_fuse_bitexact(draws, M, B, T, S):
     assert np.isfinite(outs[1]).all()
     np.testing.assert_array_equal(outs[1], outs[0])
     np.testing.assert_array_equal(fwd[1], fwd[0])
+
+
+@pytest.mark.parametrize("cyc,M", [(5, 64), (2, 80), (3, 128)])
+@pytest.mark.parametrize("B,T", [(2, 64), (3, 101), (1, 300)])
+def test_wavenet_stack_dilation_bitexact(cyc, M, B, T):
+    """r06: the stack kernel at dilation cycles > 1 (the pitch predictor's WaveNet: cycle 5, M = 64,
+    pitch_predictor.py:40-55) -- layers grouped so each launch's dilations sum to <= 16 (cycle 5:
+    {1,2,4,8} and {16}), taps at -+2^(l % cyc) -- against the one-layer kernel: bit-identical (batch
+    rows end inside the windows; the dilation-16 taps cross the whole halo).  Then within the bf16
+    bar of the fp32 path."""
+    torch.manual_seed(13 + cyc)
+    net = WaveNet(M, 256, 20, 256, cyc)
+    spec = torch.randn(B, 1, M, T, device=DEV)
+    cond = torch.randn(B, 256, T, device=DEV)
+    steps = torch.tensor([3.0, 511.0, 77.0][:B], device=DEV)
+    outs = {}
+    for name, opts in (("layer", dict(layer=0, stack=0)), ("stack", dict(stack=10))):
+        m = WaveNet(M, 256, 20, 256, cyc)
+        m.load_state_dict(net.state_dict())
+        m = m.to(DEV).set_compute_dtype("bf16").set_options(**opts)
+        outs[name] = m(spec, steps, cond).float().cpu().numpy()
+    np.testing.assert_array_equal(outs["stack"], outs["layer"])
+    m32 = WaveNet(M, 256, 20, 256, cyc)
+    m32.load_state_dict(net.state_dict())
+    ref = m32.to(DEV)(spec, steps, cond).float().cpu().numpy()
+    assert_bf16_close(outs["stack"], ref, f"wavenet cyc={cyc} stack B={B} T={T}")
+
+
+@pytest.mark.parametrize("algo", ["euler", "rk2"])
+@pytest.mark.parametrize("ragged", [False, True])
+def test_pitch_reflow_stack_bitexact(algo, ragged):
+    """The pitch predictor's sampler (PitchRectifiedFlow, 20 steps, WaveNet cycle 5, M = 64) on the
+    stack kernel -- with Euler's x += v dt fused into the last stack launch (the posterior epilogue
+    with c1 = dt, c2 = 1) -- against the one-layer kernel with the separate skip-head and output
+    launches: bit-identical, dense and ragged (per-row lens)."""
+    from prodiff_amd import PitchRectifiedFlow
+    torch.manual_seed(17)
+    B, T = 3, 150
+    net = WaveNet(64, 256, 20, 256, 5)
+    cond = torch.randn(B, T, 256, device=DEV)
+    xT = torch.randn(B, 1, 64, T, device=DEV)
+    lens = [150, 97, 64] if ragged else None
+    outs = {}
+    for name, opts in (("layer", dict(layer=0, stack=0)), ("stack", dict(stack=10))):
+        m = WaveNet(64, 256, 20, 256, 5)
+        m.load_state_dict(net.state_dict())
+        rf = PitchRectifiedFlow(64, m, time_scale=1000, sampling_algorithm=algo).to(DEV)
+        rf.set_compute_dtype("bf16")
+        m.set_options(**opts)
+        outs[name] = rf.sample(cond, infer_step=20 if algo == "euler" else 4, x_T=xT, lens=lens).cpu().numpy()
+    assert np.isfinite(outs["stack"]).all()
+    if ragged:
+        for r, n in enumerate(lens):
+            np.testing.assert_array_equal(outs["stack"][r, :n], outs["layer"][r, :n])
+    else:
+        np.testing.assert_array_equal(outs["stack"], outs["layer"])

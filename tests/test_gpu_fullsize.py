@@ -10,8 +10,14 @@
   the bf16 bar of tests/test_gpu_bf16.py.  This runs the grid-scale code the
   bench times: thousands of 384-row LVC tiles, the XCD block remap with a block
   count not divisible by 8, the kernel-predictor grouping, the 1.2 GB workspace.
+* The C3 slice in bf16 directly against the reference's outputs (the bench's dtype pinned to
+  the reference itself, not only to the fp32 HIP path).
+* C5 at real length (r06): two segments of the reference's sample song (286 and 504 frames)
+  through the reference's SVS chain -- teacher condition, ProDiff 4-iter M=128, NSF-HiFiGAN
+  spec2wav_torch -- fp32 stage by stage and end to end (<= 1e-4), bf16 end to end at the
+  shared bar, and both segments in one ragged batch.
 Every input and draw is regenerated from its seed (tests/golden/gen_golden.py,
-FULLSIZE_CASES), so only outputs are committed.
+FULLSIZE_CASES, FULLSIZE_C5), so only outputs are committed.
 """
 import numpy as np
 import pytest
@@ -184,6 +190,118 @@ def test_c5_full_bf16_vs_fp32(B):
     assert np.isfinite(outs["fp32"][1]).all() and np.abs(outs["fp32"][1]).max() <= 1.0
     assert_bf16_close(outs["bf16"][0], outs["fp32"][0], f"C5 mel bf16 vs fp32, {B}x861")
     assert_bf16_close(outs["bf16"][1], outs["fp32"][1], f"C5 wav bf16 vs fp32, {B}x861")
+
+
+def test_c3_slice_bf16_vs_reference(c3):
+    """The bench's bf16 chain directly against the reference's own C3 outputs (fullsize_c3_b2:
+    2 x 861 frames, ProDiff 2-iter -> FastDiff 4-iter, the reference's draws): the shared bf16
+    output bar, mel and the whole waveform -- the bf16 path pinned to the reference itself, not
+    only to the fp32 HIP path."""
+    B, T, ps = int(c3["B"]), int(c3["T"]), int(c3["prodiff_seed"])
+    xT, nz = prodiff_draws(ps, B, T)
+    mel = prodiff(ps, "bf16").sample(tt(synth.synth_inputs(ps + 300, (B, T, 256))), x_T=tt(xT), noise=tt(nz))
+    assert_bf16_close(mel.cpu().numpy(), c3["mel"], "C3-slice ProDiff bf16 vs reference")
+    wT, wn = fastdiff_draws(int(c3["draw_seed"]), B, T * 256)
+    b, a, s, st = SCHED
+    m = fastdiff(int(c3["fastdiff_seed"]), "bf16")
+    wav = m.sample(tt(c3["mel"]), b, a, s, st, x_T=tt(wT), noise=tt(wn))[:, 0].cpu().numpy()
+    assert_bf16_close(wav, c3["wav"], "C3-slice FastDiff bf16 vs reference (reference mel in)")
+    wav2 = m.sample(mel, b, a, s, st, x_T=tt(wT), noise=tt(wn))[:, 0].cpu().numpy()
+    assert_bf16_close(wav2, c3["wav"], "C3-slice chain bf16 vs reference (bf16 mel in)")
+
+
+C5_CASES = ("fullsize_c5_s21", "fullsize_c5_s0")
+
+
+def _c5_case(name, dtype):
+    """The SVS chain of gen_golden.gen_fullsize_c5 on the GPU: weights of SvsSynthesizer.synthetic
+    (the fixture's weight seed), the segment's inputs, the reference's recorded draws."""
+    from prodiff_amd.pipeline import SVS_VOCAB, SvsSynthesizer
+    d = G.load(name)
+    T, ntok = int(d["T"]), int(d["ntok"])
+    u = {k: tt(v) for k, v in synth.synth_svs_utterance(int(d["utt_seed"]), T, ntok, SVS_VOCAB).items()}
+    syn = SvsSynthesizer.synthetic(DEV, seed=int(d["weight_seed"]), dtype=dtype)
+    ps, ns = int(d["prodiff_seed"]), int(d["nsf_seed"])
+    xT = synth.synth_inputs(ps * 1000, (1, 1, 128, T), kind="uniform")
+    nz = np.stack([synth.synth_inputs(ps * 1000 + 1 + j, (1, 1, 128, T)) for j in range(4)])
+    ri = synth.synth_inputs(ns * 1000, (1, 9), kind="uniform")
+    wn = synth.synth_inputs(ns * 1000 + 1, (1, T * 512, 9))
+    return d, u, syn, (tt(xT), tt(nz), tt(ri), tt(wn))
+
+
+@pytest.mark.parametrize("name", C5_CASES)
+def test_c5_fullsize_fp32_vs_reference(name):
+    """C5 at real segment length (two segments of the reference's sample song, 286 and 504
+    frames) against the reference's own SVS chain, stage by stage, fp32: the teacher's
+    condition, the 4-iter M=128 sampler (the reference's condition in), NSF-HiFiGAN
+    spec2wav_torch (the reference's mel in; 146k / 258k samples), bar 1e-4 (north star)."""
+    from prodiff_amd.nsf_hifigan import LOG10_TO_LN
+    from prodiff_amd.pipeline import SvsSynthesizer
+    d, u, syn, (xT, nz, ri, wn) = _c5_case(name, "fp32")
+    cond = syn.condition(SvsSynthesizer.collate([u]))
+    e_c = float(np.abs(cond[0].cpu().numpy() - d["cond"]).max())
+    mel = syn.diffusion.sample(tt(d["cond"][None]), infer_step=4, x_T=xT, noise=nz)
+    e_m = float(np.abs(mel[0].cpu().numpy() - d["mel"]).max())
+    wav = syn.generator.synthesize(tt(d["mel"][None]), u["f0"][None], LOG10_TO_LN, rand_ini=ri, noise=wn)
+    w = wav[0].cpu().numpy().astype(np.float64)
+    e_w = float(np.abs(w - d["wav"]).max())
+    print(f"{name} fp32 max|d|: cond {e_c:.3e}, mel {e_m:.3e}, wav {e_w:.3e} (max|ref| {np.abs(d['wav']).max():.3f})")
+    assert e_c <= ABS and e_m <= ABS and e_w <= ABS
+    np.testing.assert_allclose(np.linalg.norm(w), float(d["wav_l2"]), rtol=1e-5)
+    # the whole chain from the segment's inputs, fp32, as the bench runs it
+    mel2 = syn.diffusion.sample(cond, infer_step=4, x_T=xT, noise=nz)
+    wav2 = syn.generator.synthesize(mel2, u["f0"][None], LOG10_TO_LN, rand_ini=ri, noise=wn)
+    e2m = float(np.abs(mel2[0].cpu().numpy() - d["mel"]).max())
+    e2w = float(np.abs(wav2[0].cpu().numpy() - d["wav"]).max())
+    print(f"{name} fp32 chain max|d|: mel {e2m:.3e}, wav {e2w:.3e}")
+    assert e2m <= ABS and e2w <= ABS
+
+
+@pytest.mark.parametrize("name", C5_CASES)
+def test_c5_fullsize_bf16_vs_reference(name):
+    """The bench's bf16 SVS chain (condition encoder, ProDiff 4-iter M=128, NSF on the windowed
+    MFMA convs) from the segment's inputs straight to the waveform, against the reference's
+    outputs: the shared bf16 output bar."""
+    from prodiff_amd.nsf_hifigan import LOG10_TO_LN
+    from prodiff_amd.pipeline import SvsSynthesizer
+    d, u, syn, (xT, nz, ri, wn) = _c5_case(name, "bf16")
+    cond = syn.condition(SvsSynthesizer.collate([u]))
+    assert_bf16_close(cond[0].cpu().numpy(), d["cond"], f"{name} cond bf16 vs reference")
+    mel = syn.diffusion.sample(cond, infer_step=4, x_T=xT, noise=nz)
+    assert_bf16_close(mel[0].cpu().numpy(), d["mel"], f"{name} mel bf16 vs reference")
+    wav = syn.generator.synthesize(mel, u["f0"][None], LOG10_TO_LN, rand_ini=ri, noise=wn)
+    assert_bf16_close(wav[0].cpu().numpy(), d["wav"], f"{name} wav bf16 vs reference")
+
+
+def test_c5_fullsize_ragged_pair_vs_reference():
+    """Both real-length segments in ONE ragged batch (286 + 504 frames, each row's own ``lens``),
+    fp32, explicit per-row draws: every row equals the reference's segment-alone output."""
+    from prodiff_amd.pipeline import SvsSynthesizer
+    cases = [_c5_case(n, "fp32") for n in C5_CASES]
+    syn = cases[0][2]
+    T = max(int(c[0]["T"]) for c in cases)
+    lens = [int(c[0]["T"]) for c in cases]
+    batch = SvsSynthesizer.collate([c[1] for c in cases])
+    cond = syn.condition(batch)
+
+    def pad(x, axis, n):
+        w = [(0, 0)] * x.dim()
+        w[axis] = (0, n - x.shape[axis])
+        return torch.nn.functional.pad(x, [p for pr in reversed(w) for p in pr])
+
+    xT = torch.cat([pad(c[3][0], 3, T) for c in cases], 0)
+    nz = torch.cat([pad(c[3][1], 4, T) for c in cases], 1)
+    for r, c in enumerate(cases):
+        e = float(np.abs(cond[r, :lens[r]].cpu().numpy() - c[0]["cond"]).max())
+        print(f"ragged row {r} ({lens[r]} frames) cond max|d| {e:.3e}")
+        assert e <= ABS
+    mel = syn.diffusion.sample(cond, infer_step=4, x_T=xT, noise=nz, lens=lens)
+    for r, c in enumerate(cases):
+        e = float(np.abs(mel[r, :lens[r]].cpu().numpy() - c[0]["mel"]).max())
+        print(f"ragged row {r} ({lens[r]} frames) mel max|d| {e:.3e}")
+        assert e <= ABS
+    # (NSF takes one explicit rand_ini per call, as the reference draws one per segment: the
+    # ragged NSF batch is covered with on-device draws in tests/test_gpu_ragged.py)
 
 
 def test_c3_jobs_in_flight_bitexact():

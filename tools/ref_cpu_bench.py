@@ -17,6 +17,9 @@ synthetic weights (prodiff_amd.synth) and times, fp32 under torch.no_grad():
       (modules/svs/prodiff_teacher.py:148-168: FFT-encoder condition + 4-iter ProDiff, M=128)
       then the NSF-HiFiGAN Generator (modules/nsf_hifigan/models.py:222-283, 44.1 kHz, hop 512)
       on 8 segments x 861 frames (10 s each)
+  PITCH: the pitch predictor's sampler (r06): PitchRectifiedFlow (reflow.py:86-144) over
+      WaveNet(64, 256, 20, 256, dilation cycle 5) (pitch_predictor.py:40-55,
+      handler/base_config.yaml:135-149), 20 Euler steps + denorm_spec, segments one at a time
 
 ``--configs C5`` re-times only the named configs and merges them into the JSON.
 
@@ -99,7 +102,7 @@ def main():
     ap.add_argument("--threads", type=int, default=os.cpu_count())
     ap.add_argument("--repeats", type=int, default=5)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02_ref_cpu.json"))
-    ap.add_argument("--configs", default="C3,C2,C5")
+    ap.add_argument("--configs", default="C3,C2,C5,PITCH")
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     want = set(args.configs.split(","))
@@ -110,6 +113,9 @@ def main():
     if "C5" in want:
         res["C5"] = bench_c5(args.repeats)
         print("C5", res["C5"], flush=True)
+    if "PITCH" in want:
+        res["PITCH"] = bench_pitch(args.repeats)
+        print("PITCH", res["PITCH"], flush=True)
     if not want & {"C3", "C2"}:
         return write(args, res)
     gd, fd, dh = build()
@@ -199,6 +205,30 @@ def bench_c5(repeats, B=2, T=861, tokens=120):
                       f"at 44.1 kHz), "
                       f"{tokens} phonemes each: ProDiffTeacher.forward(infer=True) (encoder condition + "
                       f"4-iter ProDiff, M=128) + NSF-HiFiGAN Generator, fp32"}
+
+
+def bench_pitch(repeats, B=2, T=861):
+    """The pitch predictor's diffusion sampler, one segment at a time (B=1, as the handler runs
+    them): PitchRectifiedFlow.forward(cond, infer_step=20, infer=True) -> pitch [1, T]."""
+    from modules.diffusion.reflow import PitchRectifiedFlow
+    net = WaveNet(64, 256, 20, 256, 5)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in
+                         synth.synth_params(synth.wavenet_param_shapes(64, 256, 20, 256), 0).items()})
+    rf = PitchRectifiedFlow(repeat_bins=64, denoise_fn=net, time_scale=1000, sampling_algorithm="euler",
+                            spec_min=-8.0, spec_max=8.0, clamp_min=-12.0, clamp_max=12.0).eval()
+    conds = [torch.from_numpy(synth.synth_inputs(i, (1, T, 256))) for i in range(B)]
+
+    @torch.no_grad()
+    def run():
+        for c in conds:
+            rf(c, infer_step=20, infer=True)
+
+    med, ts = timed(run, repeats)
+    audio = B * T * 512 / 44100
+    return {"mel_frames_per_s": round(B * T / med, 2), "seconds_median": round(med, 3), "repeats": repeats,
+            "seconds_all": [round(x, 3) for x in ts], "rtf": round(med / audio, 4),
+            "sample": f"reference modules, {B} segments one at a time (B=1) x {T} frames: PitchRectifiedFlow "
+                      f"(20 Euler steps, WaveNet 20x256, M=64 repeat bins, dilation cycle 5) + denorm_spec, fp32"}
 
 
 def write(args, res):
