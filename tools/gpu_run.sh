@@ -27,6 +27,7 @@ bench_args() {   # config -> bench.py arguments
 regex() {        # config -> kernels the PMC passes cover
   case $1 in
     C5*) echo "nsf_pair_kernel|nsf_wconv|nsf_ups_kernel|wn_stack_bf16" ;;
+    PITCH) echo "wn_stack_bf16|wn_xa|matvec" ;;
     *) echo "lvc_block_bf16_kernel|kp_kernel_bf16|wn_stack_bf16|kp_hidden_bf16|dblock_bf16" ;;
   esac
 }
@@ -56,7 +57,7 @@ print(sys.argv[2], d['ms_per_step'], 'ms/step', d['value'], d['roofline']['kerne
           python -u $R/bench.py $(bench_args $val) --overlap 1 --steps 2 --warmup 1 --cpu-frames 0 --no-kernel-timing \
           > $O/pmc_${val}_$pmc.log 2>&1)
       done
-      case $val in C4) b=32 ;; *) b=8 ;; esac
+      case $val in C4) b=32 ;; *) b=8 ;; esac   # (PITCH: 8 x 861 too)
       python tools/pmc_traffic.py $O/pmc_$val $O/${val}_traffic.json $TAG ${val%DS} $b 861 ;;
     sq)
       timeout -k 10 500 tools/pmc_sq.sh $TAG/sq_$val "$(regex $val)|enc_|dblock_bf16" $(bench_args $val) --overlap 1 --steps 1
