@@ -679,42 +679,41 @@ def main():
             syn.diffusion.denoise_fn.set_options(**{k: int(v) for k, v in (o.split("=") for o in args.wn_opt)})
         synth_fn = syn
 
-    phase = {"compute_ms": 0.0, "gather_ms": 0.0, "n": 0}    # N > 1: where each timed step went
+    phase_marks = []    # N > 1: per timed step, where it went (event marks, read after the timed region)
     ovl = None      # JobStreams when --overlap > 1
     if args.overlap is None:
-        # jobs in flight on one GPU (measured, profiles/r05_ab/job_overlap*_ab.txt): C3 2 (3: the same),
-        # C5 3 (2 on the .ds lengths, whose ragged batches already run on 4 streams); 1 with N > 1 ranks
-        # (each rank's gather runs on its job's stream) and for C4 (the scaling line)
+        # jobs in flight (measured on one GPU, profiles/r05_ab/job_overlap*_ab.txt): C3 2 (3: the same),
+        # C5 3 (2 on the .ds lengths, whose ragged batches already run on 4 streams), C4 2 (-1.4%).
+        # N > 1 ranks (r06): 2, so job i's RCCL gather to rank 0 runs beside job i + 1's compute
         args.overlap = 1
-        if world == 1 and cfg_name == "C3":
+        if cfg["vocoder"]:
             args.overlap = 2
-        elif world == 1 and cfg_name == "C5":
-            args.overlap = 2 if args.lengths == "ds" else 3
-    elif world > 1 and args.overlap > 1:
-        # every rank's gather is an RCCL collective on its job's stream: jobs in flight would put
-        # collectives of one communicator on several streams at once, which this bench does not do
-        raise SystemExit("--overlap > 1 is for one GPU (N > 1 ranks run one job at a time)")
+            if world == 1 and cfg_name == "C5" and args.lengths != "ds":
+                args.overlap = 3
 
     if cfg["vocoder"]:
-        if args.overlap > 1 and not dry:
+        if args.overlap > 1:
             # consecutive jobs on alternating HIP streams (pipeline.JobStreams): one job's
             # low-occupancy launches (the ProDiff WaveNet stack fills 157 of 256 CUs at C3) overlap
             # the previous job's vocoder.  Handles are packed first (stream-ordered packing).
-            if getattr(synth_fn, "prepare", None):
+            # N > 1: a job's gathers are issued from its own stream; torch's process group runs every
+            # collective on ONE collective stream per device in host issue order -- the same on every
+            # rank -- which waits for the issuing job's stream, and the job's stream waits for the
+            # gathers (no host wait).  So job i's gather overlaps job i + 1's compute on the other stream.
+            if getattr(synth_fn, "prepare", None) and not dry:
                 synth_fn.prepare()
-            torch.cuda.synchronize()
-            ovl = JobStreams(args.overlap, dev)
+            if not dry:
+                torch.cuda.synchronize()
+            ovl = JobStreams(args.overlap, dev)     # (a CPU device: a no-op, same schedule on the host)
 
         def step(i, timed=False, iso=False):
-            st = {} if (timed and world > 1) else None
+            st = {} if (timed and not iso and world > 1) else None
             ctx = ovl.next() if (ovl and not iso) else contextlib.nullcontext()
             with ctx:
                 out = distributed_synthesize(synth_fn, conds, seed=10_000 * i, device=dev, hop=hop, stats=st,
                                              max_frames=args.max_frames or None)
-            if st:
-                phase["compute_ms"] += st["compute_ms"]
-                phase["gather_ms"] += st["gather_ms"]
-                phase["n"] += 1
+            if st is not None:
+                phase_marks.append(st)
             return out
     elif pitch:
         # PITCH: 20 Euler steps (every velocity evaluation the fused WaveNet stack, x += v dt in its
@@ -834,9 +833,12 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        if phase["n"]:
-            # per-step compute (own shard, device-synchronized) and gather of every rank
-            v = torch.tensor([phase["compute_ms"] / phase["n"], phase["gather_ms"] / phase["n"]],
+        if phase_marks:
+            # per-step compute (own shard) and gather of every rank, from the HIP events each timed
+            # job recorded on its stream (no synchronisation inside the timed steps)
+            from prodiff_amd.pipeline import phase_ms
+            pm = [phase_ms(st) for st in phase_marks]
+            v = torch.tensor([sum(c for c, _ in pm) / len(pm), sum(g for _, g in pm) / len(pm)],
                              device=dev, dtype=torch.float64)
             allv = [torch.empty_like(v) for _ in range(world)]
             dist.all_gather(allv, v)
@@ -846,7 +848,9 @@ def main():
                       "compute_ms_per_step_fastest_rank": round(min(c), 3),
                       "gather_ms_per_step_max": round(max(g), 3),
                       "gather_ms_per_step_rank0": round(g[0], 3),
-                      "note": "per rank: its shard's synthesis (synchronized) then the ragged RCCL gather to rank 0"}
+                      "note": "per rank, from HIP events on each timed job's stream: its shard's synthesis, then "
+                              "the ragged RCCL gather to rank 0 (with jobs in flight the gather overlaps the next "
+                              "job's compute on the other job stream)"}
     if rank == 0 and not dry:
         if cfg["vocoder"]:
             mels, wavs = out
@@ -932,6 +936,10 @@ def main():
                    f"{n_batches} padded batches per GPU (ragged_batches, <= 15% padding)",
                    "batches_per_gpu": n_batches,
                    "jobs_in_flight": ovl.depth if ovl is not None else 1,
+                   "schedule": None if ovl is None or ovl.depth == 1 else
+                   (f"job i on HIP stream i % {ovl.depth}" + (
+                       "; its ragged RCCL gather to rank 0 on the process group's collective stream (host issue "
+                       "order, the same on every rank), overlapping job i + 1's compute" if world > 1 else "")),
                    "one_job_in_flight": None if dt_iso is None else
                    {"value": round(frames / dt_iso, 1), "ms_per_step": round(dt_iso / args.steps * 1e3, 3),
                     "note": "the same K steps run one after the other right after the timed region"},

@@ -14,6 +14,7 @@ rank (``gather_to_root``, RCCL over xGMI under the ``nccl`` backend).
 from __future__ import annotations
 
 import contextlib
+import time
 
 import numpy as np
 import torch
@@ -331,6 +332,29 @@ def _side_streams(dev, cur, n):
     return lst[:n]
 
 
+def _set_marks(stats, m0, m1, m2):
+    stats["marks"] = (m0, m1, m2)
+    stats.pop("compute_ms", None)
+    stats.pop("gather_ms", None)
+    if not isinstance(m0, torch.cuda.Event):       # host clock readings: resolved already
+        phase_ms(stats)
+
+
+def phase_ms(stats):
+    """``compute_ms`` / ``gather_ms`` of a ``distributed_synthesize`` job from the marks it left in
+    ``stats`` (HIP events: the caller synchronises first -- this waits for the last mark anyway).
+    Returns (compute_ms, gather_ms) and stores them in ``stats``."""
+    if "compute_ms" not in stats:
+        m0, m1, m2 = stats["marks"]
+        if isinstance(m0, torch.cuda.Event):
+            m2.synchronize()
+            c, g = m0.elapsed_time(m1), m1.elapsed_time(m2)
+        else:
+            c, g = (m1 - m0) * 1e3, (m2 - m1) * 1e3
+        stats["compute_ms"], stats["gather_ms"] = float(c), float(g)
+    return stats["compute_ms"], stats["gather_ms"]
+
+
 def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None, stats=None,
                            collectives=False, max_waste=0.15, streams=4, max_frames=None):
     """Synthesize utterances sharded over the ranks of the default process group
@@ -354,8 +378,11 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     root, which un-permutes them.  The plan is deterministic and the mel channels known
     (``synth_fn.mel_bins``), so nothing but the outputs crosses ranks.  Returns on the root the
     lists [mel_i [T_i,M]], [wav_i [T_i*hop]] in input order; (None, None) elsewhere.
-    ``stats`` (a dict, optional) receives this rank's ``compute_ms`` (its shard's
-    synthesis, device-synchronized) and ``gather_ms`` (the collectives after it).
+    ``stats`` (a dict, optional) receives where this rank's job went -- its shard's synthesis and
+    the collectives after it -- as three marks (HIP events on the job's stream on a GPU, host clock
+    readings on a CPU) with no synchronisation inside the job; ``phase_ms(stats)`` turns them into
+    ``compute_ms`` / ``gather_ms`` once the caller has synchronised (r06: two
+    ``torch.cuda.synchronize()`` per job had serialised every N > 1 bench step).
     ``collectives=True`` runs the ragged gathers even at world size 1 (otherwise
     short-circuited), so the N > 1 code path can be exercised on one GPU.
     ``streams``: a shard of several ragged batches runs them side by side on up to this many HIP
@@ -365,7 +392,6 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     ``max_frames``: cap on a batch's padded frames (``ragged_batches``); a shard split into several
     batches runs them on the streams side by side, so one batch's low-occupancy launches (the
     WaveNet stack puts 44 frames on a CU) overlap another's."""
-    import time
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     lengths = [int(c.shape[0]) if torch.is_tensor(c) else int(c[0]) for c in conds]
@@ -375,14 +401,19 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
     collate = getattr(synth_fn, "collate", _default_collate)
     plans = [ragged_batches(lengths, s, max_waste, max_frames) for s in shards]
 
-    def sync():
-        if stats is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
-            torch.cuda.synchronize()
-
     dev = device
     if dev is None:
         dev = next((c.device for c in conds if torch.is_tensor(c)), torch.device("cpu"))
     dev = torch.device(dev)
+
+    def mark():
+        if stats is None:
+            return None
+        if dev.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream(dev))
+            return ev
+        return time.perf_counter()
     plan = plans[rank]
     side = None
     if streams > 1 and len(plan) > 1 and dev.type == "cuda":
@@ -393,7 +424,7 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         for s in side:
             s.wait_stream(cur)          # the inputs and the packed handles are ready
 
-    t0 = time.perf_counter()
+    m0 = mark()
     outs = []
     for k, (T, idx) in enumerate(plan):
         lens = [lengths[i] for i in idx]
@@ -419,10 +450,9 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
             for r, (i, n) in enumerate(zip(idx, lens)):
                 mels[i] = mel[r, :n]
                 wavs[i] = wav[r, :n * hop]
-        sync()
         if stats is not None:
-            stats["compute_ms"] = (time.perf_counter() - t0) * 1e3
-            stats["gather_ms"] = 0.0
+            m1 = mark()
+            _set_marks(stats, m0, m1, m1)
         return mels, wavs
     for mel, wav, lens, T in outs:
         M = mel.shape[-1]
@@ -438,8 +468,7 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         wav_flat = torch.zeros(0, device=dev)
     else:
         mel_flat, wav_flat = torch.cat(mel_parts), torch.cat(wav_parts)
-    sync()
-    t1 = time.perf_counter()
+    m1 = mark()
     if world == 1 and not (collectives and dist.is_initialized()):
         mels_all, wavs_all = [mel_flat], [wav_flat]
     else:
@@ -453,10 +482,10 @@ def distributed_synthesize(synth_fn, conds, root=0, seed=0, hop=HOP, device=None
         wav_shapes = [(sum(lengths[i] for i in s) * hop,) for s in shards]
         mels_all = gather_to_root(mel_flat, root, mel_shapes, force=collectives)
         wavs_all = gather_to_root(wav_flat, root, wav_shapes, force=collectives)
-    sync()
     if stats is not None:
-        stats["compute_ms"] = (t1 - t0) * 1e3
-        stats["gather_ms"] = (time.perf_counter() - t1) * 1e3
+        # (the gathers' completion: torch's process group makes the current stream wait for its
+        # collective stream, so an event recorded here ends after them)
+        _set_marks(stats, m0, m1, mark())
     if rank != root:
         return None, None
     mels, wavs = [None] * len(lengths), [None] * len(lengths)

@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 
 from prodiff_amd import synth
-from prodiff_amd.pipeline import Synthesizer, distributed_synthesize, gather_to_root
+from prodiff_amd.pipeline import JobStreams, Synthesizer, distributed_synthesize, gather_to_root, phase_ms
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -68,7 +68,36 @@ def test_distributed_synthesize_collectives_bf16(nccl_group):
     stats = {}
     mels, wavs = distributed_synthesize(syn, conds, seed=5, stats=stats, collectives=True)
     mref, wref = distributed_synthesize(syn, conds, seed=5)
-    assert stats["gather_ms"] >= 0
+    torch.cuda.synchronize()
+    c, g = phase_ms(stats)          # HIP event marks: no synchronisation inside the job (r06)
+    assert c > 0 and g >= 0 and stats["gather_ms"] == g
     for i, T in enumerate(lengths):
         assert tuple(mels[i].shape) == (T, 80) and tuple(wavs[i].shape) == (T * 256,)
         assert torch.equal(mels[i], mref[i]) and torch.equal(wavs[i], wref[i])
+
+
+def test_distributed_synthesize_jobs_in_flight_rccl(nccl_group):
+    """The N > 1 bench schedule at world size 1 with the collectives forced on: jobs on two
+    JobStreams streams, each job's gathers issued from its own stream (torch's collective stream
+    waits for it), so job i's gather overlaps job i + 1's compute.  Every job equals the same job
+    run alone, element for element."""
+    syn = Synthesizer.synthetic(DEV, seed=3, dtype="bf16", residual_layers=4)
+    lengths = [9, 7, 9, 5, 12]
+    conds = [torch.from_numpy(synth.synth_inputs(70 + i, (T, 256))).to(DEV) for i, T in enumerate(lengths)]
+    syn.prepare()
+    torch.cuda.synchronize()
+    js = JobStreams(2, DEV)
+    outs, sts = [], []
+    for j in range(4):
+        st = {}
+        with js.next():
+            outs.append(distributed_synthesize(syn, conds, seed=j, stats=st, collectives=True, max_frames=20))
+        sts.append(st)
+    torch.cuda.synchronize()
+    for j, (mels, wavs) in enumerate(outs):
+        mref, wref = distributed_synthesize(syn, conds, seed=j)
+        torch.cuda.synchronize()
+        for i in range(len(lengths)):
+            assert torch.equal(mels[i], mref[i]) and torch.equal(wavs[i], wref[i])
+        c, g = phase_ms(sts[j])
+        assert c > 0 and g >= 0

@@ -177,17 +177,38 @@ def test_bench_self_launches_n_ranks_dry_run():
     assert d["config"]["global_batch"] == 2 * d["config"]["per_gpu_batch"]
 
 
-def test_bench_refuses_jobs_in_flight_with_ranks():
-    """Jobs in flight are a one-GPU mode: with N > 1 ranks every job's gather is an RCCL collective,
-    so bench.py refuses --overlap > 1 there instead of putting collectives on several streams."""
+def test_bench_jobs_in_flight_with_ranks_dry_run():
+    """N > 1 ranks keep two jobs in flight by default (r06): each job's RCCL gather runs on the
+    process group's collective stream beside the next job's compute.  The dry run (gloo, CPU)
+    exercises the launcher, the schedule and the event-free phase marks; the line names the
+    schedule and reports each rank's compute / gather split."""
     env = dict(os.environ, PYTHONPATH=ROOT)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
-                          "--warmup", "1", "--dry-run", "--overlap", "2"], cwd=ROOT, env=env, capture_output=True,
-                         text=True, timeout=300)
-    assert out.returncode != 0
-    assert "--overlap > 1 is for one GPU" in (out.stderr + out.stdout)
+    for extra, depth in (([], 2), (["--overlap", "3"], 3), (["--overlap", "1"], 1)):
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                              "--warmup", "1", "--dry-run"] + extra, cwd=ROOT, env=env, capture_output=True,
+                             text=True, timeout=300)
+        assert out.returncode == 0, out.stderr[-3000:]
+        d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+        assert d["config"]["jobs_in_flight"] == depth
+        if depth > 1:
+            assert "RCCL gather" in d["config"]["schedule"] and "overlapping job i + 1" in d["config"]["schedule"]
+        else:
+            assert d["config"]["schedule"] is None
+        ph = d["phases"]
+        assert ph["compute_ms_per_step_slowest_rank"] >= ph["compute_ms_per_step_fastest_rank"] >= 0
+        assert ph["gather_ms_per_step_max"] >= 0
+
+
+def test_phase_marks_cpu():
+    """distributed_synthesize's ``stats`` on a CPU device: host clock marks, resolved at once."""
+    from prodiff_amd.pipeline import phase_ms
+    lengths = [5, 9, 3]
+    st = {}
+    distributed_synthesize(stub_synth, _conds(lengths), hop=HOP, stats=st)
+    c, g = phase_ms(st)
+    assert c >= 0 and g == 0.0 and st["compute_ms"] == c and len(st["marks"]) == 3
 
 
 class StubSvs:
