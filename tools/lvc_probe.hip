@@ -5,6 +5,12 @@
 #define LB_TRACE 1
 #include "../prodiff_amd/csrc/fastdiff.hip"
 
+// (kernels.hip's pd_build_config names every translation unit's flags; the probe links only this one)
+namespace pd {
+const char* nsf_build_flags() { return ""; }
+const char* wavenet_build_flags() { return ""; }
+}  // namespace pd
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
