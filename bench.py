@@ -228,6 +228,8 @@ TAG_KERNEL = {
     "wn_resskip2": ("wn_resskip_bf16_kernel",),
     "nsf_pair": ("nsf_pair_kernel<",),
     "nsf_pair16": ("nsf_pair16_kernel<",),
+    "nsf_rb16": ("nsf_rb16_kernel<",),
+    "nsf_rb32": ("nsf_rb_kernel<32,",),
     "nsf_res": ("nsf_wconv_kernel<",),
     "nsf_ups": ("nsf_ups_kernel<",),
 }
@@ -347,7 +349,9 @@ def nsf_stage_dims(h=None):
 
 
 NSF_PAIR_C = (32, 64, 128)     # ResBlock1 conv pairs fused into one nsf_pair launch (bf16, NSF_OPT_PAIR)
-NSF_PAIR16_C = (16,)           # ... and into one nsf_pair16 launch (bf16, NSF_OPT_PAIR16, r05)
+NSF_PAIR16_C = (16,)           # ... and into one nsf_pair16 launch (bf16, NSF_OPT_PAIR16, r05; rb16 = 0)
+NSF_RB16_C = (16,)             # r06: a whole 16-channel ResBlock1 (3 pairs) per nsf_rb16 launch (NSF_OPT_RB16)
+NSF_RB32_KS = (3,)             # r06: the 32-channel ResBlock1s of these kernel sizes per nsf_rb32 launch (NSF_OPT_RB32 1)
 NSF_KS = (3, 7, 11)            # resblock kernel sizes; 3 dilation pairs each (ResBlock1)
 NSF_HOP, NSF_MELS, NSF_C0, NSF_HARM = 512, 128, 512, 9
 
@@ -373,10 +377,31 @@ def svs_tables(B, T, Tt, dtype, small_max=16, H=256, k_ffn=9):
     fl, by = {}, {}
     # pair (k, d): c1 (k, dil d) and c2 (k, dil 1) over F r rows; x read once (fp32), the pair's
     # output written once (fp32), the last pair of resblocks 1, 2 also reads + writes the ResBlock sum
+    # r06: the C = 16 ResBlock1 whole (three pairs) per launch: x read once, the ResBlock sum written
+    # (first ResBlock) or read + written (the other two) once
+    rf, rb_ = [], []
+    for r, c in paired16:
+        if c not in NSF_RB16_C:
+            continue
+        for j, k in enumerate(NSF_KS):
+            rf.append(3 * 2 * 2 * F * r * c * c * k)
+            rb_.append(F * r * c * 4 * (2 if j == 0 else 3) + 6 * c * c * k * wb)
+    fl["nsf_rb16"], by["nsf_rb16"] = _mean(rf), _mean(rb_)
+    rf, rb_ = [], []
+    for r, c in paired:
+        if c != 32:
+            continue
+        for j, k in enumerate(NSF_KS):
+            if k in NSF_RB32_KS:
+                rf.append(3 * 2 * 2 * F * r * c * c * k)
+                rb_.append(F * r * c * 4 * (2 if j == 0 else 3) + 6 * c * c * k * wb)
+    fl["nsf_rb32"], by["nsf_rb32"] = _mean(rf), _mean(rb_)
     for tag, stages in (("nsf_pair", paired), ("nsf_pair16", paired16)):
         pf, pb = [], []
         for r, c in stages:
             for k in NSF_KS:
+                if tag == "nsf_pair" and c == 32 and k in NSF_RB32_KS:
+                    continue        # a whole-ResBlock nsf_rb32 launch (r06)
                 for q in range(3):
                     pf.append(2 * 2 * F * r * c * c * k)
                     acc = q == 2 and k != NSF_KS[0]

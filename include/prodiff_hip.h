@@ -338,6 +338,16 @@ size_t nsf_workspace_size(const nsf_model* m, int B, int T);
  * the source kernel has at most 8 taps (the last three stages) instead of reading nsf_noise_conv's output;
  * 0 = always the separate noise conv.  Same fp32 operations in the same order. */
 #define NSF_OPT_UPS_NC 4
+/* NSF_OPT_RB16 (r06): 1 (default) runs each 16-channel ResBlock1 of the shipped shapes (taps 3/7/11, c1
+ * dilations 1, 3, 5) as ONE launch that keeps the residual in registers across its three conv pairs and reads
+ * x / writes the ResBlock sum once (32-tile windows, 4 waves); 2 = 64-tile windows of 8 waves; 0 = one
+ * launch per pair (NSF_OPT_PAIR16).  Same roundings and MFMA order: bit-identical either way. */
+#define NSF_OPT_RB16 5
+/* NSF_OPT_RB32 / NSF_OPT_RB64 (r06): the same whole-ResBlock1 launch at 32 / 64 channels, for the kernel sizes
+ * whose bit is set (1: taps 3, 2: taps 7, 4: taps 11); 0 = one launch per pair.  Bit-identical either way.
+ * Defaults: RB32 1 (taps 3 only), RB64 0 (measured). */
+#define NSF_OPT_RB32 6
+#define NSF_OPT_RB64 7
 int nsf_set_option(nsf_model* m, int option, int value);
 
 /* spec2wav_torch(mel, f0=f0) for a batch of independent utterances:

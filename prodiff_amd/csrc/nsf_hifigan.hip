@@ -61,6 +61,12 @@ struct nsf_model {
   std::vector<NsfConv> res;      // [stage][kernel][conv] flattened in state-dict order
   bool ups_window = true;        // NSF_OPT_WCONV also selects the windowed ConvTranspose
   bool pair = true;              // NSF_OPT_PAIR: a ResBlock1 conv pair in one launch (nsf_pair_kernel)
+  int rb16 = 1;                  // NSF_OPT_RB16 (r06): a whole 16-channel ResBlock1 per launch (nsf_rb16_kernel)
+  // NSF_OPT_RB32 / RB64 (r06): the same at 32 / 64 channels, per kernel-size bit.  Measured (C5, one job,
+  // profiles/r06_ab/nsf_resblock_fused_ab.txt): only the 32-channel taps-3 ResBlock gains (343 vs 3 x 130 us);
+  // with taps 7 / 11 or 64 channels the 2 x 12 (k - 1) halo rows and one 8-wave block per CU cost more
+  // than the two fp32 round trips saved (545 vs 465, 764 vs 572, 557 vs 471, 624 vs 650, 941 vs 805 us)
+  int rb32 = 1, rb64 = 0;
   bool pair16 = true;            // NSF_OPT_PAIR16: the C = 16 pairs too (nsf_pair16_kernel), with pair
   bool ups_nc = true;            // NSF_OPT_UPS_NC: the windowed upsample computes short noise convs itself
   int convs_per_block = 0;
@@ -705,6 +711,19 @@ bool wconv_ok(const NsfConv& c);
 // The fused pair for these convs, if it has one: both windowed (bf16), 32, 64 or 128 channels, equal
 // taps and packing, c2 undilated.
 // C = 16 (nsf_pair16_kernel): the shipped shapes only -- taps 3 / 7 / 11, c1 dilation 1 / 3 / 5.
+// The whole 16-channel ResBlock1 in one launch (nsf_rb16_kernel): three bf16 windowed pairs of one
+// shipped kernel size with c1 dilations 1, 3, 5 and c2 undilated.
+bool rb_ok(const nsf_model* m, const NsfConv* c1, const NsfConv* c2, int C) {
+  const int k = c1[0].taps, bit = k == 3 ? 1 : k == 7 ? 2 : k == 11 ? 4 : 0;
+  if (C == 16 ? !m->rb16 : C == 32 ? !(m->rb32 & bit) : C == 64 ? !(m->rb64 & bit) : true) return false;
+  for (int q = 0; q < 3; ++q) {
+    const NsfConv &a = c1[q], &b = c2[q];
+    if (!wconv_ok(a) || !wconv_ok(b) || a.cout != C || b.cout != C || a.kpad != (C == 16 ? 32 : C) || b.kpad != a.kpad ||
+        a.taps != c1[0].taps || b.taps != a.taps || a.dil != (q == 0 ? 1 : q == 1 ? 3 : 5) || b.dil != 1)
+      return false;
+  }
+  return c1[0].taps == 3 || c1[0].taps == 7 || c1[0].taps == 11;
+}
 bool pair_ok(const nsf_model* m, const NsfConv& c1, const NsfConv& c2) {
   const bool c16 = c1.cout == 16 && c1.kpad == 32 && (c1.taps == 3 || c1.taps == 7 || c1.taps == 11) &&
                    (c1.dil == 1 || c1.dil == 3 || c1.dil == 5);
@@ -940,6 +959,397 @@ int launch_pair16(const NsfConv& c1, const NsfConv& c2, const float* x, int B, i
   else PD_PAIR16(11, 1); else PD_PAIR16(11, 3); else PD_PAIR16(11, 5);
   else { set_error("nsf pair16: not a shipped (taps, dilation) shape"); return PD_ERR_UNSUPPORTED; }
 #undef PD_PAIR16
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// ---------------------------------------------------------------- whole ResBlock1 at C = 16 (r06)
+// One launch per ResBlock1 of the 16-channel stage (models.py:57-63: the three (c1, c2) pairs with c1
+// dilations 1 / 3 / 5): x_{q+1} = x_q + c2(lrelu(c1(lrelu(x_q)))), the last pair adding into the ResBlock
+// sum xs (models.py:275-279).  That stage is the step's largest activation (16 fp32 channels at 512
+// samples per mel frame): the three pair launches read and wrote it three times per ResBlock (HBM-bound:
+// 131-167 us each at C5).  Here a block keeps its rows' residual x_q in registers across the three pairs
+// and reads x / writes (or adds into) xs once.
+// Window: NTW 16-row tiles, W = 16 NTW rows at times tw + i (tw = t0 - H); the ResBlock's reach on each
+// side is H = sum over the pairs of p1 + p2 = 12 (TAPS - 1) / 2 rows, so TM = W - 2 H rows are output.
+// x_q is exact on rows [V_q, W - V_q), V_{q+1} = V_q + p1 + p2; each conv runs on the 16-row tiles its
+// consumers read (rows outside the exact range only ever feed rows outside it).
+// Layout: transposed MFMA D[co][t] = W . act on v_mfma_f32_16x16x32_bf16 (A = the weights exactly as
+// nsf_pair16_kernel's B operand, B = the activation window as its A operand): lane (t = lane & 15,
+// g = lane >> 4) holds channels 4g .. 4g + 3 of one row, so a row's bf16 activation goes to LDS as one
+// 8-B write and the residual is 4 registers per tile.  Same products, same k order per MFMA, same
+// epilogue roundings and additions as the pair launches: bit-identical (tests/test_gpu_nsf.py).
+// One LDS window rewritten in place: a conv reads it, a barrier, the conv's output activation replaces
+// it, a barrier.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+struct NsfRb16Args {
+  const __bf16* w1[3];
+  const __bf16* w2[3];
+  const float* b1[3];
+  const float* b2[3];
+};
+template <int TAPS, int NTW, int NW>
+__global__ __launch_bounds__(NW * 64) void nsf_rb16_kernel(const float* __restrict__ x, const NsfRb16Args A, int Tl,
+                                                           float* __restrict__ out, int accum, NsfRag rag_) {
+  constexpr int C = 16, LDA = 24, NP = (TAPS + 1) / 2, KP = 32, P2 = (TAPS - 1) / 2;
+  constexpr int H = 12 * P2, W = 16 * NTW, TM = W - 2 * H, IPW = NTW / NW, PADR = 16;
+  static_assert(NTW % NW == 0 && TM > 0, "window tiles per wave");
+  // (a conv on tiles [kf, kl] clipped to its exact rows [e, W - e) reads rows [e - r - 15, W - e + r + 14) of an
+  // input exact on [e - r, W - e + r): never more than 15 rows outside the window, whatever its reach r)
+  __shared__ __attribute__((aligned(16))) __bf16 buf[(W + 2 * PADR) * LDA];
+  __bf16* bw = buf + PADR * LDA;               // window row i at bw + i LDA, i in [-16, W + 16)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4, kg = g & 1, tg = g >> 1;
+  const int b = blockIdx.y, t0 = blockIdx.x * TM, tw = t0 - H;
+  const int Tv = nsf_tv(rag_, b, Tl);
+  const long long rowb = (long long)b * Tl;
+  const bf16x8 z8 = {};
+  auto wload = [&](const __bf16* w, bf16x8 (&wf)[NP]) {   // nsf_pair16_kernel's fragments
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int tap = 2 * p + tg, tc = min(tap, TAPS - 1);
+      const unsigned mk = tap < TAPS ? 0xffffffffu : 0u;
+      const uint4 r = *reinterpret_cast<const uint4*>(w + (long long)r16 * (TAPS * KP) + tc * KP + 8 * kg);
+      wf[p] = __builtin_bit_cast(bf16x8, make_uint4(r.x & mk, r.y & mk, r.z & mk, r.w & mk));
+    }
+  };
+  // lrelu(v) rounded to bf16, zero outside the utterance (the conv's zero padding): one 8-B LDS write
+  auto put = [&](int m, const float* v) {
+    const int i = 16 * (wave + NW * m) + r16, t = tw + i;
+    const bool in = t >= 0 && t < Tv;
+    bf16x4 u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) u[e] = (__bf16)(in ? (v[e] >= 0.f ? v[e] : NSF_LRELU * v[e]) : 0.f);
+    *reinterpret_cast<bf16x4*>(bw + i * LDA + 4 * g) = u;
+  };
+  // registers: a conv's weight fragments are loaded once the previous conv's MFMAs are issued (one set
+  // live at a time), the ResBlock sum's rows only after the last conv's (r06: loaded up front, k = 11
+  // took 240 VGPRs, two blocks per CU)
+  bf16x8 wf[NP];
+  wload(A.w1[0], wf);
+  float xr[IPW][4];                            // residual x_q of rows 16 (wave + NW m) + r16, channels 4g ..
+#pragma unroll
+  for (int m = 0; m < IPW; ++m) {             // unconditional loads at clamped rows
+    const int t = min(max(tw + 16 * (wave + NW * m) + r16, 0), Tl - 1);
+    const float4 v = *reinterpret_cast<const float4*>(x + (rowb + t) * C + 4 * g);
+    xr[m][0] = v.x; xr[m][1] = v.y; xr[m][2] = v.z; xr[m][3] = v.w;
+  }
+#pragma unroll
+  for (int m = 0; m < IPW; ++m) put(m, xr[m]);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int d = q == 0 ? 1 : q == 1 ? 3 : 5, p1 = P2 * d;
+    const int V = q == 0 ? 0 : q == 1 ? 2 * P2 : 6 * P2;           // x_q exact on [V, W - V)
+    const int kf1 = (V + p1) / 16, kl1 = (W - V - p1 - 1) / 16;   // xt tiles c2 reads
+    const int kf2 = (V + p1 + P2) / 16, kl2 = (W - V - p1 - P2 - 1) / 16;
+    const float4 bn1 = *reinterpret_cast<const float4*>(A.b1[q] + 4 * g);
+    // ---- c1 (dilation d) on the xt tiles, then xt = bf16(c1 + b1) -> lrelu -> bf16 over x_q's rows
+    f32x4 acc[IPW];
+#pragma unroll
+    for (int m = 0; m < IPW; ++m) {
+      const int k = wave + NW * m;
+      acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (k >= kf1 && k <= kl1) {   // (wave-uniform)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const int tap = 2 * p + tg;
+          bf16x8 af = *reinterpret_cast<const bf16x8*>(bw + (16 * k + r16 + min(tap, TAPS - 1) * d - p1) * LDA + 8 * kg);
+          if (TAPS % 2 == 1 && p == NP - 1) af = tap < TAPS ? af : z8;
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[p], af, acc[m], 0, 0, 0);
+        }
+      }
+    }
+    wload(A.w2[q], wf);
+    const float4 bn2 = *reinterpret_cast<const float4*>(A.b2[q] + 4 * g);
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < IPW; ++m) {
+      const int k = wave + NW * m;
+      if (k >= kf1 && k <= kl1) {
+        const float v[4] = {(float)(__bf16)(acc[m][0] + bn1.x), (float)(__bf16)(acc[m][1] + bn1.y),
+                            (float)(__bf16)(acc[m][2] + bn1.z), (float)(__bf16)(acc[m][3] + bn1.w)};
+        put(m, v);
+      }
+    }
+    __syncthreads();
+    // ---- c2 (dilation 1) + b2 + x_q (+ xs after the last pair)
+#pragma unroll
+    for (int m = 0; m < IPW; ++m) {
+      const int k = wave + NW * m;
+      acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (k >= kf2 && k <= kl2) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const int tap = 2 * p + tg;
+          bf16x8 af = *reinterpret_cast<const bf16x8*>(bw + (16 * k + r16 + min(tap, TAPS - 1) - P2) * LDA + 8 * kg);
+          if (TAPS % 2 == 1 && p == NP - 1) af = tap < TAPS ? af : z8;
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[p], af, acc[m], 0, 0, 0);
+        }
+      }
+    }
+    if (q < 2) {
+      wload(A.w1[q + 1], wf);
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < IPW; ++m) {
+        const int k = wave + NW * m;
+        if (k >= kf2 && k <= kl2) {
+          xr[m][0] = acc[m][0] + bn2.x + xr[m][0];
+          xr[m][1] = acc[m][1] + bn2.y + xr[m][1];
+          xr[m][2] = acc[m][2] + bn2.z + xr[m][2];
+          xr[m][3] = acc[m][3] + bn2.w + xr[m][3];
+          put(m, xr[m]);
+        }
+      }
+      __syncthreads();
+    } else {
+      // output rows [H, W - H) = times [t0, t0 + TM), through a buffer resource spanning the
+      // utterance: rows past Tl (and the halo rows, given an offset past the range) are dropped
+      const __amdgpu_buffer_rsrc_t ors = nsf_utt_rsrc<false>(out, b * Tl, Tl, C);
+      float xs[IPW][4];                        // the ResBlock sum's rows so far (accum)
+#pragma unroll
+      for (int m = 0; m < IPW; ++m) {
+        const int t = min(max(tw + 16 * (wave + NW * m) + r16, 0), Tl - 1);
+        const float4 v = *reinterpret_cast<const float4*>(out + (rowb + t) * C + 4 * g);
+        xs[m][0] = v.x; xs[m][1] = v.y; xs[m][2] = v.z; xs[m][3] = v.w;
+      }
+#pragma unroll
+      for (int m = 0; m < IPW; ++m) {
+        const int k = wave + NW * m;
+        if (k >= kf2 && k <= kl2) {
+          const int i = 16 * k + r16, t = tw + i;
+          const bool ok = i >= H && i < W - H;
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float rv = accum ? xr[m][e] + xs[m][e] : xr[m][e];
+            o[e] = acc[m][e] + (e == 0 ? bn2.x : e == 1 ? bn2.y : e == 2 ? bn2.z : bn2.w) + rv;
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4, make_float4(o[0], o[1], o[2], o[3])), ors,
+              ok ? (unsigned)(t * C + 4 * g) * 4u : 0xfffffff0u, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+// Whole ResBlock1 at C = 32 / 64 (r06): nsf_rb16_kernel's structure on 32x32x16 MFMAs (nsf_pair_kernel's
+// fragments, transposed: A = its weight fragments, B = its window reads).  Item = (32-row tile k, 32-channel
+// column tile ct); a wave keeps one ct and tiles k = kw + (NW / NCT) m, so lane (t = lane & 31, h = lane >> 5)
+// holds channels 32 ct + 8 g + 4 h + e (g, e < 4) of one row: 16 residual registers per item, and a row's
+// activation goes to LDS as four 8-B writes.  Weights stream from L2 through an NSF_PAIR_PF-deep register
+// ring, each fragment serving the wave's IPW items.  Bit-identical to the pair launches (same products
+// and k order per MFMA, same epilogue roundings).
+template <int C, int TAPS, int NTW, int NW>
+__global__ __launch_bounds__(NW * 64) void nsf_rb_kernel(const float* __restrict__ x, const NsfRb16Args A, int Tl,
+                                                         float* __restrict__ out, int accum, NsfRag rag_) {
+  constexpr int NCT = C / 32, LDA = C + 8, KS = C / 16, P2 = (TAPS - 1) / 2, S = TAPS * KS;
+  constexpr int H = 12 * P2, W = 32 * NTW, TM = W - 2 * H, PADR = 32, KST = NW / NCT, IPW = NTW / KST;
+  static_assert(NW % NCT == 0 && NTW % KST == 0 && TM > 0, "item tiling");
+  constexpr int PF = KS >= NSF_PAIR_PF ? NSF_PAIR_PF : KS;
+  static_assert(KS % PF == 0, "ring depth divides the k-steps per tap");
+  extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win[];
+  __bf16* bw = nsf_win + PADR * LDA;           // window row i at bw + i LDA, i in [-32, W + 32)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int ct = wave % NCT, kw = wave / NCT;
+  const int b = blockIdx.y, t0 = blockIdx.x * TM, tw = t0 - H;
+  const int Tv = nsf_tv(rag_, b, Tl);
+  const long long rowb = (long long)b * Tl;
+  const int n = ct * 32 + r32;                 // the lane's weight row (output channel)
+  auto put = [&](int m, const float* v) {      // lrelu -> bf16, zero outside the utterance
+    const int i = 32 * (kw + KST * m) + r32, t = tw + i;
+    const bool in = t >= 0 && t < Tv;
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      bf16x4 u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = v[4 * gq + e];
+        u[e] = (__bf16)(in ? (a >= 0.f ? a : NSF_LRELU * a) : 0.f);
+      }
+      *reinterpret_cast<bf16x4*>(bw + i * LDA + 32 * ct + 8 * gq + 4 * h) = u;
+    }
+  };
+  // one conv over the items of tiles [kf, kl]: acc[m] = sum over k-steps of W . window rows shifted
+  auto conv = [&](const __bf16* w, int dil, int pad, int kf, int kl, f32x16 (&acc)[IPW]) {
+    const __bf16* wr = w + (long long)n * (TAPS * C) + 8 * h;
+#pragma unroll
+    for (int m = 0; m < IPW; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+    bf16x8 bq[PF];
+    auto bload = [&](int st) {
+      const int tn = st / KS, kn = st - tn * KS;
+      return *reinterpret_cast<const bf16x8*>(wr + tn * C + 16 * kn);
+    };
+#pragma unroll
+    for (int q = 0; q < PF - 1; ++q) bq[q] = bload(q);
+#pragma unroll
+    for (int s0 = 0; s0 < S; s0 += PF) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int st = s0 + q;
+        bq[(q + PF - 1) % PF] = bload(min(st + PF - 1, S - 1));
+        const int tap = st / KS, kc = st - tap * KS;
+#pragma unroll
+        for (int m = 0; m < IPW; ++m) {
+          const int k = kw + KST * m;
+          if (k >= kf && k <= kl) {   // (wave-uniform)
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(bw + (32 * k + r32 + tap * dil - pad) * LDA + 16 * kc + 8 * h);
+            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bq[q], af, acc[m], 0, 0, 0);
+          }
+        }
+      }
+    }
+  };
+  float xr[IPW][16];                           // residual x_q
+#pragma unroll
+  for (int m = 0; m < IPW; ++m) {
+    const int t = min(max(tw + 32 * (kw + KST * m) + r32, 0), Tl - 1);
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const float4 v = *reinterpret_cast<const float4*>(x + (rowb + t) * C + 32 * ct + 8 * gq + 4 * h);
+      xr[m][4 * gq] = v.x; xr[m][4 * gq + 1] = v.y; xr[m][4 * gq + 2] = v.z; xr[m][4 * gq + 3] = v.w;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < IPW; ++m) put(m, xr[m]);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int d = q == 0 ? 1 : q == 1 ? 3 : 5, p1 = P2 * d;
+    const int V = q == 0 ? 0 : q == 1 ? 2 * P2 : 6 * P2;
+    const int kf1 = (V + p1) / 32, kl1 = (W - V - p1 - 1) / 32;
+    const int kf2 = (V + p1 + P2) / 32, kl2 = (W - V - p1 - P2 - 1) / 32;
+    f32x16 acc[IPW];
+    conv(A.w1[q], d, p1, kf1, kl1, acc);
+    __syncthreads();
+    {
+      float bn[16];
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const float4 v = *reinterpret_cast<const float4*>(A.b1[q] + 32 * ct + 8 * gq + 4 * h);
+        bn[4 * gq] = v.x; bn[4 * gq + 1] = v.y; bn[4 * gq + 2] = v.z; bn[4 * gq + 3] = v.w;
+      }
+#pragma unroll
+      for (int m = 0; m < IPW; ++m) {
+        const int k = kw + KST * m;
+        if (k >= kf1 && k <= kl1) {
+          float v[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = (float)(__bf16)(acc[m][r] + bn[r]);
+          put(m, v);
+        }
+      }
+    }
+    __syncthreads();
+    conv(A.w2[q], 1, P2, kf2, kl2, acc);
+    float bn[16];
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const float4 v = *reinterpret_cast<const float4*>(A.b2[q] + 32 * ct + 8 * gq + 4 * h);
+      bn[4 * gq] = v.x; bn[4 * gq + 1] = v.y; bn[4 * gq + 2] = v.z; bn[4 * gq + 3] = v.w;
+    }
+    if (q < 2) {
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < IPW; ++m) {
+        const int k = kw + KST * m;
+        if (k >= kf2 && k <= kl2) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xr[m][r] = acc[m][r] + bn[r] + xr[m][r];
+          put(m, xr[m]);
+        }
+      }
+      __syncthreads();
+    } else {
+      const __amdgpu_buffer_rsrc_t ors = nsf_utt_rsrc<false>(out, b * Tl, Tl, C);
+#pragma unroll
+      for (int m = 0; m < IPW; ++m) {
+        const int k = kw + KST * m;
+        if (k >= kf2 && k <= kl2) {
+          const int i = 32 * k + r32, t = tw + i, tc = min(max(t, 0), Tl - 1);
+          const bool ok = i >= H && i < W - H;
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const int col = 32 * ct + 8 * gq + 4 * h;
+            const float4 a = *reinterpret_cast<const float4*>(out + (rowb + tc) * C + col);   // the sum so far
+            const float av[4] = {a.x, a.y, a.z, a.w};
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float rv = accum ? xr[m][4 * gq + e] + av[e] : xr[m][4 * gq + e];
+              o[e] = acc[m][4 * gq + e] + bn[4 * gq + e] + rv;
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(o[0], o[1], o[2], o[3])), ors,
+                                                   ok ? (unsigned)(t * C + col) * 4u : 0xfffffff0u, 0, 0);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int C, int TAPS, int NTW, int NW>
+int launch_rb_ct(const NsfRb16Args& a, const float* x, int B, int Tl, float* out, int accum, hipStream_t st,
+                 NsfRag rag_) {
+  constexpr int LDS = (32 * NTW + 64) * (C + 8) * 2;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&nsf_rb_kernel<C, TAPS, NTW, NW>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+  if (attr != hipSuccess) { set_error("nsf rb: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }
+  hipLaunchKernelGGL((nsf_rb_kernel<C, TAPS, NTW, NW>), dim3(cdiv(Tl, 32 * NTW - 12 * (TAPS - 1)), B), dim3(64 * NW),
+                     LDS, st, x, a, Tl, out, accum, rag_);
+  PD_LAUNCH_CHECK();
+  return PD_OK;
+}
+
+// NSF_OPT_RB32 / RB64: the 32- / 64-channel ResBlock1s as one launch each, for the kernel sizes whose bit
+// (1: taps 3, 2: taps 7, 4: taps 11) is set
+int launch_rb(const NsfConv* c1, const NsfConv* c2, const float* x, int B, int Tl, float* out, int accum,
+              hipStream_t st, NsfRag rag_) {
+  NsfRb16Args a{};
+  for (int q = 0; q < 3; ++q) {
+    a.w1[q] = lookup_bf16(c1[q].w); a.w2[q] = lookup_bf16(c2[q].w);
+    a.b1[q] = c1[q].b; a.b2[q] = c2[q].b;
+  }
+  ProfScope ps(c1[0].cout == 32 ? "nsf_rb32" : "nsf_rb64", st);
+  const int k = c1[0].taps;
+  if (c1[0].cout == 32) {
+    if (k == 3) return launch_rb_ct<32, 3, 16, 8>(a, x, B, Tl, out, accum, st, rag_);
+    if (k == 7) return launch_rb_ct<32, 7, 16, 8>(a, x, B, Tl, out, accum, st, rag_);
+    return launch_rb_ct<32, 11, 16, 8>(a, x, B, Tl, out, accum, st, rag_);
+  }
+  if (k == 3) return launch_rb_ct<64, 3, 8, 8>(a, x, B, Tl, out, accum, st, rag_);
+  if (k == 7) return launch_rb_ct<64, 7, 16, 8>(a, x, B, Tl, out, accum, st, rag_);
+  return launch_rb_ct<64, 11, 16, 8>(a, x, B, Tl, out, accum, st, rag_);
+}
+
+// NSF_OPT_RB16: the 16-channel ResBlock1s of the shipped shapes as one launch each (nsf_rb16_kernel)
+int launch_rb16(const NsfConv* c1, const NsfConv* c2, const float* x, int B, int Tl, float* out, int accum,
+                hipStream_t st, NsfRag rag_, int geo) {
+  NsfRb16Args a{};
+  for (int q = 0; q < 3; ++q) {
+    a.w1[q] = lookup_bf16(c1[q].w); a.w2[q] = lookup_bf16(c2[q].w);
+    a.b1[q] = c1[q].b; a.b2[q] = c2[q].b;
+  }
+  ProfScope ps("nsf_rb16", st);
+  // geometry (NSF_OPT_RB16): 1 = 32-tile windows of 4 waves (3 blocks per CU), 2 = 64-tile windows of 8
+  // waves (half the halo share, one block per CU)
+#define PD_RB16(K, NTW, NW)                                                                                 \
+  hipLaunchKernelGGL((nsf_rb16_kernel<K, NTW, NW>), dim3(cdiv(Tl, 16 * NTW - 12 * (K - 1)), B), dim3(64 * NW), 0, \
+                     st, x, a, Tl, out, accum, rag_)
+  if (geo == 2) {
+    if (c1[0].taps == 3) PD_RB16(3, 64, 8);
+    else if (c1[0].taps == 7) PD_RB16(7, 64, 8);
+    else PD_RB16(11, 64, 8);
+  } else {
+    if (c1[0].taps == 3) PD_RB16(3, 32, 4);
+    else if (c1[0].taps == 7) PD_RB16(7, 32, 4);
+    else PD_RB16(11, 32, 4);
+  }
+#undef PD_RB16
   PD_LAUNCH_CHECK();
   return PD_OK;
 }
@@ -1588,6 +1998,16 @@ int nsf_set_option(nsf_model* m, int option, int value) {
     m->ups_nc = value != 0;
     return PD_OK;
   }
+  if (option == NSF_OPT_RB32 || option == NSF_OPT_RB64) {
+    PD_CHECK_ARG(value >= 0 && value <= 7, "NSF_OPT_RB32 / RB64: a kernel-size bit mask (1: 3, 2: 7, 4: 11)");
+    (option == NSF_OPT_RB32 ? m->rb32 : m->rb64) = value;
+    return PD_OK;
+  }
+  if (option == NSF_OPT_RB16) {
+    PD_CHECK_ARG(value >= 0 && value <= 2, "NSF_OPT_RB16 is 0, 1 or 2");
+    m->rb16 = value;
+    return PD_OK;
+  }
   if (option == NSF_OPT_PAIR16) {
     PD_CHECK_ARG(value == 0 || value == 1, "NSF_OPT_PAIR16 is 0 or 1");
     m->pair16 = value != 0;
@@ -1699,6 +2119,19 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
       const float* cur = X;
       bool summed = false;   // resblock_j(x) already added into XS by its last conv
       const int D = d.num_dilations;
+      if (d.resblock == 1 && D == 3) {
+        NsfConv c1s[3], c2s[3];
+        for (int q = 0; q < 3; ++q) { c1s[q] = m->res[r + q]; c2s[q] = m->res[r + D + q]; }
+        const int Cr = c1s[0].cout;
+        if ((Cr == 16 || Cr == 32 || Cr == 64) && rb_ok(m, c1s, c2s, Cr)) {
+          // r06: the whole ResBlock in one launch, x read once, xs written / added once
+          if ((long long)B * Lc * Cr >= (1ll << 31)) { set_error("nsf rb: B * T * C >= 2^31"); return PD_ERR_UNSUPPORTED; }
+          if (Cr == 16) PD_TRY(launch_rb16(c1s, c2s, X, B, Lc, XS, j > 0 ? 1 : 0, st, rag_, m->rb16));
+          else PD_TRY(launch_rb(c1s, c2s, X, B, Lc, XS, j > 0 ? 1 : 0, st, rag_));
+          r += m->convs_per_block;
+          continue;
+        }
+      }
       for (int q = 0; q < D; ++q) {
         if (d.resblock == 1) {
           const NsfConv& c1 = m->res[r + q];

@@ -239,19 +239,22 @@ def test_bench_tables_cover_every_dominant_tag():
     fl.update(sf)
     by.update(sb)
     for tag in ("wn_stack", "wn_gate", "wn_resskip", "fd_lvc_block_final", "fd_kp_kernel", "fd_kp_hidden",
-                "fd_lvc_block_ups", "fd_lvc_block_sub", "fd_dblock_fused", "nsf_pair", "nsf_pair16", "nsf_res",
+                "fd_lvc_block_ups", "fd_lvc_block_sub", "fd_dblock_fused", "nsf_pair", "nsf_pair16", "nsf_rb16", "nsf_res",
                 "nsf_ups", "nsf_noise_conv", "nsf_source", "nsf_post"):
         assert tag in fl and tag in by and by[tag] > 0, tag
     # the stack's mean launch: 10 layers of 26.2 MFLOP per frame plus half the in/out projections
     per_frame = fl["wn_stack"] / (8 * 861)
     assert 10 * 2 * 2 * 256 * 1280 < per_frame < 10 * 2 * 2 * 256 * 1280 * 1.02
-    # 27 pair launches per C5 forward carry all ResBlock FLOPs of the C = 128 / 64 / 32 stages
+    # 24 pair launches + 1 nsf_rb32 launch (r06: the 32-channel taps-3 ResBlock whole) per C5 forward carry
+    # all ResBlock FLOPs of the C = 128 / 64 / 32 stages
     F = 8 * 861
     pair_total = sum(2 * 2 * 3 * 21 * F * r * c * c for r, c in bench.nsf_stage_dims() if c in bench.NSF_PAIR_C)
-    assert abs(fl["nsf_pair"] * 27 - pair_total) < 1e-6 * pair_total
+    assert abs(fl["nsf_pair"] * 24 + fl["nsf_rb32"] - pair_total) < 1e-6 * pair_total
     # ... and 9 nsf_pair16 launches the C = 16 stage's (r05); no single 16-channel convs remain in bf16
     p16 = sum(2 * 2 * 3 * 21 * F * r * c * c for r, c in bench.nsf_stage_dims() if c in bench.NSF_PAIR16_C)
     assert abs(fl["nsf_pair16"] * 9 - p16) < 1e-6 * p16 and by["nsf_res_small"] == 0
+    # ... or 3 nsf_rb16 launches (r06: one per whole ResBlock1, the default), the same FLOPs
+    assert abs(fl["nsf_rb16"] * 3 - p16) < 1e-6 * p16 and by["nsf_rb16"] > 0
     with pytest.raises(SystemExit):
         bench.dominant_kernel({"mystery": (1, 5.0), "wn_stack": (2, 1.0)}, fl, by)
     assert bench.dominant_kernel({"nsf_pair": (27, 5.0), "wn_stack": (2, 1.0)}, fl, by) == "nsf_pair"

@@ -144,3 +144,68 @@ def test_bf16_ups_noise_conv_fused_bitexact(T, B, lens):
     else:
         for r, n in enumerate(lens):
             np.testing.assert_array_equal(outs[1][r, :n * g.upp], outs[0][r, :n * g.upp])
+
+
+@pytest.mark.parametrize("T,B,lens", [(24, 1, None), (37, 2, [37, 21]), (1, 3, None), (300, 2, [300, 251])])
+def test_bf16_resblock16_fused_bitexact(T, B, lens):
+    """NSF_OPT_RB16 (r06: each 16-channel ResBlock1 -- three conv pairs, dilations 1 / 3 / 5 -- as one
+    launch with the residual in registers; geometry 1 = 32-tile windows, 2 = 64-tile windows) against
+    one nsf_pair16 launch per pair: the transposed MFMA sums the same products in the same k order and
+    the epilogues round and add as the pair launches do, so the waveform is bit-identical -- partial
+    windows, T = 1 (all halo), utterances side by side, ragged rows (zero past each one's end) and
+    T = 300 (several windows per utterance at the 512-sample stage)."""
+    h = dict(synth.NSF_DEFAULTS)
+    g, _ = _gen(h, 7)
+    rng = np.random.default_rng(8)
+    mel = torch.from_numpy(rng.normal(-2.0, 1.0, size=(B, T, 128)).astype(np.float32)).to(DEV)
+    f0 = torch.from_numpy(rng.uniform(60.0, 900.0, size=(B, T)).astype(np.float32)).to(DEV)
+    outs = []
+    from prodiff_amd import _lib
+    for rb in (0, 1, 2):
+        g.set_compute_dtype("bf16").set_options(rb16=rb)
+        _lib.profile_enable(True)
+        outs.append(g.synthesize(mel, f0, 2.30259, seed=9, lens=lens).cpu().numpy())
+        torch.cuda.synchronize()
+        tags = set(_lib.profile_summary())
+        _lib.profile_enable(False)
+        assert ("nsf_rb16" in tags) == (rb > 0) and ("nsf_pair16" in tags) == (rb == 0), (rb, tags)
+    g.set_options(rb16=1)
+    assert np.isfinite(outs[1]).all()
+    for rb in (1, 2):
+        if lens is None:
+            np.testing.assert_array_equal(outs[rb], outs[0])
+        else:
+            for r, n in enumerate(lens):
+                np.testing.assert_array_equal(outs[rb][r, :n * g.upp], outs[0][r, :n * g.upp])
+
+
+@pytest.mark.parametrize("opt", ["rb32", "rb64"])
+@pytest.mark.parametrize("T,B,lens", [(24, 1, None), (37, 2, [37, 21]), (1, 3, None), (150, 2, [150, 97])])
+def test_bf16_resblock_fused_bitexact(opt, T, B, lens):
+    """NSF_OPT_RB32 / RB64 (r06: the 32- / 64-channel ResBlock1s as one launch each, every kernel
+    size enabled) against one nsf_pair launch per pair: bit-identical, as the C = 16 variant."""
+    h = dict(synth.NSF_DEFAULTS)
+    g, _ = _gen(h, 7)
+    rng = np.random.default_rng(11)
+    mel = torch.from_numpy(rng.normal(-2.0, 1.0, size=(B, T, 128)).astype(np.float32)).to(DEV)
+    f0 = torch.from_numpy(rng.uniform(60.0, 900.0, size=(B, T)).astype(np.float32)).to(DEV)
+    from prodiff_amd import _lib
+    outs = []
+    tag = "nsf_rb32" if opt == "rb32" else "nsf_rb64"
+    for v in (0, 7):
+        g.set_compute_dtype("bf16").set_options(**{opt: v})
+        _lib.profile_enable(True)
+        outs.append(g.synthesize(mel, f0, 2.30259, seed=9, lens=lens).cpu().numpy())
+        torch.cuda.synchronize()
+        tags = _lib.profile_summary()
+        _lib.profile_enable(False)
+        assert (tag in tags) == (v > 0), (v, tags)
+        if v:
+            assert tags[tag][0] == 3, tags[tag]   # one launch per ResBlock of that stage
+    g.set_options(**{opt: 0})
+    assert np.isfinite(outs[1]).all()
+    if lens is None:
+        np.testing.assert_array_equal(outs[1], outs[0])
+    else:
+        for r, n in enumerate(lens):
+            np.testing.assert_array_equal(outs[1][r, :n * g.upp], outs[0][r, :n * g.upp])
