@@ -348,6 +348,12 @@ size_t nsf_workspace_size(const nsf_model* m, int B, int T);
  * Defaults: RB32 1 (taps 3 only), RB64 0 (measured). */
 #define NSF_OPT_RB32 6
 #define NSF_OPT_RB64 7
+/* NSF_OPT_C256 (r06): the 256-channel ResBlock convs' block shape -- 0: 4 waves and 128 output channels per
+ * block (two blocks stage each row tile's window), 1 (default): 8 waves and all 256.  Bit-identical. */
+#define NSF_OPT_C256 8
+/* NSF_OPT_NC_MFMA (r06): 2 (default) runs the first two stages' source convs (K = 128 / 16, stride K / 2) on the
+ * f32 MFMA (fmaf chains from the bias, k ascending: bit-identical), 1 only the K = 128 one, 0 = the fp32 VALU kernel. */
+#define NSF_OPT_NC_MFMA 9
 int nsf_set_option(nsf_model* m, int option, int value);
 
 /* spec2wav_torch(mel, f0=f0) for a batch of independent utterances:

@@ -32,6 +32,7 @@ struct NsfConv {
   const float* w = nullptr;   // packed [cout][taps * kpad]
   const float* b = nullptr;
   int taps = 0, dil = 1, cin = 0, cout = 0, kpad = 0;
+  int w256 = 1;               // NSF_OPT_C256 (r06): the 256-channel windowed conv's block shape
   // ResBlock convs with at most this many channels use nsf_conv_small_kernel (NSF_OPT_SMALL_MAX;
   // measured: 32 channels run faster on the bf16 GEMM)
   int small_max = 16;
@@ -67,6 +68,7 @@ struct nsf_model {
   // with taps 7 / 11 or 64 channels the 2 x 12 (k - 1) halo rows and one 8-wave block per CU cost more
   // than the two fp32 round trips saved (545 vs 465, 764 vs 572, 557 vs 471, 624 vs 650, 941 vs 805 us)
   int rb32 = 1, rb64 = 0;
+  int nc_mfma = 2;               // NSF_OPT_NC_MFMA (r06): the K = 128 and K = 16 source convs on the f32 MFMA
   bool pair16 = true;            // NSF_OPT_PAIR16: the C = 16 pairs too (nsf_pair16_kernel), with pair
   bool ups_nc = true;            // NSF_OPT_UPS_NC: the windowed upsample computes short noise convs itself
   int convs_per_block = 0;
@@ -213,6 +215,67 @@ __global__ __launch_bounds__(256) void nsf_noise_conv_kernel(const float* __rest
 }
 
 // noise conv weight [C][1][K] -> tap-major [K][C]
+// The two long source convs (the first two stages: Conv1d(1, C, K = 2 s, stride s), s = 64 / 8; models.py:255-262)
+// on the f32 MFMA (r06): out^T[o][r] = b[o] + sum_k w[k][o] har[r s - pad + k] as v_mfma_f32_32x32x2_f32
+// chains started from the bias, k ascending -- the VALU kernel's fmaf chain (MI355X_MICROARCH.md: the f32-input
+// MFMA is exact f32, bitwise an fmaf chain).  Block = 4 waves x 32 rows, 32 channels: the block's source
+// window and its channels' weights in LDS; lane (row, k half) holds 4 consecutive channels per register
+// group, so results leave as float4 stores.  The VALU kernel ran 100-106 us per launch at C5 (3.6 and 1.8
+// GFLOP): fp32 VALU-bound.
+template <int K>
+__global__ __launch_bounds__(256) void nsf_noise_mfma_kernel(const float* __restrict__ har, long long L,
+                                                             const float* __restrict__ wt,
+                                                             const float* __restrict__ bias, int C, int pad,
+                                                             long long Tout, float* __restrict__ out, NsfRag rag_) {
+  constexpr int S = K / 2, RB = 128, WIN = (RB - 1) * S + K;
+  __shared__ float s_har[WIN];
+  __shared__ float s_w[K * 32];                 // [k][channel within the block's 32]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 31, kh = lane >> 5;
+  const int b = blockIdx.z, o0 = blockIdx.y * 32;
+  const long long row0 = (long long)blockIdx.x * RB;
+  const float* hb = har + (long long)b * L;
+  const long long s0 = row0 * S - pad;
+  const long long Lv = rag_.lens ? min((long long)rag_.lens[b] * rag_.rate, L) : L;   // the utterance's own end
+  // staging: every load of the window and the weights issued before any LDS store (a load-store loop
+  // waited one round trip per item: 33 of them per thread at K = 128)
+  constexpr int NH = (WIN + 255) / 256, NWV = K * 32 / 256;
+  float hv[NH], wv[NWV];
+#pragma unroll
+  for (int u = 0; u < NH; ++u) {
+    const long long sidx = s0 + tid + 256 * u;
+    const long long sc = sidx < 0 ? 0 : sidx >= L ? L - 1 : sidx;      // unconditional load, masked value
+    hv[u] = hb[sc];
+  }
+#pragma unroll
+  for (int u = 0; u < NWV; ++u) {
+    const int i = tid + 256 * u;
+    wv[u] = wt[(long long)(i >> 5) * C + o0 + (i & 31)];
+  }
+#pragma unroll
+  for (int u = 0; u < NH; ++u) {
+    const int i = tid + 256 * u;
+    const long long sidx = s0 + i;
+    if (i < WIN) s_har[i] = (sidx >= 0 && sidx < Lv) ? hv[u] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < NWV; ++u) s_w[tid + 256 * u] = wv[u];
+  f32x16 acc;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) acc[reg] = bias[o0 + (reg & 3) + 8 * (reg >> 2) + 4 * kh];
+  __syncthreads();
+  const float* hr = s_har + (wave * 32 + j) * S + kh;
+#pragma unroll 8
+  for (int k0 = 0; k0 < K; k0 += 2)
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_w[(k0 + kh) * 32 + j], hr[k0], acc, 0, 0, 0);
+  const long long r = row0 + wave * 32 + j;
+  if (r < Tout) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(out + ((long long)b * Tout + r) * C + o0 + 8 * g + 4 * kh) =
+          make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+  }
+}
+
 __global__ void nsf_pack_noise_kernel(float* __restrict__ dst, const float* __restrict__ src, int C, int K) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= C * K) return;
@@ -348,16 +411,16 @@ __device__ __forceinline__ void nsf_store_utt(__amdgpu_buffer_rsrc_t r, int elem
 // store unconditional -- items past the window go to row W, one spare row the callers allocate
 // (or that the next stage overwrites): with `if (ok)` loads / `if (i < nitems)` stores hipcc sank
 // the loads into the branches and waited for each one, a round trip per item instead of per batch.
-template <int C, bool IN_BF>
+template <int C, bool IN_BF, int NT = 256>
 __device__ __forceinline__ void stage_window(const void* __restrict__ in, int b, int Tl, int Tv, int r0, int W,
                                              float alpha, float scale, __bf16* __restrict__ win, int lda, int tid) {
   constexpr int C8 = C / 8;
   const int nitems = W * C8;
-  for (int base = tid; base < nitems; base += 256 * NSF_WB) {
+  for (int base = tid; base < nitems; base += NT * NSF_WB) {
     float f[NSF_WB][8];
 #pragma unroll
     for (int u = 0; u < NSF_WB; ++u) {
-      const int i = base + 256 * u;
+      const int i = base + NT * u;
       const int row = i / C8, c8 = i - row * C8;
       const int t = r0 + row;
       const bool ok = i < nitems && t >= 0 && t < Tv;
@@ -376,7 +439,7 @@ __device__ __forceinline__ void stage_window(const void* __restrict__ in, int b,
     }
 #pragma unroll
     for (int u = 0; u < NSF_WB; ++u) {
-      const int i = base + 256 * u;
+      const int i = base + NT * u;
       const bool in_w = i < nitems;
       const int row = in_w ? i / C8 : W, c8 = in_w ? i - (i / C8) * C8 : 0;
       bf16x8 v;
@@ -401,13 +464,16 @@ constexpr int NSF_PF = NSF_PF_DEPTH;
 #define NSF_PAIR_PF NSF_PF_DEPTH   // the pair kernel's weight ring depth (k-steps)
 #endif
 
+// WM x WN = 4 waves, or 8 (r06, C = 256: one block covers all 256 output channels, so the window is
+// staged once per row tile instead of once per 128-channel half, two waves per SIMD)
 template <int C, int FM, int FN, int WM, int WN, bool IN_BF, bool OUT_BF>
-__global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
+__global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 3 : 1) void nsf_wconv_kernel(const void* __restrict__ in, const __bf16* __restrict__ w,
                                                         int ldw, int kpad, const float* __restrict__ bias, int taps,
                                                         int dil, float alpha, float scale, int Tl,
                                                         const float* __restrict__ res, void* __restrict__ out,
                                                         int accum, NsfRag rag_) {
-  static_assert(WM * WN == 4, "4 waves");
+  static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 waves");
+  constexpr int NT = 64 * WM * WN;
   constexpr int TM = 32 * FM * WM, TN = 32 * FN * WN, LDA = C + 8, KS = C / 16;
   static_assert(C % TN == 0, "channel tiling");
   extern __shared__ __attribute__((aligned(16))) __bf16 nsf_win[];
@@ -418,7 +484,7 @@ __global__ __launch_bounds__(256, 3) void nsf_wconv_kernel(const void* __restric
   const int W = TM + (taps - 1) * dil;
   // 1. the input window, 8 channels (16 B of bf16) per item, NSF_WB items per thread in flight
   //    together (a load-convert-store loop waits one HBM round trip per item)
-  stage_window<C, IN_BF>(in, b, Tl, nsf_tv(rag_, b, Tl), t0 - pad, W, alpha, scale, nsf_win, LDA, tid);
+  stage_window<C, IN_BF, NT>(in, b, Tl, nsf_tv(rag_, b, Tl), t0 - pad, W, alpha, scale, nsf_win, LDA, tid);
   __syncthreads();
   // 2. taps x 16-deep k-steps; B fragments prefetched one step ahead
   const int r32 = lane & 31, h = lane >> 5;
@@ -1656,7 +1722,7 @@ int launch_wconv_c(const NsfConv& c, const __bf16* wb, const void* in, bool in_b
         reinterpret_cast<const void*>(&nsf_wconv_kernel<C, FM, FN, WM, WN, IB, OB>),                              \
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                                                  \
     if (attr != hipSuccess) { set_error("nsf conv: cannot raise the dynamic LDS limit"); return PD_ERR_HIP; }    \
-    hipLaunchKernelGGL((nsf_wconv_kernel<C, FM, FN, WM, WN, IB, OB>), grid, dim3(256), lds, st, in, wb, ldw,      \
+    hipLaunchKernelGGL((nsf_wconv_kernel<C, FM, FN, WM, WN, IB, OB>), grid, dim3(64 * WM * WN), lds, st, in, wb, ldw, \
                        c.kpad, c.b, c.taps, c.dil, alpha, scale, Tl, res, out, accum, rag_);                        \
   } while (0)
   ProfScope ps("nsf_res", st);
@@ -1696,7 +1762,10 @@ int launch_wconv(const NsfConv& c, const void* in, bool in_bf, float alpha, floa
     // 2 x 2 wave grids at C = 128/256 read every fragment twice; C5 21.07 -> 19.19 ms/step,
     // ResBlock convs 187 -> 159 us avg).  C = 32: 128, 256 or 512 rows per block measured
     // equal or slower than 128 rows with four row-waves.
-    case 256: return launch_wconv_c<256, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
+    case 256:
+      if (c.w256 == 1)   // NSF_OPT_C256 (r06): 8 waves, all 256 output channels per block (95 -> 83 us)
+        return launch_wconv_c<256, 4, 1, 1, 8>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
+      return launch_wconv_c<256, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
     case 128: return launch_wconv_c<128, 4, 1, 1, 4>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
     case 64: return launch_wconv_c<64, 4, 1, 2, 2>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
     case 32: return launch_wconv_c<32, 1, 1, 4, 1>(c, wb, in, in_bf, alpha, scale, B, Tl, out, out_bf, res, st, accum, rag_);
@@ -1998,6 +2067,16 @@ int nsf_set_option(nsf_model* m, int option, int value) {
     m->ups_nc = value != 0;
     return PD_OK;
   }
+  if (option == NSF_OPT_NC_MFMA) {
+    PD_CHECK_ARG(value >= 0 && value <= 2, "NSF_OPT_NC_MFMA is 0, 1 or 2");
+    m->nc_mfma = value;
+    return PD_OK;
+  }
+  if (option == NSF_OPT_C256) {
+    PD_CHECK_ARG(value == 0 || value == 1, "NSF_OPT_C256 is 0 or 1");
+    for (auto& c : m->res) c.w256 = value;
+    return PD_OK;
+  }
   if (option == NSF_OPT_RB32 || option == NSF_OPT_RB64) {
     PD_CHECK_ARG(value >= 0 && value <= 7, "NSF_OPT_RB32 / RB64: a kernel-size bit mask (1: 3, 2: 7, 4: 11)");
     (option == NSF_OPT_RB32 ? m->rb32 : m->rb64) = value;
@@ -2079,7 +2158,20 @@ int nsf_forward(const nsf_model* m, const float* mel, float mel_scale, const flo
       nz.har = har; nz.L = L; nz.w = U.nc_w; nz.b = U.nc_b;
       nz.k = U.nc_k; nz.stride = U.nc_stride; nz.pad = U.nc_pad; nz.rag = rag(m->upp);
     }
-    if (!nz.har) {
+    // (NSF_OPT_NC_MFMA 1: the K = 128 conv only; 2 (default): the K = 16 one too.  C5: 104-105 -> 91-93 us per
+    // launch, profiles/r06_ab/nsf_c256_noise_ab.txt)
+    if (!nz.har && m->nc_mfma && U.nc_stride * 2 == U.nc_k && (U.nc_k == 128 || (U.nc_k == 16 && m->nc_mfma == 2)) &&
+        U.cout % 32 == 0) {
+      ProfScope ps("nsf_noise_conv", st);
+      const dim3 grid(cdiv(Lc, 128), U.cout / 32, B);
+      if (U.nc_k == 128)
+        hipLaunchKernelGGL(nsf_noise_mfma_kernel<128>, grid, dim3(256), 0, st, har, L, U.nc_w, U.nc_b, U.cout,
+                           U.nc_pad, (long long)Lc, XSRC, rag(m->upp));
+      else
+        hipLaunchKernelGGL(nsf_noise_mfma_kernel<16>, grid, dim3(256), 0, st, har, L, U.nc_w, U.nc_b, U.cout,
+                           U.nc_pad, (long long)Lc, XSRC, rag(m->upp));
+      PD_LAUNCH_CHECK();
+    } else if (!nz.har) {
       const int CT = U.cout < 256 ? U.cout : 256, G = 256 / CT;
       const size_t lds = (size_t)((G * NC_ROWS - 1) * U.nc_stride + U.nc_k) * sizeof(float);
       ProfScope ps("nsf_noise_conv", st);

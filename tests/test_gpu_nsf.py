@@ -209,3 +209,29 @@ def test_bf16_resblock_fused_bitexact(opt, T, B, lens):
     else:
         for r, n in enumerate(lens):
             np.testing.assert_array_equal(outs[1][r, :n * g.upp], outs[0][r, :n * g.upp])
+
+
+@pytest.mark.parametrize("T,B,lens", [(24, 1, None), (37, 2, [37, 21]), (1, 3, None)])
+def test_bf16_c256_nc_mfma_bitexact(T, B, lens):
+    """r06 launch shapes against the previous ones, the waveform bit for bit: NSF_OPT_C256 (the 256-channel
+    windowed convs with 8 waves and all output channels per block) and NSF_OPT_NC_MFMA (the K = 128 / 16
+    source convs as f32-MFMA chains from the bias, the VALU kernel's fmaf order)."""
+    h = dict(synth.NSF_DEFAULTS)
+    g, _ = _gen(h, 7)
+    rng = np.random.default_rng(12)
+    mel = torch.from_numpy(rng.normal(-2.0, 1.0, size=(B, T, 128)).astype(np.float32)).to(DEV)
+    f0 = torch.from_numpy(rng.uniform(60.0, 900.0, size=(B, T)).astype(np.float32)).to(DEV)
+    g.set_compute_dtype("bf16")
+    outs = {}
+    for name, o in (("base", dict(c256=0, nc_mfma=0)), ("c256", dict(c256=1, nc_mfma=0)),
+                    ("nc_mfma", dict(c256=0, nc_mfma=2))):
+        g.set_options(**o)
+        outs[name] = g.synthesize(mel, f0, 2.30259, seed=9, lens=lens).cpu().numpy()
+    g.set_options(c256=1, nc_mfma=2)
+    for name in ("c256", "nc_mfma"):
+        assert np.isfinite(outs[name]).all()
+        if lens is None:
+            np.testing.assert_array_equal(outs[name], outs["base"], err_msg=name)
+        else:
+            for r, n in enumerate(lens):
+                np.testing.assert_array_equal(outs[name][r, :n * g.upp], outs["base"][r, :n * g.upp], err_msg=name)
