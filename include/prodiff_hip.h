@@ -244,6 +244,8 @@ size_t fd_workspace_size(const fd_model* m, int B, int Tc, int S);
 #define FD_OPT_LVC_TPW 10     /* 32-row tiles per wave of the 384-sample hop >= 32 LVC blocks: 2 (8 waves) or 1 (16 waves) */
 #define FD_OPT_LVC_PRIO 11    /* 1: s_setprio(1) for the second half of an LVC block's waves */
 /* 12: reserved (r04's persistent LVC kernel with LDS-DMA prefetch, removed: measured slower) */
+#define FD_OPT_LVC_PS 14      /* 1 (r06): the final (fused, prefetching, 384-sample) LVC block as a persistent kernel whose
+                               * next tile's audio / x_prev / biases arrive by LDS-DMA under the current tile's layers */
 /* 13: reserved (r04's multi-tile fused-DBlock blocks, removed: measured slower) */
 int fd_set_option(fd_model* m, int option, int value);
 

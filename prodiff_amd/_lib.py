@@ -16,7 +16,7 @@ PD_DTYPE_BF16 = 1
 PD_REFLOW = {"euler": 0, "rk2": 1, "rk4": 2, "rk5": 3}
 # fd_set_option / nsf_set_option ids (include/prodiff_hip.h)
 FD_OPTIONS = {"lvc_ts": 0, "lvc_ts_sub": 1, "lvc_fuse": 2, "lvc_pf": 3, "lvc_sub": 4, "kp_side": 5, "kp_chunk": 7,
-               "lvc_tpw": 10, "lvc_prio": 11}
+               "lvc_tpw": 10, "lvc_prio": 11, "lvc_ps": 14}
 NSF_OPTIONS = {"small_max": 0, "wconv": 1, "pair": 2, "pair16": 3, "ups_nc": 4, "rb16": 5, "rb32": 6, "rb64": 7, "c256": 8, "nc_mfma": 9}
 WN_OPTIONS = {"layer": 0, "ksplit": 1, "l2pf": 2, "stack": 3, "stack_ro": 4, "stack_fuse": 6, "f32_layer": 7}
 

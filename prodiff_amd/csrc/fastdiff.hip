@@ -71,6 +71,7 @@ struct fd_model {
   int kp_chunk = 0;   // FD_OPT_KP_CHUNK: utterances per kernel-predictor -> LVC chunk (0 = whole batch)
   int lvc_tpw = 2;    // FD_OPT_LVC_TPW: 32-row tiles per wave of the 384-sample hop >= 32 blocks (2 or 1)
   int lvc_prio = 0;   // FD_OPT_LVC_PRIO: 1 = s_setprio(1) for the second half of an LVC block's waves
+  int lvc_ps = 1;     // FD_OPT_LVC_PS (r06): the final block as a persistent kernel with LDS-DMA prefetch
 
   mutable hipStream_t side = nullptr;
   mutable hipEvent_t ev_hidden = nullptr, ev_kp[4] = {}, ev_lvc[4] = {};
@@ -1077,6 +1078,448 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
   LB_STAMP(15);
 #undef TILE
 }
+
+// ------------------------------------------------------------------ persistent final block (r06)
+// LDS-DMA by inline asm: one global_load_lds per wave (M0 = the wave's LDS destination, lane i's `bytes`
+// land at M0 + i * bytes).  Not the builtin: hipcc cannot tell the DMA's LDS destination from the U / Y
+// windows, so after a builtin DMA it waited vmcnt(0) -- for the DMA itself -- before every later LDS access.
+// Hidden from the waitcnt pass, the DMA must be OLDER than every load the pass waits on while it is in
+// flight (vmcnt retires in order): it is issued right after a tile's layer-0 MFMAs, before the layer-1
+// kernel fragments, and waited for explicitly (vmcnt at the next tile's top).  The asm sets M0, which hipcc
+// treats as reserved: this kernel has no other M0 use (no LDS-DMA builtin, no indirect register indexing).
+__device__ __forceinline__ void lds_dma16(const void* g, void* lds) {
+  const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(g) : "memory");
+}
+__device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
+  const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(l), "v"(g) : "memory");
+}
+// lvc_block_bf16_kernel<384, UPS, AUD, FIN, PF> as a persistent kernel (FD_OPT_LVC_PS): one 8-wave block
+// per CU walks the launch's tiles in the same XCD-aware order.  Each tile's prologue loads -- the audio
+// window, the x_prev rows, the frames' LVC biases -- arrive by LDS-DMA (global_load_lds) issued during the
+// PREVIOUS tile's layers, and layer 0's kernel fragments by register loads issued after the previous
+// tile's last LVC MFMAs: the phase probe (tools/lvc_probe, profiles/r06_ab/lvc_xprev_bf16_ab.txt) put 15%
+// of a one-tile block's life in waiting for those loads, with one block per CU and nothing to overlap them.
+// The tile-invariant operands (pre-conv weights and biases, first / final conv, upsample bias) are staged
+// once per block.  DMA'd values land raw: the masks (zero outside the utterance) and the gate pre-scale of
+// the biases are applied where they are read -- the same values the one-tile kernel stores, so the same
+// arithmetic, roundings and MFMA order: bit-identical (tests/test_gpu_bf16.py).
+#ifdef LB_TRACE
+// tools/lvc_probe ps mode: per-phase s_memtime stamps of iteration 5 of every 4th block, lane 0 of each wave
+#define PS_STAMP(i)                                                                                        \
+  do {                                                                                                     \
+    if (it == 5 && (tq & 63) == 0 && blockIdx.x % 4 == 0)                                                  \
+      P.trace[((blockIdx.x / 4) * NW + (tq >> 6)) * 24 + (i)] = __builtin_readcyclecounter();              \
+  } while (0)
+#else
+#define PS_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+__global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs P, int ntx, int ntiles) {
+  constexpr int TS = 384, TPW = 2;
+  using G = LbGeo<TS, TPW>;
+  constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF, GR = NG * 32, EX = 3, NT = G::NT;
+  constexpr int BFR = GR / 256 + 2;                    // frames a tile touches at hop 256 (host-checked)
+  constexpr int XROWS = G::NTJ_MAX * 32 + 1, XROWS8 = (XROWS + 7) / 8 * 8;   // x_prev rows (r = 4: 161)
+  constexpr int NAS = GR + 6, NAS64 = (NAS + 63) / 64 * 64;                  // audio samples of a tile
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  __shared__ __attribute__((aligned(16))) float AS[2][NAS64];                // audio, times tg - 3 + i (raw)
+  __shared__ __attribute__((aligned(16))) float XPN[XROWS8 * CI];           // x_prev rows jb + rr (raw)
+  __shared__ __attribute__((aligned(16))) float BFL[2][BFR * 2 * CI * NLY]; // frames' LVC biases (raw)
+  __shared__ __attribute__((aligned(16))) float FW[7 * 32];
+  __shared__ __attribute__((aligned(16))) float FWF[7 * 32];
+  __shared__ __attribute__((aligned(16))) float FBL[32];
+  __shared__ __attribute__((aligned(16))) float BUL[32];
+  __shared__ __attribute__((aligned(16))) bf16x8 WCL[NLY * 6 * 64];
+  __shared__ __attribute__((aligned(16))) float BCL[NLY * CI];
+  __bf16* U = reinterpret_cast<__bf16*>(smem);
+  __bf16* Y = U + G::UROWS * LB_LD;
+  float* XS = reinterpret_cast<float*>(smem);
+  __bf16* XP = reinterpret_cast<__bf16*>(smem + G::XS_BYTES);
+  const int tid = threadIdx.x;
+  const int Tc = P.Tc, hop = P.hop, Lh = Tc * hop;
+  const int r = P.r, pp = P.p, Tin = Lh / r;
+  const int ntj = (GR / r + 2 + 31) / 32;
+  constexpr int RLO = 64 - 44 - EX, RHI = 64 + TS + 44 + EX;
+  // ---- tile-invariant operands, once per block
+  if (tid < 224) FW[tid] = P.fw[(tid & 31) * 7 + (tid >> 5)];
+  if (tid < 32) FBL[tid] = P.fb[tid];
+  if (tid < 32) BUL[tid] = P.bup[tid];
+  if (tid < 224) FWF[tid] = P.wfin[tid];
+  if (tid < 6 * 64) {
+    const int kk = tid >> 6, ln = tid & 63;
+#pragma unroll
+    for (int l = 0; l < NLY; ++l) {
+      const __bf16* w = P.Wc[l] + (ln & 31) * 96 + (kk >> 1) * 32 + 16 * (ln >> 5) + 4 * (kk & 1);
+      const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(w), w1 = *reinterpret_cast<const bf16x4*>(w + 8);
+      WCL[l * 384 + tid] = bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+    }
+  }
+  if (tid < NLY * CI) BCL[tid] = P.bc[tid / CI][tid % CI];
+  const float bfin = P.bfin[0];
+  // tile v -> (utterance, time tile): the one-tile kernel's XCD-aware order (gridDim.x % 8 == 0, so tile v
+  // runs on the XCD of block v % gridDim.x, as block v did there)
+  auto coords = [&](int v, int& b, int& bx) {
+    const int xcd = v & 7, slot = v >> 3, per = ntiles >> 3, rem = ntiles & 7;
+    const int logical = xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
+    b = __builtin_amdgcn_readfirstlane(logical / ntx);   // (uniform: scalar loads of lens / uid)
+    bx = __builtin_amdgcn_readfirstlane(logical - b * ntx);
+  };
+  // a tile's loads straight into LDS (buffer s of AS / BFL, and XPN)
+  auto dma = [&](int v, int s, int wave, int lane) {
+    int b, bx;
+    coords(v, b, bx);
+    const int tg = bx * TS - 64, jb = floordiv(tg + pp, r) - 2, fbase = (tg > 0 ? tg : 0) / hop;
+    const long long base = (long long)b * Lh;
+#pragma unroll
+    for (int q0 = 0; q0 < NAS64 / 64; q0 += NW) {          // 4-B pieces, one sample per lane
+      const int q = q0 + wave;
+      if (q * 64 < NAS) {
+        const int t = tg - 3 + q * 64 + lane;
+        lds_dma4(P.audio + base + min(max(t, 0), Lh - 1), &AS[s][q * 64]);
+      }
+    }
+#pragma unroll
+    for (int q0 = 0; q0 < XROWS8 / 8; q0 += NW) {          // 16-B pieces, 8 rows of 32 channels per wave
+      const int q = q0 + wave;
+      if (q * 8 < XROWS) {
+        const int j = min(max(jb + q * 8 + (lane >> 3), 0), Tin - 1);
+        lds_dma16(P.xin + ((long long)b * Tin + j) * CI + (lane & 7) * 4, &XPN[q * 8 * CI]);
+      }
+    }
+    if (wave < BFR) {                                       // one frame (256 floats) per wave
+      const int fr = min(fbase + wave, Tc - 1);
+      lds_dma16(P.Bf + ((long long)b * Tc + fr) * (2 * CI * NLY) + lane * 4, &BFL[s][wave * 2 * CI * NLY]);
+    }
+  };
+  bf16x8 kn[12];
+  auto kload = [&](int b, int fpair, int l, int lane) {
+    const __bf16* kq = P.Kf[l] + ((long long)b * Tc + fpair) * KPERLAYER;
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk) kn[kk] = *reinterpret_cast<const bf16x8*>(kq + (kk * 64 + lane) * 8);
+  };
+  auto fpair_of = [&](int tg, int wave) { return min(max(tg + 32 * TPW * wave + 16 * TPW, 0) / hop, Tc - 1); };
+  // a tile's utterance end and utterance id, loaded a tile ahead (at the DMA) by unconditional loads from a
+  // selected pointer: under `P.lens ?` / `P.uid ?` branches the waitcnt pass waited vmcnt(0) at the join --
+  // for the DMA and the kernel-fragment loads in flight
+  // (raw values only: used -- and so waited for -- at the next tile's top, both loads in flight together;
+  // r06 probe: computed at the load, they cost two serial round trips inside layer 0)
+  int lv_n = 0, uv_n = 0;
+  float zn_n = 0.f;     // the explicit sampler draw of thread tq's sample (P.noise; unconditional load)
+  auto tile_scalars = [&](int v, int tq) {
+    int b, bx;
+    coords(v, b, bx);
+    lv_n = *(P.lens ? P.lens + b : reinterpret_cast<const int*>(P.Bf));
+    uv_n = *(P.uid ? P.uid + b + P.b_off : reinterpret_cast<const int*>(P.Bf));
+    zn_n = (P.noise ? P.noise : P.audio)[(long long)b * Lh + min(bx * TS + tq, Lh - 1)];
+  };
+  const int v0 = blockIdx.x;
+  __syncthreads();                                         // the invariant operands are staged
+  if (v0 < ntiles) {
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    int b, bx;
+    coords(v0, b, bx);
+    tile_scalars(v0, tid);
+    dma(v0, 0, wave, lane);
+    kload(b, fpair_of(bx * TS - 64, wave), 0, lane);
+  }
+  int it = 0;
+  for (int v = v0; v < ntiles; v += gridDim.x, ++it) {
+    const int cur = it & 1;
+    // thread ids through an opaque copy: addresses derived from them are recomputed per tile instead of
+    // hoisted out of the loop and spilled
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    const int lane = tq & 63, n = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tq >> 6);
+    PS_STAMP(0);
+    int b, bx;
+    coords(v, b, bx);
+    const int Le = P.lens ? min(__builtin_amdgcn_readfirstlane(lv_n), Tc) * hop : Lh;
+    const unsigned uidv = P.uid ? (unsigned)__builtin_amdgcn_readfirstlane(uv_n) : (unsigned)(b + P.b_off);
+    const int t0 = bx * TS, tg = t0 - 64;
+    const long long base = (long long)b * Lh;
+    const int Tin_e = Le / r;
+    const int fbase = (tg > 0 ? tg : 0) / hop;
+    const int jb = floordiv(tg + pp, r) - 2;
+    const int fpair = fpair_of(tg, wave);
+    // this tile's DMA (issued a tile ago) has landed for every wave: each waits for its own pieces -- the
+    // 12 younger kernel-fragment loads (and at most one audio_out store) may stay in flight -- then a barrier
+    __builtin_amdgcn_s_waitcnt(0x0F7C);                    // vmcnt(12)
+    __syncthreads();
+    PS_STAMP(1);
+    // phase-GEMM weights (NW % r == 0: wave w computes phase w % r), FIN noise
+    bf16x8 wfj[4];
+    {
+      const __bf16* wa = P.Wup + ((long long)(wave % r) * 32 + n) * 64 + 8 * h;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wfj[kk] = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
+    }
+    // (the explicit draw loaded a tile ahead, unconditionally: under `P.noise ?` the waitcnt pass waited for
+    // every outstanding load -- the next tile's kernel fragments included -- at the join)
+    const float znz = zn_n;
+    const float zph = philox_normal_u(P.seed, uidv, (unsigned)(t0 + tq), P.stream);
+    const float zr = (tq < TS && t0 + tq < Lh && P.sig != 0.f) ? (P.noise ? znz : zph) : 0.f;
+    // audio samples outside the utterance -> 0 in place (the one-tile kernel's masked staging: the DMA
+    // lands raw values; only the out-of-range ones are rewritten, so no LDS read)
+#pragma unroll
+    for (int ia = 0; ia < NAS64 / NT + 1; ++ia) {
+      const int i = tq + ia * NT, t = tg - 3 + i;
+      if (i < NAS && (t < 0 || t >= Le)) AS[cur][i] = 0.f;
+    }
+    // (a) XP[j - jb] = bf16 lrelu(x_prev[j]), zero outside the utterance
+    constexpr int IX = ((G::NTJ_MAX * 32 + 1) * 8 + NT - 1) / NT;
+#pragma unroll
+    for (int itx = 0; itx < IX; ++itx) {
+      const int i = tq + itx * NT, rr = i >> 3, q = (i & 7) * 4, j = jb + rr;
+      if (i < (ntj * 32 + 1) * 8) {
+        const float m = (j >= 0 && j < Tin_e) ? 1.f : 0.f;
+        const float4 xv = *reinterpret_cast<const float4*>(&XPN[rr * CI + q]);
+        const f32x2 u0 = lrelu2(f32x2{xv.x, xv.y} * m), u1 = lrelu2(f32x2{xv.z, xv.w} * m);
+        *reinterpret_cast<bf16x4*>(&XP[rr * LB_LD + q]) = bf16x4{(__bf16)u0.x, (__bf16)u0.y, (__bf16)u1.x, (__bf16)u1.y};
+      }
+    }
+    __syncthreads();
+    PS_STAMP(2);
+    // (b) phase GEMMs: C^T[co][col] = [W_k^T | W_{k+r}^T] . [xp(j0); xp(j0 - 1)], t = r j0 + k - p
+    {
+      const int k = wave % r;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int jt = wave / r + qq * (NW / r);
+        if (jt < ntj) {
+          f32x16 acc;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const bf16x8 xb = *reinterpret_cast<const bf16x8*>(
+                &XP[(jt * 32 + n + (kk < 2 ? 1 : 0)) * LB_LD + 16 * (kk & 1) + 8 * h]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfj[kk], xb, acc, 0, 0, 0);
+          }
+          const int j0 = jb + 1 + jt * 32 + n, row = r * j0 + k - pp - tg;
+          if (row >= RLO && row < RHI) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const float4 bv = *reinterpret_cast<const float4*>(&BUL[8 * g + 4 * h]);
+              *reinterpret_cast<float4*>(&XS[row * LB_XLD + 8 * g + 4 * h]) =
+                  make_float4(acc[4 * g] + bv.x, acc[4 * g + 1] + bv.y, acc[4 * g + 2] + bv.z, acc[4 * g + 3] + bv.w);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    PS_STAMP(3);
+    // x rows -> registers: z = x + a, a = first_conv(audio) (first_conv_kernel's order)
+    f32x2 xr[TPW][8], ar[TPW][8];
+    const float* as = AS[cur];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int k = 2 * wave + j, row = k * 32 + n, t = tg + row;
+      const bool ok = row >= RLO && row < RHI && t >= 0 && t < Le;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
+        if (ok) {
+          xv = *reinterpret_cast<const float4*>(&XS[row * LB_XLD + 8 * i + 4 * h]);
+          float a4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a4[e] = FBL[8 * i + 4 * h + e];
+#pragma unroll
+          for (int tap = 0; tap < 7; ++tap) {
+            const float sv = as[row + tap];
+            const float4 w = *reinterpret_cast<const float4*>(&FW[tap * 32 + 8 * i + 4 * h]);
+            a4[0] = fmaf(w.x, sv, a4[0]); a4[1] = fmaf(w.y, sv, a4[1]);
+            a4[2] = fmaf(w.z, sv, a4[2]); a4[3] = fmaf(w.w, sv, a4[3]);
+          }
+          av = make_float4(a4[0], a4[1], a4[2], a4[3]);
+        }
+        xr[j][2 * i] = f32x2{xv.x + av.x, xv.y + av.y}; xr[j][2 * i + 1] = f32x2{xv.z + av.z, xv.w + av.w};
+        ar[j][2 * i] = f32x2{av.x, av.y}; ar[j][2 * i + 1] = f32x2{av.z, av.w};
+      }
+    }
+    __syncthreads();                                       // XS reads done before U / Y (aliased) are written
+    PS_STAMP(4);
+    if (P.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    const float* bfl = BFL[cur];
+#pragma unroll
+    for (int l = 0; l < NLY; ++l) {
+      const int d = l == 0 ? 1 : l == 1 ? 3 : l == 2 ? 9 : 27;
+      const int e = (l == 0 ? 42 : l == 1 ? 38 : l == 2 ? 28 : 0) + EX;
+      const int kf = (64 - e) / 32, kl = (64 + TS + e - 1) / 32;
+      const int kpl = kl + 1 < NG - 1 ? kl + 1 : NG - 1;
+      // (1) u = lrelu(z) of the owned tiles the pre-conv reads
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const int k = 2 * wave + j;
+        if (k >= kf - 1 && k <= kl + 2) {
+          bf16x8 u0, u1;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const f32x2 v0 = lrelu2(xr[j][p]), v1 = lrelu2(xr[j][4 + p]);
+            u0[2 * p] = (__bf16)v0.x; u0[2 * p + 1] = (__bf16)v0.y;
+            u1[2 * p] = (__bf16)v1.x; u1[2 * p + 1] = (__bf16)v1.y;
+          }
+          const int ts = tg + k * 32;
+          if (ts < 0 || ts >= Le) { u0 = bf16x8{}; u1 = bf16x8{}; }
+          __bf16* dst = &U[(k * 32 + n + UOFF) * LB_LD + 16 * h];
+          *reinterpret_cast<bf16x8*>(dst) = u0;
+          *reinterpret_cast<bf16x8*>(dst + 8) = u1;
+        }
+      }
+      __syncthreads();
+      PS_STAMP(5 + 3 * l);
+      // (2) y^T = lrelu(W_c . [u(t-d); u(t); u(t+d)]^T + b)
+      {
+        bf16x8 wf[6];
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) wf[kk] = WCL[(l * 6 + kk) * 64 + lane];
+        f32x2 bias[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 bv = *reinterpret_cast<const float4*>(&BCL[l * CI + 8 * i + 4 * h]);
+          bias[2 * i] = f32x2{bv.x, bv.y}; bias[2 * i + 1] = f32x2{bv.z, bv.w};
+        }
+        for (int kp = kf + wave; kp <= kpl; kp += NW) {
+          f32x16 acc;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+          for (int kk = 0; kk < 6; ++kk) {
+            const int tap = kk >> 1;
+            const bf16x8 bu = *reinterpret_cast<const bf16x8*>(
+                &U[(kp * 32 + n + UOFF - 1 + (tap - 1) * d) * LB_LD + 16 * (kk & 1) + 8 * h]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc, 0, 0, 0);
+          }
+          f32x2 vv[8];
+#pragma unroll
+          for (int p = 0; p < 8; ++p) vv[p] = lrelu2(f32x2{acc[2 * p], acc[2 * p + 1]} + bias[p]);
+          const int tt = tg + kp * 32 - 1;
+          if (tt < 0 || tt + 31 >= Le) {
+            const int t = tt + n;
+            const bool in = t >= 0 && t < Le;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) vv[p] = in ? vv[p] : f32x2{0.f, 0.f};
+          }
+          bf16x8 y0, y1;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            y0[2 * p] = (__bf16)vv[p].x; y0[2 * p + 1] = (__bf16)vv[p].y;
+            y1[2 * p] = (__bf16)vv[4 + p].x; y1[2 * p + 1] = (__bf16)vv[4 + p].y;
+          }
+          __bf16* dst = &Y[(kp * 32 + n) * LB_LD + 16 * h];
+          *reinterpret_cast<bf16x8*>(dst) = y0;
+          *reinterpret_cast<bf16x8*>(dst + 8) = y1;
+        }
+      }
+      __syncthreads();
+      PS_STAMP(6 + 3 * l);
+      // (3) o^T = K_frame . [y(t-1); y(t); y(t+1)]^T + Bf;  x += a + sigmoid(o_g) tanh(o_f)
+      f32x16 g[TPW], f[TPW];
+      const float* bq = &bfl[((fpair - fbase) * NLY + l) * 2 * CI];
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {   // the gate pre-scale the one-tile kernel applies at staging
+          const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
+          const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
+          g[j][4 * i] = bg.x * -LOG2E; g[j][4 * i + 1] = bg.y * -LOG2E;
+          g[j][4 * i + 2] = bg.z * -LOG2E; g[j][4 * i + 3] = bg.w * -LOG2E;
+          f[j][4 * i] = bl.x * (2.f * LOG2E); f[j][4 * i + 1] = bl.y * (2.f * LOG2E);
+          f[j][4 * i + 2] = bl.z * (2.f * LOG2E); f[j][4 * i + 3] = bl.w * (2.f * LOG2E);
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) {
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          const bf16x8 yb = *reinterpret_cast<const bf16x8*>(
+              &Y[((2 * wave + j) * 32 + n + (kk >> 1)) * LB_LD + 16 * (kk & 1) + 8 * h]);
+          g[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[kk], yb, g[j], 0, 0, 0);
+          f[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kn[6 + kk], yb, f[j], 0, 0, 0);
+        }
+      }
+      // the next tile's DMA after layer 0's MFMAs (its XPN was read in this tile's prologue, its AS / BFL
+      // buffer cur ^ 1 by the previous tile), ahead of the kernel-fragment loads
+      if (l == 0 && v + (int)gridDim.x < ntiles) {   // (the scalars' loads first: waiting for them is not
+        tile_scalars(v + gridDim.x, tq);               // waiting for the DMA)
+        dma(v + gridDim.x, cur ^ 1, wave, lane);
+      }
+      if (l + 1 < NLY) {
+        kload(b, fpair, l + 1, lane);
+      } else if (v + (int)gridDim.x < ntiles) {            // the next tile's layer-0 fragments
+        int b2, bx2;
+        coords(v + gridDim.x, b2, bx2);
+        kload(b2, fpair_of(bx2 * TS - 64, wave), 0, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x2 gs0 = {g[j][4 * i], g[j][4 * i + 1]}, gs1 = {g[j][4 * i + 2], g[j][4 * i + 3]};
+          const f32x2 fs0 = {f[j][4 * i], f[j][4 * i + 1]}, fs1 = {f[j][4 * i + 2], f[j][4 * i + 3]};
+          const f32x2 r0 = gate2r(gs0, fs0), r1 = gate2r(gs1, fs1);
+          const f32x2 ef0 = gate2ef(fs0), ef1 = gate2ef(fs1);
+          const f32x2 q0 = (l + 1 < NLY ? xr[j][2 * i] + ar[j][2 * i] : xr[j][2 * i]) - r0;
+          const f32x2 q1 = (l + 1 < NLY ? xr[j][2 * i + 1] + ar[j][2 * i + 1] : xr[j][2 * i + 1]) - r1;
+          xr[j][2 * i] = efma(ef0, r0, q0);
+          xr[j][2 * i + 1] = efma(ef1, r1, q1);
+        }
+      }
+      PS_STAMP(7 + 3 * l);
+    }
+    if (P.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(0);
+    // FIN: eps(t) = b + sum_tap E[t + tap - 3][tap], then the sampler update (util.py:222-226)
+    float* E = XS;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int k = 2 * wave + j, row = k * 32 + n;
+      if (k >= 1 && k <= NG - 2) {
+        float st[7];
+#pragma unroll
+        for (int tap = 0; tap < 7; ++tap) {
+          f32x2 acc = {0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 w = *reinterpret_cast<const float4*>(&FWF[tap * 32 + 8 * i + 4 * h]);
+            acc = efma(xr[j][2 * i], f32x2{w.x, w.y}, acc);
+            acc = efma(xr[j][2 * i + 1], f32x2{w.z, w.w}, acc);
+          }
+          st[tap] = acc.x + acc.y;
+        }
+#pragma unroll
+        for (int tap = 0; tap < 7; ++tap) st[tap] += __shfl_xor(st[tap], 32);
+        const int ts = tg + k * 32;
+        if (ts < 0 || ts >= Le) {
+#pragma unroll
+          for (int tap = 0; tap < 7; ++tap) st[tap] = 0.f;
+        }
+        if (h == 0) {
+          *reinterpret_cast<float4*>(&E[row * 8]) = make_float4(st[0], st[1], st[2], st[3]);
+          *reinterpret_cast<float4*>(&E[row * 8 + 4]) = make_float4(st[4], st[5], st[6], 0.f);
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const int s = tq, t = t0 + s;
+      if (s < TS && t < Lh) {
+        float e = bfin;
+#pragma unroll
+        for (int tap = 0; tap < 7; ++tap) e += E[(64 + s + tap - 3) * 8 + tap];
+        float vv = (as[67 + s] - P.ce * e) / P.den;
+        if (P.sig != 0.f) vv += P.sig * zr;
+        P.audio_out[base + t] = vv;
+      }
+    }
+    PS_STAMP(17);
+  }
+}
+#undef PS_STAMP
 
 // ------------------------------------------------------------------ DiffusionDBlock (bf16)
 // modules.py:131-138 in one launch:
@@ -2168,7 +2611,19 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
                                                                                    : "fd_lvc_block", st);
         const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
         const bool pf = m->lvc_pf && hop % 64 == 0;   // a 64-row tile pair shares one frame
-        if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
+        if (fuse_fin && pf && ts == 384 && m->lvc_tpw == 2 && m->lvc_ps && r == 4 && hop % 256 == 0) {
+          // r06: persistent, one block per CU (a multiple of 8 blocks keeps the XCD-aware tile order)
+          static int ncu = 0;
+          if (!ncu) {
+            int dev = 0;
+            PD_HIP(hipGetDevice(&dev));
+            PD_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+          }
+          const int ntx = (int)cdiv(Tout, 384), ntiles = ntx * nbk;
+          const int grid = ntiles <= ncu ? ntiles : ncu / 8 * 8;
+          hipLaunchKernelGGL(lvc_final_ps_kernel, dim3(grid), dim3(512), 0, st, la, ntx, ntiles);
+          PD_LAUNCH_CHECK();
+        } else if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
         else if (ts == 384 && m->lvc_tpw == 1 && hop >= 32 && ups && (last && aud) == fuse_fin)
           PD_TRY((launch_lvc_block_ts<384, 1>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st)));
         else if (ts == 384) PD_TRY(launch_lvc_block_ts<384>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
@@ -2458,6 +2913,10 @@ int fd_set_option(fd_model* m, int option, int value) {
     case FD_OPT_LVC_PRIO:
       PD_CHECK_ARG(value == 0 || value == 1, "FD_OPT_LVC_PRIO in {0,1}");
       m->lvc_prio = value;
+      return PD_OK;
+    case FD_OPT_LVC_PS:
+      PD_CHECK_ARG(value == 0 || value == 1, "FD_OPT_LVC_PS in {0,1}");
+      m->lvc_ps = value;
       return PD_OK;
     case FD_OPT_LVC_TPW:
       PD_CHECK_ARG(value == 1 || value == 2, "FD_OPT_LVC_TPW in {1,2}");

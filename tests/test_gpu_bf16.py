@@ -380,3 +380,41 @@ def test_pitch_reflow_stack_bitexact(algo, ragged):
             np.testing.assert_array_equal(outs["stack"][r, :n], outs["layer"][r, :n])
     else:
         np.testing.assert_array_equal(outs["stack"], outs["layer"])
+
+
+@pytest.mark.parametrize("B,Tc,lens,draws", [(1, 1, None, "explicit"), (3, 5, [5, 2, 4], "explicit"),
+                                              (4, 100, None, "philox"), (8, 200, [200, 150, 199, 3, 200, 120, 77, 200],
+                                                                          "philox")])
+def test_fastdiff_lvc_persistent_bitexact(B, Tc, lens, draws):
+    """FD_OPT_LVC_PS (r06: the final LVC block as a persistent kernel, one block per CU walking the tiles,
+    the next tile's audio / x_prev / biases by LDS-DMA under the current tile's layers) against the
+    one-tile-per-block kernel: the 4-step sample bit for bit -- one tile, ragged rows, and grids of 268 and
+    1 072 tiles (several per block), explicit and on-device draws."""
+    from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
+    from prodiff_amd import _lib
+    p = G.fastdiff_params(31)
+    b, a, s, st = fastdiff_infer_params(fastdiff_reverse_schedule(4), fastdiff_train_alpha())
+    mel = synth.synth_inputs(80 + B, (B, Tc, 80), loc=-5.0, scale=2.0)
+    kw = {}
+    if draws == "explicit":
+        kw = dict(x_T=tt(synth.synth_inputs(81 + B, (B, 1, Tc * 256))),
+                  noise=tt(synth.synth_inputs(82 + B, (3, B, 1, Tc * 256))))
+    else:
+        kw = dict(seed=77)
+    outs = []
+    for ps in (0, 1):
+        m = FastDiff()
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+        m = m.to(DEV).set_compute_dtype("bf16").set_options(lvc_ps=ps)
+        _lib.profile_enable(True)
+        outs.append(m.sample(tt(mel), b, a, s, st, lens=lens, **kw).cpu().numpy())
+        torch.cuda.synchronize()
+        assert "fd_lvc_block_final" in _lib.profile_summary()
+        _lib.profile_enable(False)
+    assert np.isfinite(outs[1]).all()
+    if lens is None:
+        np.testing.assert_array_equal(outs[1], outs[0])
+    else:
+        o0, o1 = outs[0].reshape(B, -1), outs[1].reshape(B, -1)
+        for r, n in enumerate(lens):
+            np.testing.assert_array_equal(o1[r, :n * 256], o0[r, :n * 256])

@@ -41,7 +41,7 @@ template <typename T> static T* upload(size_t n, float scale) {
 
 // FINAL: the sampler's last block as bench.py runs it (upsample r=4 + first conv + final
 // update fused, next-layer kernel prefetch): lvc_block_bf16_kernel<TS, true, true, true, true>.
-template <int TS, bool FINAL = false> static void run(int hop) {
+template <int TS, bool FINAL = false, bool PS = false> static void run(int hop) {
   using G = LbGeo<TS>;
   constexpr bool UPS = FINAL, AUD = FINAL, FIN = FINAL, PF = FINAL;
   const int B = 8, Tc = 861;
@@ -71,6 +71,48 @@ template <int TS, bool FINAL = false> static void run(int hop) {
     la.bfin = upload<float>(1, 0.05f);
     CK(hipMalloc((void**)&la.audio_out, rows * sizeof(float)));
     la.ce = 0.3f; la.den = 0.9f; la.sig = 0.1f; la.seed = 7; la.stream = 1;
+  }
+  if (PS) {   // the persistent final block (r06): iteration-5 stamps of every 4th block
+    const int ntx = cdiv(Lh, TS), ntiles = ntx * B, nblk = 256;
+    constexpr int NS = 24;
+    const int nsamp = nblk / 4;
+    CK(hipMalloc((void**)&la.trace, (size_t)nsamp * G::NW * NS * 8));
+    CK(hipMemset(la.trace, 0, (size_t)nsamp * G::NW * NS * 8));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(lvc_final_ps_kernel, dim3(nblk), dim3(512), 0, 0, la, ntx, ntiles);
+    const int reps = 20;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(lvc_final_ps_kernel, dim3(nblk), dim3(512), 0, 0, la, ntx, ntiles);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("PS TS=%d hop=%d tiles=%d blocks=%d  %.1f us/launch\n", TS, hop, ntiles, nblk, ms * 1000.0 / reps);
+    std::vector<unsigned long long> tr((size_t)nsamp * G::NW * NS);
+    CK(hipMemcpy(tr.data(), la.trace, tr.size() * 8, hipMemcpyDeviceToHost));
+    const char* names[18] = {"top", "dma wait", "XP fill", "phase GEMM", "x/a regs", "L0 stage", "L0 preconv",
+                             "L0 lvc", "L1 stage", "L1 preconv", "L1 lvc", "L2 stage", "L2 preconv", "L2 lvc",
+                             "L3 stage", "L3 preconv", "L3 lvc", "FIN"};
+    std::vector<std::vector<double>> ph(18);
+    std::vector<double> life;
+    for (int w = 0; w < nsamp * G::NW; ++w) {
+      const unsigned long long* t = &tr[(size_t)w * NS];
+      bool ok = t[0] != 0;
+      for (int q = 1; q < 18 && ok; ++q) ok = t[q] >= t[q - 1] && t[q] - t[q - 1] < 100000000ull;
+      if (!ok) continue;
+      for (int q = 1; q < 18; ++q) ph[q].push_back((double)(t[q] - t[q - 1]));
+      life.push_back((double)(t[17] - t[0]));
+    }
+    auto med = [](std::vector<double> v) {
+      if (v.empty()) return 0.0;
+      std::sort(v.begin(), v.end());
+      return v[v.size() / 2];
+    };
+    const double L = med(life);
+    printf("  %zu sampled waves, median tile time %.0f cycles\n", life.size(), L);
+    for (int q = 1; q < 18; ++q) printf("    %-11s %8.0f cyc  %5.1f%%\n", names[q], med(ph[q]), 100.0 * med(ph[q]) / L);
+    return;
   }
   const dim3 grid(cdiv(Lh, TS), B);
   const int nsamp = (grid.x * grid.y) / 61 + 1;
@@ -128,7 +170,8 @@ template <int TS, bool FINAL = false> static void run(int hop) {
 int main(int argc, char** argv) {
   const int hop = argc > 1 ? atoi(argv[1]) : 256;
   const int ts = argc > 2 ? atoi(argv[2]) : 128;
-  if (argc > 3 && atoi(argv[3]) == 1) run<384, true>(hop);
+  if (argc > 3 && atoi(argv[3]) == 2) run<384, true, true>(hop);
+  else if (argc > 3 && atoi(argv[3]) == 1) run<384, true>(hop);
   else if (ts == 256) run<256>(hop);
   else run<128>(hop);
   return 0;
