@@ -1134,6 +1134,7 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
   __shared__ __attribute__((aligned(16))) float BUL[32];
   __shared__ __attribute__((aligned(16))) bf16x8 WCL[NLY * 6 * 64];
   __shared__ __attribute__((aligned(16))) float BCL[NLY * CI];
+  __shared__ float EB[8][2][3][8];                                           // FIN: pairs' outer E rows
   __bf16* U = reinterpret_cast<__bf16*>(smem);
   __bf16* Y = U + G::UROWS * LB_LD;
   float* XS = reinterpret_cast<float*>(smem);
@@ -1207,13 +1208,13 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
   // (raw values only: used -- and so waited for -- at the next tile's top, both loads in flight together;
   // r06 probe: computed at the load, they cost two serial round trips inside layer 0)
   int lv_n = 0, uv_n = 0;
-  float zn_n = 0.f;     // the explicit sampler draw of thread tq's sample (P.noise; unconditional load)
+  float zn_n = 0.f;     // the explicit sampler draw of thread tq's sample tq - 64 (P.noise; unconditional load)
   auto tile_scalars = [&](int v, int tq) {
     int b, bx;
     coords(v, b, bx);
     lv_n = *(P.lens ? P.lens + b : reinterpret_cast<const int*>(P.Bf));
     uv_n = *(P.uid ? P.uid + b + P.b_off : reinterpret_cast<const int*>(P.Bf));
-    zn_n = (P.noise ? P.noise : P.audio)[(long long)b * Lh + min(bx * TS + tq, Lh - 1)];
+    zn_n = (P.noise ? P.noise : P.audio)[(long long)b * Lh + min(max(bx * TS + tq - 64, 0), Lh - 1)];
   };
   const int v0 = blockIdx.x;
   __syncthreads();                                         // the invariant operands are staged
@@ -1260,8 +1261,10 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     // (the explicit draw loaded a tile ahead, unconditionally: under `P.noise ?` the waitcnt pass waited for
     // every outstanding load -- the next tile's kernel fragments included -- at the join)
     const float znz = zn_n;
-    const float zph = philox_normal_u(P.seed, uidv, (unsigned)(t0 + tq), P.stream);
-    const float zr = (tq < TS && t0 + tq < Lh && P.sig != 0.f) ? (P.noise ? znz : zph) : 0.f;
+    // (thread tq writes sample s = tq - 64: lane (n, h) of wave w holds row 64 w + 32 h + n of the window)
+    const int so = tq - 64;
+    const float zph = philox_normal_u(P.seed, uidv, (unsigned)(t0 + so), P.stream);
+    const float zr = (so >= 0 && so < TS && t0 + so < Lh && P.sig != 0.f) ? (P.noise ? znz : zph) : 0.f;
     // audio samples outside the utterance -> 0 in place (the one-tile kernel's masked staging: the DMA
     // lands raw values; only the out-of-range ones are rewritten, so no LDS read)
 #pragma unroll
@@ -1472,46 +1475,58 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
       PS_STAMP(7 + 3 * l);
     }
     if (P.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(0);
-    // FIN: eps(t) = b + sum_tap E[t + tap - 3][tap], then the sampler update (util.py:222-226)
-    float* E = XS;
-    __syncthreads();
+    // FIN: eps(t) = b + sum_tap E[t + tap - 3][tap], then the sampler update (util.py:222-226).  E stays in
+    // registers: lane (n, h) of wave w holds E of its pair's rows n (tile 2w) and 32 + n (tile 2w + 1) after the
+    // halves' partial sums meet, so the row shifts t + tap - 3 are lane permutes (ds_bpermute) within the
+    // 64-row pair; only the pair's outer three rows on each side go through LDS to the neighbouring waves.  One
+    // barrier instead of two, and no 16 KB E image (the one-tile kernel: 7.1k of 56k cycles per tile)
+    float ev[TPW][7];
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
-      const int k = 2 * wave + j, row = k * 32 + n;
-      if (k >= 1 && k <= NG - 2) {
-        float st[7];
 #pragma unroll
-        for (int tap = 0; tap < 7; ++tap) {
-          f32x2 acc = {0.f, 0.f};
+      for (int tap = 0; tap < 7; ++tap) {
+        f32x2 acc = {0.f, 0.f};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float4 w = *reinterpret_cast<const float4*>(&FWF[tap * 32 + 8 * i + 4 * h]);
-            acc = efma(xr[j][2 * i], f32x2{w.x, w.y}, acc);
-            acc = efma(xr[j][2 * i + 1], f32x2{w.z, w.w}, acc);
-          }
-          st[tap] = acc.x + acc.y;
+        for (int i = 0; i < 4; ++i) {             // channels 8i + 4h .. +3 = regs 4i .. 4i+3
+          const float4 w = *reinterpret_cast<const float4*>(&FWF[tap * 32 + 8 * i + 4 * h]);
+          acc = efma(xr[j][2 * i], f32x2{w.x, w.y}, acc);
+          acc = efma(xr[j][2 * i + 1], f32x2{w.z, w.w}, acc);
         }
-#pragma unroll
-        for (int tap = 0; tap < 7; ++tap) st[tap] += __shfl_xor(st[tap], 32);
-        const int ts = tg + k * 32;
-        if (ts < 0 || ts >= Le) {
-#pragma unroll
-          for (int tap = 0; tap < 7; ++tap) st[tap] = 0.f;
-        }
-        if (h == 0) {
-          *reinterpret_cast<float4*>(&E[row * 8]) = make_float4(st[0], st[1], st[2], st[3]);
-          *reinterpret_cast<float4*>(&E[row * 8 + 4]) = make_float4(st[4], st[5], st[6], 0.f);
-        }
+        ev[j][tap] = acc.x + acc.y;
       }
+#pragma unroll
+      for (int tap = 0; tap < 7; ++tap) ev[j][tap] += __shfl_xor(ev[j][tap], 32);
+      const int ts = tg + (2 * wave + j) * 32;
+      if (ts < 0 || ts >= Le) {                    // x is zero outside the utterance (the final conv's padding)
+#pragma unroll
+        for (int tap = 0; tap < 7; ++tap) ev[j][tap] = 0.f;
+      }
+    }
+    // the pair's rows 0..2 (tile 2w) and 61..63 (tile 2w + 1) for the neighbouring waves
+    if (h == 0 && n < 3) {
+#pragma unroll
+      for (int tap = 0; tap < 7; ++tap) EB[wave][0][n][tap] = ev[0][tap];
+    }
+    if (h == 0 && n >= 29) {
+#pragma unroll
+      for (int tap = 0; tap < 7; ++tap) EB[wave][1][n - 29][tap] = ev[1][tap];
     }
     __syncthreads();
     {
-      const int s = tq, t = t0 + s;
-      if (s < TS && t < Lh) {
-        float e = bfin;
+      const int rho = lane;                        // = 32 h + n: this lane's row within the pair
+      float e = bfin;
 #pragma unroll
-        for (int tap = 0; tap < 7; ++tap) e += E[(64 + s + tap - 3) * 8 + tap];
-        float vv = (as[67 + s] - P.ce * e) / P.den;
+      for (int tap = 0; tap < 7; ++tap) {
+        const int src = rho + tap - 3;             // source row within the pair, [-3, 67)
+        const int sl = src & 31;
+        const float v0 = __shfl(ev[0][tap], sl), v1 = __shfl(ev[1][tap], sl);
+        const float vl = EB[wave > 0 ? wave - 1 : 0][1][min(max(src + 3, 0), 2)][tap];        // wave w - 1, rows 61..63
+        const float vr = EB[wave < NW - 1 ? wave + 1 : NW - 1][0][min(max(src - 64, 0), 2)][tap];   // wave w + 1, rows 0..2
+        e += src < 0 ? vl : src < 32 ? v0 : src < 64 ? v1 : vr;
+      }
+      const int t = t0 + so;
+      if (so >= 0 && so < TS && t < Lh) {
+        float vv = (as[67 + so] - P.ce * e) / P.den;
         if (P.sig != 0.f) vv += P.sig * zr;
         P.audio_out[base + t] = vv;
       }
