@@ -828,17 +828,9 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
         const float4 bv = *reinterpret_cast<const float4*>((WW ? &BCL[l * CI] : P.bc[l]) + 8 * i + 4 * h);
         bias[2 * i] = f32x2{bv.x, bv.y}; bias[2 * i + 1] = f32x2{bv.z, bv.w};
       }
-      for (int kp = kf + wave; kp <= kpl; kp += NW) {
-        f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
-          const int tap = kk >> 1;
-          const bf16x8 bu = *reinterpret_cast<const bf16x8*>(
-              &U[(kp * 32 + n + UOFF - 1 + (tap - 1) * d) * LB_LD + 16 * (kk & 1) + 8 * h]);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc, 0, 0, 0);
-        }
+      // a wave's pre-conv tiles kp0 = kf + wave and kp1 = kp0 + NW (NG <= 2 NW: no third), their MFMA
+      // chains interleaved when it has both -- the same per-tile MFMA order, so the same values
+      auto pre_epi = [&](int kp, const f32x16& acc) {
         f32x2 v[8];
 #pragma unroll
         for (int p = 0; p < 8; ++p) v[p] = lrelu2(f32x2{acc[2 * p], acc[2 * p + 1]} + bias[p]);
@@ -858,6 +850,32 @@ void lvc_block_bf16_kernel(const LvcBlockArgs P) {
         __bf16* dst = &Y[(kp * 32 + n) * LB_LD + 16 * h];
         *reinterpret_cast<bf16x8*>(dst) = y0;
         *reinterpret_cast<bf16x8*>(dst + 8) = y1;
+      };
+      static_assert(NG <= 2 * NW, "at most two pre-conv tiles per wave");
+      const int kp0 = kf + wave, kp1 = kp0 + NW;
+      auto urow = [&](int kp, int kk) {
+        return *reinterpret_cast<const bf16x8*>(
+            &U[(kp * 32 + n + UOFF - 1 + ((kk >> 1) - 1) * d) * LB_LD + 16 * (kk & 1) + 8 * h]);
+      };
+      if (kp1 <= kpl) {
+        f32x16 a0, a1;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) { a0[q] = 0.f; a1[q] = 0.f; }
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const bf16x8 b0 = urow(kp0, kk), b1 = urow(kp1, kk);
+          a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], b0, a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], b1, a1, 0, 0, 0);
+        }
+        pre_epi(kp0, a0);
+        pre_epi(kp1, a1);
+      } else if (kp0 <= kpl) {
+        f32x16 a0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) a0[q] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], urow(kp0, kk), a0, 0, 0, 0);
+        pre_epi(kp0, a0);
       }
     }
     __syncthreads();
@@ -1103,8 +1121,9 @@ __device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
 // of a one-tile block's life in waiting for those loads, with one block per CU and nothing to overlap them.
 // The tile-invariant operands (pre-conv weights and biases, first / final conv, upsample bias) are staged
 // once per block.  DMA'd values land raw: the masks (zero outside the utterance) and the gate pre-scale of
-// the biases are applied where they are read -- the same values the one-tile kernel stores, so the same
-// arithmetic, roundings and MFMA order: bit-identical (tests/test_gpu_bf16.py).
+// the biases are applied in place in the tile's prologue or where they are read -- the same values the
+// one-tile kernel stores, so the same arithmetic, roundings and MFMA order: bit-identical
+// (tests/test_gpu_bf16.py).
 #ifdef LB_TRACE
 // tools/lvc_probe ps mode: per-phase s_memtime stamps of iteration 5 of every 4th block, lane 0 of each wave
 #define PS_STAMP(i)                                                                                        \
@@ -1127,7 +1146,7 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   __shared__ __attribute__((aligned(16))) float AS[2][NAS64];                // audio, times tg - 3 + i (raw)
   __shared__ __attribute__((aligned(16))) float XPN[XROWS8 * CI];           // x_prev rows jb + rr (raw)
-  __shared__ __attribute__((aligned(16))) float BFL[2][BFR * 2 * CI * NLY]; // frames' LVC biases (raw)
+  __shared__ __attribute__((aligned(16))) float BFL[2][BFR * 2 * CI * NLY]; // frames' LVC biases (pre-scaled)
   __shared__ __attribute__((aligned(16))) float FW[7 * 32];
   __shared__ __attribute__((aligned(16))) float FWF[7 * 32];
   __shared__ __attribute__((aligned(16))) float FBL[32];
@@ -1235,6 +1254,10 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     asm volatile("" : "+v"(tq));
     const int lane = tq & 63, n = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tq >> 6);
+    // the next tile, pinned in an SGPR here: rematerialised where it is used, its kernarg load waited
+    // lgkmcnt(0) -- for the LDS reads in flight -- inside the layer-0 MFMAs
+    int vnext = v + (int)gridDim.x;
+    asm volatile("" : "+s"(vnext));
     PS_STAMP(0);
     int b, bx;
     coords(v, b, bx);
@@ -1271,6 +1294,16 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     for (int ia = 0; ia < NAS64 / NT + 1; ++ia) {
       const int i = tq + ia * NT, t = tg - 3 + i;
       if (i < NAS && (t < 0 || t >= Le)) AS[cur][i] = 0.f;
+    }
+    // the frames' LVC biases: the gate pre-scale the one-tile kernel applies at staging, once per tile in
+    // place (read from the LVC phases on, past the barriers below)
+    {
+      float* bfs = BFL[cur];
+#pragma unroll
+      for (int ib = 0; ib < (BFR * 2 * CI * NLY + NT - 1) / NT; ++ib) {
+        const int i = tq + ib * NT;
+        if (i < BFR * 2 * CI * NLY) bfs[i] *= (i & 63) < 32 ? -LOG2E : 2.f * LOG2E;
+      }
     }
     // (a) XP[j - jb] = bf16 lrelu(x_prev[j]), zero outside the utterance
     constexpr int IX = ((G::NTJ_MAX * 32 + 1) * 8 + NT - 1) / NT;
@@ -1386,17 +1419,9 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
           const float4 bv = *reinterpret_cast<const float4*>(&BCL[l * CI + 8 * i + 4 * h]);
           bias[2 * i] = f32x2{bv.x, bv.y}; bias[2 * i + 1] = f32x2{bv.z, bv.w};
         }
-        for (int kp = kf + wave; kp <= kpl; kp += NW) {
-          f32x16 acc;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-#pragma unroll
-          for (int kk = 0; kk < 6; ++kk) {
-            const int tap = kk >> 1;
-            const bf16x8 bu = *reinterpret_cast<const bf16x8*>(
-                &U[(kp * 32 + n + UOFF - 1 + (tap - 1) * d) * LB_LD + 16 * (kk & 1) + 8 * h]);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], bu, acc, 0, 0, 0);
-          }
+        // a wave's pre-conv tiles kp0 = kf + wave and kp1 = kp0 + NW (NG <= 2 NW: no third), their
+        // MFMA chains interleaved -- the same per-tile MFMA order, so the same values
+        auto pre_epi = [&](int kp, const f32x16& acc) {
           f32x2 vv[8];
 #pragma unroll
           for (int p = 0; p < 8; ++p) vv[p] = lrelu2(f32x2{acc[2 * p], acc[2 * p + 1]} + bias[p]);
@@ -1416,6 +1441,32 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
           __bf16* dst = &Y[(kp * 32 + n) * LB_LD + 16 * h];
           *reinterpret_cast<bf16x8*>(dst) = y0;
           *reinterpret_cast<bf16x8*>(dst + 8) = y1;
+        };
+        static_assert(NG <= 2 * NW, "at most two pre-conv tiles per wave");
+        const int kp0 = kf + wave, kp1 = kp0 + NW;
+        auto urow = [&](int kp, int kk) {
+          return *reinterpret_cast<const bf16x8*>(
+              &U[(kp * 32 + n + UOFF - 1 + ((kk >> 1) - 1) * d) * LB_LD + 16 * (kk & 1) + 8 * h]);
+        };
+        if (kp1 <= kpl) {
+          f32x16 a0, a1;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) { a0[q] = 0.f; a1[q] = 0.f; }
+#pragma unroll
+          for (int kk = 0; kk < 6; ++kk) {
+            const bf16x8 b0 = urow(kp0, kk), b1 = urow(kp1, kk);
+            a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], b0, a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], b1, a1, 0, 0, 0);
+          }
+          pre_epi(kp0, a0);
+          pre_epi(kp1, a1);
+        } else if (kp0 <= kpl) {
+          f32x16 a0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) a0[q] = 0.f;
+#pragma unroll
+          for (int kk = 0; kk < 6; ++kk) a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kk], urow(kp0, kk), a0, 0, 0, 0);
+          pre_epi(kp0, a0);
         }
       }
       __syncthreads();
@@ -1426,13 +1477,11 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
 #pragma unroll
       for (int j = 0; j < TPW; ++j) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {   // the gate pre-scale the one-tile kernel applies at staging
+        for (int i = 0; i < 4; ++i) {   // (pre-scaled in the prologue)
           const float4 bg = *reinterpret_cast<const float4*>(bq + 8 * i + 4 * h);
           const float4 bl = *reinterpret_cast<const float4*>(bq + 32 + 8 * i + 4 * h);
-          g[j][4 * i] = bg.x * -LOG2E; g[j][4 * i + 1] = bg.y * -LOG2E;
-          g[j][4 * i + 2] = bg.z * -LOG2E; g[j][4 * i + 3] = bg.w * -LOG2E;
-          f[j][4 * i] = bl.x * (2.f * LOG2E); f[j][4 * i + 1] = bl.y * (2.f * LOG2E);
-          f[j][4 * i + 2] = bl.z * (2.f * LOG2E); f[j][4 * i + 3] = bl.w * (2.f * LOG2E);
+          g[j][4 * i] = bg.x; g[j][4 * i + 1] = bg.y; g[j][4 * i + 2] = bg.z; g[j][4 * i + 3] = bg.w;
+          f[j][4 * i] = bl.x; f[j][4 * i + 1] = bl.y; f[j][4 * i + 2] = bl.z; f[j][4 * i + 3] = bl.w;
         }
       }
 #pragma unroll
@@ -1447,15 +1496,15 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
       }
       // the next tile's DMA after layer 0's MFMAs (its XPN was read in this tile's prologue, its AS / BFL
       // buffer cur ^ 1 by the previous tile), ahead of the kernel-fragment loads
-      if (l == 0 && v + (int)gridDim.x < ntiles) {   // (the scalars' loads first: waiting for them is not
-        tile_scalars(v + gridDim.x, tq);               // waiting for the DMA)
-        dma(v + gridDim.x, cur ^ 1, wave, lane);
+      if (l == 0 && vnext < ntiles) {                 // (the scalars' loads first: waiting for them is not
+        tile_scalars(vnext, tq);                       // waiting for the DMA)
+        dma(vnext, cur ^ 1, wave, lane);
       }
       if (l + 1 < NLY) {
         kload(b, fpair, l + 1, lane);
-      } else if (v + (int)gridDim.x < ntiles) {            // the next tile's layer-0 fragments
+      } else if (vnext < ntiles) {                         // the next tile's layer-0 fragments
         int b2, bx2;
-        coords(v + gridDim.x, b2, bx2);
+        coords(vnext, b2, bx2);
         kload(b2, fpair_of(bx2 * TS - 64, wave), 0, lane);
       }
 #pragma unroll
