@@ -1349,30 +1349,34 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     }
     __syncthreads();
     PS_STAMP(3);
-    // x rows -> registers: z = x + a, a = first_conv(audio) (first_conv_kernel's order)
+    // x rows -> registers: z = x + a, a = first_conv(audio) in first_conv_kernel's order -- from the bias,
+    // taps ascending: taps 0..5 as three v_mfma_f32_32x32x2_f32 (exact f32, bitwise the fmaf chain; A = two
+    // taps' weights, B = the tile's audio rows shifted by those taps; D lands in the x registers' layout),
+    // tap 6 by fmaf.  (The VALU chain: 112 fmaf and 28 16-B LDS reads per lane and tile.)
     f32x2 xr[TPW][8], ar[TPW][8];
     const float* as = AS[cur];
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       const int k = 2 * wave + j, row = k * 32 + n, t = tg + row;
       const bool ok = row >= RLO && row < RHI && t >= 0 && t < Le;
+      f32x16 fa;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
-        if (ok) {
-          xv = *reinterpret_cast<const float4*>(&XS[row * LB_XLD + 8 * i + 4 * h]);
-          float a4[4];
+        const float4 bv = *reinterpret_cast<const float4*>(&FBL[8 * i + 4 * h]);
+        fa[4 * i] = bv.x; fa[4 * i + 1] = bv.y; fa[4 * i + 2] = bv.z; fa[4 * i + 3] = bv.w;
+      }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) a4[e] = FBL[8 * i + 4 * h + e];
+      for (int q = 0; q < 3; ++q)   // (every lane, masked rows too: row + 6 < NAS, staged finite samples)
+        fa = __builtin_amdgcn_mfma_f32_32x32x2f32(FW[(2 * q + h) * 32 + n], as[row + 2 * q + h], fa, 0, 0, 0);
+      const float s6 = as[row + 6];
 #pragma unroll
-          for (int tap = 0; tap < 7; ++tap) {
-            const float sv = as[row + tap];
-            const float4 w = *reinterpret_cast<const float4*>(&FW[tap * 32 + 8 * i + 4 * h]);
-            a4[0] = fmaf(w.x, sv, a4[0]); a4[1] = fmaf(w.y, sv, a4[1]);
-            a4[2] = fmaf(w.z, sv, a4[2]); a4[3] = fmaf(w.w, sv, a4[3]);
-          }
-          av = make_float4(a4[0], a4[1], a4[2], a4[3]);
-        }
+      for (int i = 0; i < 4; ++i) {
+        const float4 w = *reinterpret_cast<const float4*>(&FW[6 * 32 + 8 * i + 4 * h]);
+        float4 av = make_float4(fmaf(w.x, s6, fa[4 * i]), fmaf(w.y, s6, fa[4 * i + 1]),
+                                fmaf(w.z, s6, fa[4 * i + 2]), fmaf(w.w, s6, fa[4 * i + 3]));
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) xv = *reinterpret_cast<const float4*>(&XS[row * LB_XLD + 8 * i + 4 * h]);
+        else av = xv;
         xr[j][2 * i] = f32x2{xv.x + av.x, xv.y + av.y}; xr[j][2 * i + 1] = f32x2{xv.z + av.z, xv.w + av.w};
         ar[j][2 * i] = f32x2{av.x, av.y}; ar[j][2 * i + 1] = f32x2{av.z, av.w};
       }
