@@ -1500,6 +1500,7 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
       }
       // the next tile's DMA after layer 0's MFMAs (its XPN was read in this tile's prologue, its AS / BFL
       // buffer cur ^ 1 by the previous tile), ahead of the kernel-fragment loads
+      if (l == 0) PS_STAMP(18);
       if (l == 0 && vnext < ntiles) {                 // (the scalars' loads first: waiting for them is not
         tile_scalars(vnext, tq);                       // waiting for the DMA)
         dma(vnext, cur ^ 1, wave, lane);
@@ -1511,6 +1512,7 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
         coords(vnext, b2, bx2);
         kload(b2, fpair_of(bx2 * TS - 64, wave), 0, lane);
       }
+      if (l == 0) PS_STAMP(19);
 #pragma unroll
       for (int j = 0; j < TPW; ++j) {
 #pragma unroll

@@ -112,6 +112,14 @@ template <int TS, bool FINAL = false, bool PS = false> static void run(int hop) 
     const double L = med(life);
     printf("  %zu sampled waves, median tile time %.0f cycles\n", life.size(), L);
     for (int q = 1; q < 18; ++q) printf("    %-11s %8.0f cyc  %5.1f%%\n", names[q], med(ph[q]), 100.0 * med(ph[q]) / L);
+    // layer 0's LVC phase split by stamps 18 (after its MFMAs) and 19 (after the next tile's DMA / fragment loads)
+    std::vector<double> s0, s1, s2;
+    for (int w = 0; w < nsamp * G::NW; ++w) {
+      const unsigned long long* t = &tr[(size_t)w * NS];
+      if (t[0] == 0 || t[18] < t[6] || t[19] < t[18] || t[7] < t[19]) continue;
+      s0.push_back((double)(t[18] - t[6])); s1.push_back((double)(t[19] - t[18])); s2.push_back((double)(t[7] - t[19]));
+    }
+    printf("    L0 lvc = MFMAs %.0f + next tile's DMA / loads %.0f + gate %.0f cyc\n", med(s0), med(s1), med(s2));
     return;
   }
   const dim3 grid(cdiv(Lh, TS), B);
