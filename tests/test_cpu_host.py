@@ -258,3 +258,31 @@ def test_bench_tables_cover_every_dominant_tag():
     with pytest.raises(SystemExit):
         bench.dominant_kernel({"mystery": (1, 5.0), "wn_stack": (2, 1.0)}, fl, by)
     assert bench.dominant_kernel({"nsf_pair": (27, 5.0), "wn_stack": (2, 1.0)}, fl, by) == "nsf_pair"
+
+
+def test_collate_pad_stack_equals_per_item_pad():
+    """pipeline._pad_stack (the batch collate: one stack for equal lengths, one zero fill and a copy
+    per row otherwise) equals the per-item F.pad + stack it replaced, for float frames and integer
+    tokens, ragged and equal lengths."""
+    from prodiff_amd.pipeline import SvsSynthesizer, Synthesizer, _pad_stack
+
+    def ref(items):
+        n = max(int(v.shape[0]) for v in items)
+        pad = [(0, 0) * (v.dim() - 1) + (0, n - int(v.shape[0])) for v in items]
+        return torch.stack([torch.nn.functional.pad(v, p) for v, p in zip(items, pad)])
+
+    g = torch.Generator().manual_seed(3)
+    cases = [[torch.randn(t, 4, generator=g) for t in (5, 2, 4)],
+             [torch.randn(3, 4, generator=g) for _ in range(3)],
+             [torch.randint(0, 9, (t,), generator=g) for t in (4, 1, 4)],
+             [torch.randn(1, 2, generator=g)]]
+    for items in cases:
+        out = _pad_stack(items)
+        assert out.dtype == items[0].dtype
+        assert torch.equal(out, ref(items))
+    assert torch.equal(Synthesizer.collate(cases[0]), ref(cases[0]))
+    b = SvsSynthesizer.collate([{"txt_tokens": torch.arange(1, 4), "mel2ph": torch.ones(5, dtype=torch.long)},
+                                {"txt_tokens": torch.arange(1, 3), "mel2ph": torch.ones(2, dtype=torch.long)}])
+    assert b["ntok"] == [3, 2] and b["nframes"] == [5, 2]
+    assert b["txt_tokens"].tolist() == [[1, 2, 3], [1, 2, 0]]
+    assert b["mel2ph"].tolist() == [[1] * 5, [1, 1, 0, 0, 0]]
