@@ -492,33 +492,32 @@ def ref_cpu_baseline(config):
             "source": os.path.relpath(path, ROOT)}
 
 
-def port_cpu_baseline(frames, vocoder=True):
+def port_cpu_baseline(frames, batch=1, vocoder=True):
     """The torch-fp32 CPU restatement (oracle/oracle_torch.py, a port of the
-    reference math) timed on THIS host's cores on a bounded sample: one utterance
-    of `frames` mel frames through the same 2-iter ProDiff (+ 4-iter FastDiff)."""
+    reference math) timed on THIS host's cores on a bounded sample of the workload: `batch`
+    utterances of `frames` mel frames through the same 2-iter ProDiff (+ 4-iter FastDiff).
+    r06: by default the workload's own batch (C3: 8 x 861, ~8 s on the box's 16 cores), timed once
+    after a 200-frame warm-up (r05 timed one 200-frame utterance: 34x smaller than C3's batch)."""
     from oracle import oracle_torch as OT
     from prodiff_amd import synth
     threads = torch.get_num_threads()
     model = OT.PortModels(synth, seed=0)
-    cond = torch.from_numpy(synth.synth_inputs(0, (1, frames, 256)))
 
-    def run():
+    def run(b, t):
+        cond = torch.from_numpy(synth.synth_inputs(0, (b, t, 256)))
         mel = model.prodiff(cond, seed=1)
         if vocoder:
             model.fastdiff(mel, seed=2)
 
-    run()                                     # warm-up
-    ts = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        run()
-        ts.append(time.perf_counter() - t0)
-    dt = float(np.median(ts))
-    audio_s = frames * HOP / SAMPLE_RATE
-    return {"value": round(frames / dt, 2), "unit": "mel-frames/s", "cores": threads, "kind": "port",
-            "sample": f"torch fp32 CPU restatement (oracle/oracle_torch.py), 1 utterance x {frames} frames "
+    run(1, min(frames, 200))                  # warm-up (thread pool, allocator)
+    t0 = time.perf_counter()
+    run(batch, frames)
+    dt = time.perf_counter() - t0
+    audio_s = batch * frames * HOP / SAMPLE_RATE
+    return {"value": round(batch * frames / dt, 2), "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "sample": f"torch fp32 CPU restatement (oracle/oracle_torch.py), {batch} utterance(s) x {frames} frames "
                       f"({audio_s:.2f} s audio), 2-iter ProDiff" + (" + 4-iter FastDiff" if vocoder else "") +
-                      f", median of 3 after 1 warm-up: {dt:.2f} s",
+                      f", one timed run after a 200-frame warm-up: {dt:.2f} s",
             "rtf": round(dt / audio_s, 4)}
 
 
@@ -581,7 +580,9 @@ def main():
     ap.add_argument("--lengths", default="fixed", choices=["fixed", "ds"],
                     help="ds: the reference song's 30 segment lengths (and phoneme counts) per GPU "
                          "(tests/golden/ds_lengths.json, from samples/00_*.ds), run as ragged batches")
-    ap.add_argument("--cpu-frames", type=int, default=200, help="cpu_baseline_port sample length (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=-1,
+                    help="cpu_baseline_port sample: -1 = the workload's batch (at most 8 x 861 frames' worth), "
+                         "N > 0 = one utterance of N frames, 0 = skip")
     ap.add_argument("--overlap", type=int, default=None,
                     help="jobs in flight: step i runs on HIP stream i %% N, so consecutive jobs overlap "
                          "(default: 2 for C3 / C5 on one GPU, else 1)")
@@ -987,9 +988,12 @@ def main():
     }
     if rank == 0 and world == 1 and not dry:
         out_line["cpu_baseline"] = ref_cpu_baseline(cfg_name)
-        if args.cpu_frames > 0 and not svs and not pitch:
-            out_line["cpu_baseline_port"] = port_cpu_baseline(args.cpu_frames if cfg["vocoder"] else T,
-                                                              vocoder=cfg["vocoder"])
+        if args.cpu_frames != 0 and not svs and not pitch:
+            if args.cpu_frames > 0:
+                pb, pt = 1, args.cpu_frames
+            else:                                # the workload's own batch, bounded to C3's 6 888 frames
+                pb, pt = max(1, min(B, 8 * 861 // T)), T
+            out_line["cpu_baseline_port"] = port_cpu_baseline(pt, batch=pb, vocoder=cfg["vocoder"])
     if rank == 0:
         print(json.dumps(out_line), flush=True)
     if world > 1:
