@@ -2682,15 +2682,13 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
         const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
         const bool pf = m->lvc_pf && hop % 64 == 0;   // a 64-row tile pair shares one frame
         if (fuse_fin && pf && ts == 384 && m->lvc_tpw == 2 && m->lvc_ps && r == 4 && hop % 256 == 0) {
-          // r06: persistent, one block per CU (a multiple of 8 blocks keeps the XCD-aware tile order)
-          static int ncu = 0;
-          if (!ncu) {
-            int dev = 0;
-            PD_HIP(hipGetDevice(&dev));
-            PD_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-          }
+          // r06: persistent, one block per CU (a multiple of 8 blocks keeps the XCD-aware tile order;
+          // any grid size walks every tile once)
+          int dev = 0, ncu = 0;
+          PD_HIP(hipGetDevice(&dev));
+          PD_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
           const int ntx = (int)cdiv(Tout, 384), ntiles = ntx * nbk;
-          const int grid = ntiles <= ncu ? ntiles : ncu / 8 * 8;
+          const int grid = ntiles <= ncu ? ntiles : ncu >= 8 ? ncu / 8 * 8 : ncu;
           hipLaunchKernelGGL(lvc_final_ps_kernel, dim3(grid), dim3(512), 0, st, la, ntx, ntiles);
           PD_LAUNCH_CHECK();
         } else if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
