@@ -213,10 +213,10 @@ def bytes_per_launch(B, T, dtype, hops=(8, 64, 256), M=80, C=256, H=256, cyc=1):
 # the last template arguments (r04 added the tiles-per-wave argument).
 TAG_KERNEL = {
     # the default (two tiles per wave) instantiation first: a summary may hold both
-    # (r06: the persistent final block, FD_OPT_LVC_PS, is the default; the one-tile kernel with lvc_ps=0)
-    "fd_lvc_block_final": ("lvc_final_ps_kernel", "lvc_block_bf16_kernel<384, true, true, true, true, false, 2>",
+    # (r06: the persistent kernels, FD_OPT_LVC_PS, are the default; the one-tile kernel with lvc_ps=0)
+    "fd_lvc_block_final": ("lvc_ps_kernel<true>", "lvc_final_ps_kernel", "lvc_block_bf16_kernel<384, true, true, true, true, false, 2>",
                            "lvc_block_bf16_kernel<384, true, true, true, true, false,"),
-    "fd_lvc_block_ups": ("lvc_block_bf16_kernel<384, true, false, false, true, false, 2>",
+    "fd_lvc_block_ups": ("lvc_ps_kernel<false>", "lvc_block_bf16_kernel<384, true, false, false, true, false, 2>",
                          "lvc_block_bf16_kernel<384, true, false, false, true, false,"),
     "fd_lvc_block_sub": ("lvc_block_bf16_kernel<256, true, false, false, false, true,",
                          "lvc_block_bf16_kernel<128, true, false, false, false, true,"),

@@ -1136,24 +1136,28 @@ __device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
   do {              \
   } while (0)
 #endif
-__global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs P, int ntx, int ntiles) {
+// FINAL = the sampler's last block (upsample r = 4, first conv, final conv + sampler update; hop 256); !FINAL
+// (r06) = the hop-64 block (upsample r = 8, audio_down from HBM, x out), the one-tile kernel's <384, UPS, PF>.
+template <bool FINAL>
+__global__ __launch_bounds__(512, 1) void lvc_ps_kernel(const LvcBlockArgs P, int ntx, int ntiles) {
   constexpr int TS = 384, TPW = 2;
   using G = LbGeo<TS, TPW>;
-  constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF, GR = NG * 32, EX = 3, NT = G::NT;
-  constexpr int BFR = GR / 256 + 2;                    // frames a tile touches at hop 256 (host-checked)
-  constexpr int XROWS = G::NTJ_MAX * 32 + 1, XROWS8 = (XROWS + 7) / 8 * 8;   // x_prev rows (r = 4: 161)
+  constexpr int NW = G::NW, NG = G::NG, UOFF = G::UOFF, GR = NG * 32, EX = FINAL ? 3 : 0, NT = G::NT;
+  constexpr int BFR = GR / (FINAL ? 256 : 64) + 2;      // frames a tile touches at hop 256 / 64 (host-checked)
+  constexpr int XROWS = G::NTJ_MAX * 32 + 1, XROWS8 = (XROWS + 7) / 8 * 8;   // x_prev rows (r >= 4: <= 161)
   constexpr int NAS = GR + 6, NAS64 = (NAS + 63) / 64 * 64;                  // audio samples of a tile
+  constexpr int FA = FINAL ? 1 : 0;                     // (the audio / first / final conv arrays: FINAL only)
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
-  __shared__ __attribute__((aligned(16))) float AS[2][NAS64];                // audio, times tg - 3 + i (raw)
+  __shared__ __attribute__((aligned(16))) float AS[2][FINAL ? NAS64 : 4];   // audio, times tg - 3 + i (raw)
   __shared__ __attribute__((aligned(16))) float XPN[XROWS8 * CI];           // x_prev rows jb + rr (raw)
   __shared__ __attribute__((aligned(16))) float BFL[2][BFR * 2 * CI * NLY]; // frames' LVC biases (pre-scaled)
-  __shared__ __attribute__((aligned(16))) float FW[7 * 32];
-  __shared__ __attribute__((aligned(16))) float FWF[7 * 32];
-  __shared__ __attribute__((aligned(16))) float FBL[32];
+  __shared__ __attribute__((aligned(16))) float FW[FA ? 7 * 32 : 4];
+  __shared__ __attribute__((aligned(16))) float FWF[FA ? 7 * 32 : 4];
+  __shared__ __attribute__((aligned(16))) float FBL[FA ? 32 : 4];
   __shared__ __attribute__((aligned(16))) float BUL[32];
   __shared__ __attribute__((aligned(16))) bf16x8 WCL[NLY * 6 * 64];
   __shared__ __attribute__((aligned(16))) float BCL[NLY * CI];
-  __shared__ float EB[8][2][3][8];                                           // FIN: pairs' outer E rows
+  __shared__ float EB[FA ? 8 : 1][2][3][8];                                  // FIN: pairs' outer E rows
   __bf16* U = reinterpret_cast<__bf16*>(smem);
   __bf16* Y = U + G::UROWS * LB_LD;
   float* XS = reinterpret_cast<float*>(smem);
@@ -1164,10 +1168,12 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
   const int ntj = (GR / r + 2 + 31) / 32;
   constexpr int RLO = 64 - 44 - EX, RHI = 64 + TS + 44 + EX;
   // ---- tile-invariant operands, once per block
-  if (tid < 224) FW[tid] = P.fw[(tid & 31) * 7 + (tid >> 5)];
-  if (tid < 32) FBL[tid] = P.fb[tid];
+  if constexpr (FINAL) {
+    if (tid < 224) FW[tid] = P.fw[(tid & 31) * 7 + (tid >> 5)];
+    if (tid < 32) FBL[tid] = P.fb[tid];
+    if (tid < 224) FWF[tid] = P.wfin[tid];
+  }
   if (tid < 32) BUL[tid] = P.bup[tid];
-  if (tid < 224) FWF[tid] = P.wfin[tid];
   if (tid < 6 * 64) {
     const int kk = tid >> 6, ln = tid & 63;
 #pragma unroll
@@ -1178,7 +1184,7 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     }
   }
   if (tid < NLY * CI) BCL[tid] = P.bc[tid / CI][tid % CI];
-  const float bfin = P.bfin[0];
+  const float bfin = FINAL ? P.bfin[0] : 0.f;
   // tile v -> (utterance, time tile): the one-tile kernel's XCD-aware order (gridDim.x % 8 == 0, so tile v
   // runs on the XCD of block v % gridDim.x, as block v did there)
   auto coords = [&](int v, int& b, int& bx) {
@@ -1193,12 +1199,14 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     coords(v, b, bx);
     const int tg = bx * TS - 64, jb = floordiv(tg + pp, r) - 2, fbase = (tg > 0 ? tg : 0) / hop;
     const long long base = (long long)b * Lh;
+    if constexpr (FINAL) {
 #pragma unroll
-    for (int q0 = 0; q0 < NAS64 / 64; q0 += NW) {          // 4-B pieces, one sample per lane
-      const int q = q0 + wave;
-      if (q * 64 < NAS) {
-        const int t = tg - 3 + q * 64 + lane;
-        lds_dma4(P.audio + base + min(max(t, 0), Lh - 1), &AS[s][q * 64]);
+      for (int q0 = 0; q0 < NAS64 / 64; q0 += NW) {        // 4-B pieces, one sample per lane
+        const int q = q0 + wave;
+        if (q * 64 < NAS) {
+          const int t = tg - 3 + q * 64 + lane;
+          lds_dma4(P.audio + base + min(max(t, 0), Lh - 1), &AS[s][q * 64]);
+        }
       }
     }
 #pragma unroll
@@ -1209,9 +1217,13 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
         lds_dma16(P.xin + ((long long)b * Tin + j) * CI + (lane & 7) * 4, &XPN[q * 8 * CI]);
       }
     }
-    if (wave < BFR) {                                       // one frame (256 floats) per wave
-      const int fr = min(fbase + wave, Tc - 1);
-      lds_dma16(P.Bf + ((long long)b * Tc + fr) * (2 * CI * NLY) + lane * 4, &BFL[s][wave * 2 * CI * NLY]);
+#pragma unroll
+    for (int f0 = 0; f0 < BFR; f0 += NW) {                  // one frame (256 floats) per wave and piece
+      const int fq = f0 + wave;
+      if (fq < BFR) {
+        const int fr = min(fbase + fq, Tc - 1);
+        lds_dma16(P.Bf + ((long long)b * Tc + fr) * (2 * CI * NLY) + lane * 4, &BFL[s][fq * 2 * CI * NLY]);
+      }
     }
   };
   bf16x8 kn[12];
@@ -1232,8 +1244,10 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     int b, bx;
     coords(v, b, bx);
     lv_n = *(P.lens ? P.lens + b : reinterpret_cast<const int*>(P.Bf));
-    uv_n = *(P.uid ? P.uid + b + P.b_off : reinterpret_cast<const int*>(P.Bf));
-    zn_n = (P.noise ? P.noise : P.audio)[(long long)b * Lh + min(max(bx * TS + tq - 64, 0), Lh - 1)];
+    if constexpr (FINAL) {
+      uv_n = *(P.uid ? P.uid + b + P.b_off : reinterpret_cast<const int*>(P.Bf));
+      zn_n = (P.noise ? P.noise : P.audio)[(long long)b * Lh + min(max(bx * TS + tq - 64, 0), Lh - 1)];
+    }
   };
   const int v0 = blockIdx.x;
   __syncthreads();                                         // the invariant operands are staged
@@ -1262,7 +1276,7 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     int b, bx;
     coords(v, b, bx);
     const int Le = P.lens ? min(__builtin_amdgcn_readfirstlane(lv_n), Tc) * hop : Lh;
-    const unsigned uidv = P.uid ? (unsigned)__builtin_amdgcn_readfirstlane(uv_n) : (unsigned)(b + P.b_off);
+    const unsigned uidv = !FINAL ? 0u : P.uid ? (unsigned)__builtin_amdgcn_readfirstlane(uv_n) : (unsigned)(b + P.b_off);
     const int t0 = bx * TS, tg = t0 - 64;
     const long long base = (long long)b * Lh;
     const int Tin_e = Le / r;
@@ -1270,8 +1284,10 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     const int jb = floordiv(tg + pp, r) - 2;
     const int fpair = fpair_of(tg, wave);
     // this tile's DMA (issued a tile ago) has landed for every wave: each waits for its own pieces -- the
-    // 12 younger kernel-fragment loads (and at most one audio_out store) may stay in flight -- then a barrier
-    __builtin_amdgcn_s_waitcnt(0x0F7C);                    // vmcnt(12)
+    // 12 younger kernel-fragment loads (and at most one audio_out store; !FINAL: 8 x stores) may stay in
+    // flight -- then a barrier
+    constexpr int VMY = FINAL ? 12 : 20;
+    __builtin_amdgcn_s_waitcnt((VMY & 15) | ((VMY >> 4) << 14) | 0x0F70);   // vmcnt(VMY)
     __syncthreads();
     PS_STAMP(1);
     // phase-GEMM weights (NW % r == 0: wave w computes phase w % r), FIN noise
@@ -1281,19 +1297,34 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) wfj[kk] = *reinterpret_cast<const bf16x8*>(wa + kk * 16);
     }
+    // !FINAL: the tile's audio_down rows (x += a, modules.py:209) straight into registers, loaded here so
+    // their HBM round trip runs under the XP fill and the phase GEMMs (unconditional at clamped rows,
+    // masked where they are used)
+    float4 araw[TPW][4];
+    if constexpr (!FINAL) {
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const int t = min(max(tg + (2 * wave + j) * 32 + n, 0), Lh - 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) araw[j][i] = *reinterpret_cast<const float4*>(P.a + (base + t) * CI + 8 * i + 4 * h);
+      }
+    }
     // (the explicit draw loaded a tile ahead, unconditionally: under `P.noise ?` the waitcnt pass waited for
     // every outstanding load -- the next tile's kernel fragments included -- at the join)
     const float znz = zn_n;
     // (thread tq writes sample s = tq - 64: lane (n, h) of wave w holds row 64 w + 32 h + n of the window)
     const int so = tq - 64;
-    const float zph = philox_normal_u(P.seed, uidv, (unsigned)(t0 + so), P.stream);
-    const float zr = (so >= 0 && so < TS && t0 + so < Lh && P.sig != 0.f) ? (P.noise ? znz : zph) : 0.f;
-    // audio samples outside the utterance -> 0 in place (the one-tile kernel's masked staging: the DMA
-    // lands raw values; only the out-of-range ones are rewritten, so no LDS read)
+    float zr = 0.f;
+    if constexpr (FINAL) {
+      const float zph = philox_normal_u(P.seed, uidv, (unsigned)(t0 + so), P.stream);
+      zr = (so >= 0 && so < TS && t0 + so < Lh && P.sig != 0.f) ? (P.noise ? znz : zph) : 0.f;
+      // audio samples outside the utterance -> 0 in place (the one-tile kernel's masked staging: the DMA
+      // lands raw values; only the out-of-range ones are rewritten, so no LDS read)
 #pragma unroll
-    for (int ia = 0; ia < NAS64 / NT + 1; ++ia) {
-      const int i = tq + ia * NT, t = tg - 3 + i;
-      if (i < NAS && (t < 0 || t >= Le)) AS[cur][i] = 0.f;
+      for (int ia = 0; ia < NAS64 / NT + 1; ++ia) {
+        const int i = tq + ia * NT, t = tg - 3 + i;
+        if (i < NAS && (t < 0 || t >= Le)) AS[cur][i] = 0.f;
+      }
     }
     // the frames' LVC biases: the gate pre-scale the one-tile kernel applies at staging, once per tile in
     // place (read from the LVC phases on, past the barriers below)
@@ -1359,6 +1390,18 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
     for (int j = 0; j < TPW; ++j) {
       const int k = 2 * wave + j, row = k * 32 + n, t = tg + row;
       const bool ok = row >= RLO && row < RHI && t >= 0 && t < Le;
+      if constexpr (!FINAL) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), av = xv;
+          if (ok) {
+            xv = *reinterpret_cast<const float4*>(&XS[row * LB_XLD + 8 * i + 4 * h]);
+            av = araw[j][i];
+          }
+          xr[j][2 * i] = f32x2{xv.x + av.x, xv.y + av.y}; xr[j][2 * i + 1] = f32x2{xv.z + av.z, xv.w + av.w};
+          ar[j][2 * i] = f32x2{av.x, av.y}; ar[j][2 * i + 1] = f32x2{av.z, av.w};
+        }
+      } else {
       f32x16 fa;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1379,6 +1422,7 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
         else av = xv;
         xr[j][2 * i] = f32x2{xv.x + av.x, xv.y + av.y}; xr[j][2 * i + 1] = f32x2{xv.z + av.z, xv.w + av.w};
         ar[j][2 * i] = f32x2{av.x, av.y}; ar[j][2 * i + 1] = f32x2{av.z, av.w};
+      }
       }
     }
     __syncthreads();                                       // XS reads done before U / Y (aliased) are written
@@ -1530,6 +1574,21 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
       PS_STAMP(7 + 3 * l);
     }
     if (P.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(0);
+    if constexpr (!FINAL) {
+      // centre tiles [2, 2 + TS/32) -> x out (plain stores: they stay in flight into the next tile, whose
+      // top waits for at most 20 younger operations -- these 8 and the 12 kernel-fragment loads)
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const int k = 2 * wave + j, t = tg + k * 32 + n;
+        if (k >= 2 && k < 2 + TS / 32 && t < Lh) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<float4*>(P.xout + (base + t) * CI + 8 * i + 4 * h) =
+                make_float4(xr[j][2 * i].x, xr[j][2 * i].y, xr[j][2 * i + 1].x, xr[j][2 * i + 1].y);
+        }
+      }
+      PS_STAMP(17);
+    } else {
     // FIN: eps(t) = b + sum_tap E[t + tap - 3][tap], then the sampler update (util.py:222-226).  E stays in
     // registers: lane (n, h) of wave w holds E of its pair's rows n (tile 2w) and 32 + n (tile 2w + 1) after the
     // halves' partial sums meet, so the row shifts t + tap - 3 are lane permutes (ds_bpermute) within the
@@ -1587,6 +1646,7 @@ __global__ __launch_bounds__(512, 1) void lvc_final_ps_kernel(const LvcBlockArgs
       }
     }
     PS_STAMP(17);
+    }
   }
 }
 #undef PS_STAMP
@@ -2681,15 +2741,21 @@ int fd_net(const fd_model* m, float* ws, const FdWs& W, const float* xa, const f
                                                                                    : "fd_lvc_block", st);
         const int ts = hop < 32 ? m->lvc_ts_sub : m->lvc_ts;
         const bool pf = m->lvc_pf && hop % 64 == 0;   // a 64-row tile pair shares one frame
-        if (fuse_fin && pf && ts == 384 && m->lvc_tpw == 2 && m->lvc_ps && r == 4 && hop % 256 == 0) {
-          // r06: persistent, one block per CU (a multiple of 8 blocks keeps the XCD-aware tile order;
-          // any grid size walks every tile once)
+        // r06: the persistent kernel -- the final block (upsample r = 4, hop 256) and the hop-64 block
+        // (upsample r = 8, audio_down from HBM): the phase GEMMs one phase per wave (NW % r == 0), the
+        // frames' biases staged for hop >= 256 / 64
+        const bool ps_fin = fuse_fin && r == 4 && hop % 256 == 0;
+        const bool ps_ups = ups && !fuse_fin && !(last && aud) && la.a && r == 8 && hop % 64 == 0;
+        if (pf && ts == 384 && m->lvc_tpw == 2 && m->lvc_ps && (ps_fin || ps_ups)) {
+          // one block per CU (a multiple of 8 blocks keeps the XCD-aware tile order; any grid size walks
+          // every tile once)
           int dev = 0, ncu = 0;
           PD_HIP(hipGetDevice(&dev));
           PD_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
           const int ntx = (int)cdiv(Tout, 384), ntiles = ntx * nbk;
           const int grid = ntiles <= ncu ? ntiles : ncu >= 8 ? ncu / 8 * 8 : ncu;
-          hipLaunchKernelGGL(lvc_final_ps_kernel, dim3(grid), dim3(512), 0, st, la, ntx, ntiles);
+          if (ps_fin) hipLaunchKernelGGL(lvc_ps_kernel<true>, dim3(grid), dim3(512), 0, st, la, ntx, ntiles);
+          else hipLaunchKernelGGL(lvc_ps_kernel<false>, dim3(grid), dim3(512), 0, st, la, ntx, ntiles);
           PD_LAUNCH_CHECK();
         } else if (ts == 256) PD_TRY(launch_lvc_block_ts<256>(la, ups, last && aud, fuse_fin, pf, Tout, nbk, st));
         else if (ts == 384 && m->lvc_tpw == 1 && hop >= 32 && ups && (last && aud) == fuse_fin)

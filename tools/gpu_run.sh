@@ -28,7 +28,7 @@ regex() {        # config -> kernels the PMC passes cover
   case $1 in
     C5*) echo "nsf_pair_kernel|nsf_wconv|nsf_ups_kernel|wn_stack_bf16" ;;
     PITCH) echo "wn_stack_bf16|wn_xa|matvec" ;;
-    *) echo "lvc_block_bf16_kernel|lvc_final_ps_kernel|kp_kernel_bf16|wn_stack_bf16|kp_hidden_bf16|dblock_bf16" ;;
+    *) echo "lvc_block_bf16_kernel|lvc_ps_kernel|kp_kernel_bf16|wn_stack_bf16|kp_hidden_bf16|dblock_bf16" ;;
   esac
 }
 

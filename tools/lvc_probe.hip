@@ -80,10 +80,10 @@ template <int TS, bool FINAL = false, bool PS = false> static void run(int hop) 
     CK(hipMemset(la.trace, 0, (size_t)nsamp * G::NW * NS * 8));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(lvc_final_ps_kernel, dim3(nblk), dim3(512), 0, 0, la, ntx, ntiles);
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(lvc_ps_kernel<true>, dim3(nblk), dim3(512), 0, 0, la, ntx, ntiles);
     const int reps = 20;
     CK(hipEventRecord(e0));
-    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(lvc_final_ps_kernel, dim3(nblk), dim3(512), 0, 0, la, ntx, ntiles);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(lvc_ps_kernel<true>, dim3(nblk), dim3(512), 0, 0, la, ntx, ntiles);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;
