@@ -386,10 +386,11 @@ def test_pitch_reflow_stack_bitexact(algo, ragged):
                                               (4, 100, None, "philox"), (8, 200, [200, 150, 199, 3, 200, 120, 77, 200],
                                                                           "philox")])
 def test_fastdiff_lvc_persistent_bitexact(B, Tc, lens, draws):
-    """FD_OPT_LVC_PS (r06: the final LVC block as a persistent kernel, one block per CU walking the tiles,
-    the next tile's audio / x_prev / biases by LDS-DMA under the current tile's layers) against the
-    one-tile-per-block kernel: the 4-step sample bit for bit -- one tile, ragged rows, and grids of 268 and
-    1 072 tiles (several per block), explicit and on-device draws."""
+    """FD_OPT_LVC_PS (r06: the final and the hop-64 LVC blocks as persistent kernels, one block per CU
+    walking the tiles, the next tile's audio / x_prev / biases by LDS-DMA under the current tile's layers)
+    against the one-tile-per-block kernels: the 4-step sample bit for bit -- one tile, ragged rows, and grids
+    of 268 and 1 072 final-block tiles (several per block; 4x as many hop-64 tiles), explicit and on-device
+    draws."""
     from prodiff_amd.schedules import fastdiff_infer_params, fastdiff_reverse_schedule, fastdiff_train_alpha
     from prodiff_amd import _lib
     p = G.fastdiff_params(31)
